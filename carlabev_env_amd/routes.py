@@ -1,0 +1,122 @@
+"""Reset-time route preparation on the host (NumPy/SciPy).
+
+Scene construction stays on the host (`src/managers/` is out of
+scope for the device path). What the device needs from a reset is the
+realised controller state, so the packer runs the reference's reset-time
+arithmetic here, with the same libraries the reference uses:
+
+  smooth_and_compute     src/control/utils.py:200-269 (scipy savgol_filter)
+  Controller.set_route   src/control/stanley_controller.py:34-49 (±1 px jitter)
+  calc_target_index      src/control/stanley_controller.py:100-123
+  stanley_control        src/control/stanley_controller.py:64-89
+"""
+from __future__ import annotations
+
+import numpy as np
+from scipy.signal import savgol_filter
+
+L_WHEELBASE = 2.9
+K_GAIN = 2.0
+MAX_STEER = np.radians(30.0)
+
+
+def smooth_and_compute(ax, ay, window: int = 9, poly: int = 3):
+    ax = np.asarray(ax, dtype=float)
+    ay = np.asarray(ay, dtype=float)
+    if ax.size != ay.size:
+        raise ValueError("ax and ay must have same length")
+    d = np.hypot(np.diff(ax), np.diff(ay))
+    keep = np.concatenate(([True], d > 1e-9))
+    ax, ay = ax[keep], ay[keep]
+    if len(ax) < 2:
+        x0, y0 = ax[0], ay[0]
+        ax = np.array([x0, x0 + 1e-3])
+        ay = np.array([y0, y0])
+    if window % 2 == 0:
+        window += 1
+    if window > len(ax):
+        window = len(ax) if len(ax) % 2 == 1 else len(ax) - 1
+    if window < 3:
+        window = 3
+    poly = min(poly, window - 1)
+    if len(ax) >= window:
+        cx = savgol_filter(ax, window_length=window, polyorder=poly)
+        cy = savgol_filter(ay, window_length=window, polyorder=poly)
+    else:
+        cx, cy = ax.copy(), ay.copy()
+    seg = np.hypot(np.diff(cx), np.diff(cy))
+    s = np.concatenate(([0.0], np.cumsum(seg)))
+    if s[-1] <= 1e-9:
+        z = np.zeros_like(cx)
+        return cx, cy, z.copy(), z.copy(), s
+    dx_ds = np.gradient(cx, s)
+    dy_ds = np.gradient(cy, s)
+    cyaw = np.unwrap(np.arctan2(dy_ds, dx_ds))
+    d2x = np.gradient(dx_ds, s)
+    d2y = np.gradient(dy_ds, s)
+    denom = dx_ds ** 2 + dy_ds ** 2
+    small = denom < 1e-9
+    denom_safe = np.where(small, 1.0, denom)
+    ck = (dx_ds * d2y - dy_ds * d2x) / (denom_safe ** 1.5)
+    ck[small] = 0.0
+    return cx, cy, cyaw, ck, s
+
+
+def angle_mod(x):
+    return ((np.asarray(x, dtype=float).flatten() + np.pi) % (2 * np.pi) - np.pi).item()
+
+
+def calc_target_index(x, y, yaw, cx, cy):
+    fx = x + L_WHEELBASE * np.cos(yaw)
+    fy = y + L_WHEELBASE * np.sin(yaw)
+    dx = [fx - icx for icx in cx]
+    dy = [fy - icy for icy in cy]
+    d = np.hypot(dx, dy)
+    idx = int(np.argmin(d))
+    fav = [-np.cos(yaw + np.pi / 2), -np.sin(yaw + np.pi / 2)]
+    err = np.dot([dx[idx], dy[idx]], fav)
+    return idx, err
+
+
+def stanley_target(x, y, yaw, v, cx, cy, cyaw, target_idx):
+    cur, err = calc_target_index(x, y, yaw, cx, cy)
+    if target_idx >= cur:
+        cur = target_idx
+    return cur
+
+
+class ControllerInit:
+    """Realised controller state after `Controller.set_route` (+ hero's initial
+    stanley_control, hero.py:83-86)."""
+
+    __slots__ = ("x", "y", "yaw", "v", "cx", "cy", "cyaw", "target_idx")
+
+    def __init__(self, ax, ay, v0: float, *, jitter_start: bool = True, np_rng=None, yaw0: float = 0.0,
+                 hero: bool = False):
+        cx, cy, cyaw, _, _ = smooth_and_compute(ax, ay, window=11, poly=3)
+        if jitter_start:
+            if np_rng is None:
+                np_rng = np.random.default_rng()
+            x = cx[0] + int(np_rng.integers(-1, 2))
+            y = cy[0] + int(np_rng.integers(-1, 2))
+        else:
+            x, y = cx[0], cy[0]
+        # State.__init__ leaves yaw = 0.0 until set_route assigns it
+        tidx, _ = calc_target_index(x, y, yaw0, cx, cy)
+        yaw = cyaw[tidx]
+        if hero:
+            tidx = stanley_target(x, y, yaw, v0, cx, cy, cyaw, tidx)
+        self.x, self.y, self.yaw, self.v = float(x), float(y), float(yaw), float(v0)
+        self.cx, self.cy, self.cyaw = cx, cy, cyaw
+        self.target_idx = int(tidx)
+
+
+def cumulative_lengths_int(rx, ry):
+    """CaRL cumulative route lengths over the int32 raw route (carl_reward_fn.py:20-26)."""
+    route = list(zip(np.asarray(rx, np.int32), np.asarray(ry, np.int32)))
+    lengths = [0.0]
+    for i in range(1, len(route)):
+        dx = route[i][0] - route[i - 1][0]
+        dy = route[i][1] - route[i - 1][1]
+        lengths.append(lengths[-1] + np.hypot(dx, dy))
+    return np.asarray(lengths, dtype=np.float64)
