@@ -1,0 +1,252 @@
+"""Benchmark: env-steps/sec of the batched CarlaBEV step on MI355X.
+
+Workload (BASELINE.json configs; default = configs[1], the metric's config):
+  --config 2  4096 envs/GPU, 128x128 semantic obs, ego-only (rt_no_traffic_v1),
+              discrete9, scene_seed = 10000 + global_env_id, actions default_rng(1234 + env_id)
+  --config 3  4096 envs/GPU, bev_rgb (grayscale 4-stack), rt_hard_v1 traffic, actions default_rng(7 + id)
+  --config 4  8192 envs/GPU, semantic, continuous, rt_medium_v1, RCCL gather of frames to rank 0 every step
+  --config 5  2048 envs/GPU, 256x256 semantic, lead_brake/jaywalk/red_light_runner mix, comfort export
+
+One timed "step" = `step()` for every env (ego + actors + raster + collision/reward
++ termination) followed by the reference's canonical loop reset of the envs that
+terminated (reset_mask = terminated | truncated, served on the device from a
+pre-built scene bank). Inputs are resident in HBM before the timed region.
+`value` = env-steps/s summed over ranks (weak scaling: envs per GPU fixed).
+The wire-format observation (float32 one-hot 4-stack / gray stack) is timed
+in a second pass and reported as `with_wire_obs`.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+CONFIGS = {
+    2: dict(envs=4096, size=128, obs_mode="bev_semantic", difficulty="rt_no_traffic_v1", action="discrete9_v1",
+            seed0=10_000, act_seed=1234, caps=dict(route_cap=64, actor_cap=0, actor_route_cap=2, tl_cap=0),
+            workload="ego-only empty scene (rt_no_traffic_v1), 4096 envs/GPU, 128x128 semantic 6-class"),
+    3: dict(envs=4096, size=128, obs_mode="bev_rgb", difficulty="rt_hard_v1", action="discrete9_v1",
+            seed0=20_000, act_seed=7, caps=dict(route_cap=64, actor_cap=25, actor_route_cap=64, tl_cap=0),
+            workload="random traffic (rt_hard_v1, 25 vehicles), 4096 envs/GPU, 128x128 RGB->gray 4-stack"),
+    4: dict(envs=8192, size=128, obs_mode="bev_semantic", difficulty="rt_medium_v1", action="continuous_gsb_v1",
+            seed0=40_000, act_seed=99, caps=dict(route_cap=64, actor_cap=16, actor_route_cap=64, tl_cap=0),
+            gather=True, workload="rt_medium_v1, continuous, 8192 envs/GPU, RCCL frame gather to rank 0"),
+    5: dict(envs=2048, size=256, obs_mode="bev_semantic", difficulty="mix3", action="discrete9_v1",
+            seed0=30_000, act_seed=1234, caps=dict(route_cap=64, actor_cap=4, actor_route_cap=64, tl_cap=4),
+            workload="lead_brake/jaywalk/red_light_runner mix, 2048 envs/GPU, 256x256 semantic, comfort export"),
+}
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip-level parameters (spec)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def scene_options(cfgd, env_id):
+    from carlabev_env_amd.config import RandomNavigationReset, build_random_navigation_options
+    if cfgd["difficulty"] == "mix3":
+        return {"scene": ("lead_brake", "jaywalk", "red_light_runner")[env_id % 3]}
+    return build_random_navigation_options(RandomNavigationReset(difficulty_id=cfgd["difficulty"]))
+
+
+def make_actions(P, n, steps, seed0, offset):
+    out = np.zeros((steps, n), np.int32) if P.action_kind == 0 else np.zeros((steps, n, 3), np.float32)
+    for e in range(n):
+        rng = np.random.default_rng(seed0 + offset + e)
+        if P.action_kind == 0:
+            out[:, e] = rng.integers(0, P.n_discrete, size=steps)
+        else:
+            out[:, e] = rng.uniform([0, -1, 0], [1, 1, 1], size=(steps, 3)).astype(np.float32)
+    return out
+
+
+def build_env(cfgd, n, rank, device):
+    """Vector env with every env reset to its seeded scene (host scene-gen)."""
+    from carlabev_env_amd.config import EnvConfig
+    from carlabev_env_amd.host_reset import HostResetBuilder
+    from carlabev_env_amd.vector_env import CarlaBEVVectorEnv
+    import torch
+    S = cfgd["size"]
+    action_mode = "continuous" if cfgd["action"].startswith("continuous") else "discrete"
+    cfg = EnvConfig(size=S, obs_size=(S, S), obs_mode=cfgd["obs_mode"], render_mode="rgb_array",
+                    action_mode=action_mode, action_profile_id=cfgd["action"])
+    env = CarlaBEVVectorEnv({"env": cfg, "num_envs": n}, device=device, caps=cfgd["caps"], info_mode="none")
+    first = rank * n
+    t0 = time.time()
+    host = np.zeros((n, env.rb), np.uint8)
+    for i in range(n):
+        gid = first + i
+        opts = dict(scene_options(cfgd, gid), scene_seed=cfgd["seed0"] + gid)
+        env.builder.build(host[i], None, opts)
+    recs = torch.from_numpy(host).to(device)
+    # bank of further seeded scenes for the canonical reset-on-termination loop
+    nb = min(n, 512)
+    bank = np.zeros((nb, env.rb), np.uint8)
+    for i in range(nb):
+        gid = 1_000_000 + first + i
+        env.builder.build(bank[i], None, dict(scene_options(cfgd, gid), scene_seed=cfgd["seed0"] + gid))
+    log(f"[rank {rank}] built {n} scenes + {nb} bank scenes in {time.time() - t0:.1f}s")
+    env.attach_bank(torch.from_numpy(bank).to(device))
+    # initial reset: records = seeded scenes, reset observation rendered on device
+    env.attach_bank(recs)
+    env.reset_from_bank(mask=None, bank_idx=torch.arange(n, dtype=torch.int32, device=device))
+    env.attach_bank(torch.from_numpy(bank).to(device))
+    return env, host
+
+
+def cpu_baseline(cfgd, host_recs, env, seconds):
+    """Reference-semantics CPU oracle (single thread) on a bounded sample of the
+    same workload: first 64 envs, same scenes and action streams."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle as O
+    P = env.params
+    n = min(64, host_recs.shape[0])
+    recs = host_recs[:n].copy()
+    orc = O.Oracle(P, env.map_host, env.caps.c(), env.rb)
+    frames = np.zeros((n, P.size, P.size), np.uint8)
+    acts = make_actions(P, n, 4000, cfgd["act_seed"], 0)
+    steps = 0
+    t0 = time.perf_counter()
+    t = 0
+    while time.perf_counter() - t0 < seconds and t < acts.shape[0]:
+        orc.step(recs, n, np.ascontiguousarray(acts[t]), frames)
+        steps += n
+        t += 1
+    dt = time.perf_counter() - t0
+    return {"value": steps / dt, "unit": "env-steps/s", "cores": 1, "kind": "port",
+            "sample": f"{n} envs x {t} steps of the same workload ({steps} env-steps, {dt:.1f}s), "
+                      "oracle/cbev_oracle.c single thread, per-step full padded-map restore as in scene.py:93"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS))
+    ap.add_argument("--envs", type=int, default=None, help="envs per GPU (default: the config's)")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-wire", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    device = torch.device("cuda", local)
+    torch.cuda.set_device(device)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=device)
+    cfgd = CONFIGS[args.config]
+    n = args.envs or cfgd["envs"]
+    from carlabev_env_amd._lib import check, lib
+    env, host_recs = build_env(cfgd, n, rank, device)
+    P = env.params
+    total_steps = args.warmup + args.steps
+    acts = torch.from_numpy(make_actions(P, n, total_steps, cfgd["act_seed"], rank * n)).to(device)
+    gather = cfgd.get("gather", False) and world > 1
+    gbuf = [torch.empty_like(env.frames()) for _ in range(world)] if gather and rank == 0 else None
+
+    def one_step(t, wire):
+        env.step_async_only(acts[t])
+        if wire:
+            env._obs()
+        if gather:
+            dist.gather(env.frames(), gbuf, dst=0)
+        env.reset_from_bank(mask=env.term)
+
+    def timed(wire, profile):
+        for t in range(args.warmup):
+            one_step(t, wire)
+        if profile:
+            check(lib().cbev_profile(env._ctx, 1), "profile")
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        for t in range(args.warmup, total_steps):
+            one_step(t, wire)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        if world > 1:
+            tt = torch.tensor([el], dtype=torch.float64, device=device)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            el = float(tt.item())
+        ms3 = None
+        if profile:
+            buf = (ctypes.c_double * 3)()
+            cnt = ctypes.c_int64()
+            check(lib().cbev_profile_read(env._ctx, buf, ctypes.byref(cnt)), "profile_read")
+            check(lib().cbev_profile(env._ctx, 0), "profile")
+            ms3 = [buf[i] / max(cnt.value, 1) for i in range(3)]
+        return el, ms3
+
+    el, ms3 = timed(False, True)
+    value = world * n * args.steps / el
+    wire_value = None
+    if not args.no_wire:
+        # re-seed the state so the second pass replays a comparable workload
+        env.attach_bank(torch.from_numpy(host_recs).to(device))
+        env.reset_from_bank(mask=None, bank_idx=torch.arange(n, dtype=torch.int32, device=device))
+        el_w, _ = timed(True, False)
+        wire_value = world * n * args.steps / el_w
+
+    S = P.size
+    algo_bytes = 2 * S * S + 64  # per env: S^2 texels sampled + S^2 frame bytes + ego state
+    raster_ms = ms3[1]
+    achieved = n * algo_bytes / (raster_ms * 1e-3) / 1e9
+    traffic = None
+    pmc_path = os.path.join(REPO, "profiles", f"pmc_raster_config{args.config}.json")
+    if os.path.exists(pmc_path):
+        with open(pmc_path) as f:
+            pmc = json.load(f)
+        if pmc.get("envs") == n:
+            traffic = pmc.get("hbm_bytes_per_launch")
+    cpu = None
+    if rank == 0 and not args.no_cpu_baseline and world == 1:
+        cpu = cpu_baseline(cfgd, host_recs, env, args.cpu_seconds)
+    if rank == 0:
+        out = {
+            "metric": "env-steps/sec (whole node) at N_envs x 128x128 semantic obs",
+            "value": round(value, 1),
+            "unit": "env-steps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(el / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64 state / u8 frames",
+            "data": "synthetic seeded scenes (host scene-gen on the Town01 class map), seeded action streams",
+            "config": {"workload": cfgd["workload"], "config_id": args.config, "envs_per_gpu": n,
+                       "global_envs": n * world, "obs_size": S, "obs_mode": cfgd["obs_mode"],
+                       "parallelism": f"env-sharded x{world}" + (" + RCCL gather" if gather else "")},
+            "kernel_ms": {"k_dyn": round(ms3[0], 5), "k_raster": round(ms3[1], 5), "k_collide": round(ms3[2], 5)},
+            "roofline": {"bound": "hbm", "kernel": "k_raster", "achieved": round(achieved, 1),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": traffic, "algorithmic_bytes_per_env": algo_bytes},
+            "with_wire_obs": None if wire_value is None else round(wire_value, 1),
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    env.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,70 @@
+"""ctypes binding of libcbev.so (the HIP C-ABI declared in include/cbev.h).
+
+The library is built in-tree (`__graft_entry__.build()` or `python -m
+carlabev_env_amd.build`). There is no CPU fallback: if the library is missing
+or cannot be loaded, `lib()` raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libcbev.so")
+
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_I64 = ctypes.c_int64
+
+_lib = None
+
+
+class CbevError(RuntimeError):
+    pass
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise CbevError(f"{LIB_PATH} not built; run `python -m carlabev_env_amd.build` (hipcc, gfx950)")
+    L = ctypes.CDLL(LIB_PATH)
+    L.cbev_abi_version.restype = _I
+    L.cbev_params_size.restype = _I
+    L.cbev_layout_of.argtypes = [_P, _P]
+    L.cbev_layout_of.restype = _I
+    L.cbev_field_names.argtypes = [_I]
+    L.cbev_field_names.restype = ctypes.c_char_p
+    L.cbev_last_error.restype = ctypes.c_char_p
+    L.cbev_create.argtypes = [_P, _P, _I, ctypes.POINTER(_P)]
+    L.cbev_create.restype = _I
+    L.cbev_destroy.argtypes = [_P]
+    L.cbev_destroy.restype = None
+    L.cbev_set_map.argtypes = [_P, _P, _I64]
+    L.cbev_set_map.restype = _I
+    L.cbev_step.argtypes = [_P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P]
+    L.cbev_step.restype = _I
+    L.cbev_reset.argtypes = [_P, _P, _I, _P, _I, _P, _P, _P, _P]
+    L.cbev_reset.restype = _I
+    L.cbev_fill_ring.argtypes = [_P, _P, _I, _I, _P, _P, _P]
+    L.cbev_fill_ring.restype = _I
+    L.cbev_expand_obs.argtypes = [_P, _P, _I, _I, _I, _I, _I, _P, _P, _P]
+    L.cbev_expand_obs.restype = _I
+    L.cbev_profile.argtypes = [_P, _I]
+    L.cbev_profile.restype = _I
+    L.cbev_profile_read.argtypes = [_P, _P, _P]
+    L.cbev_profile_read.restype = _I
+    _lib = L
+    return L
+
+
+def check(rc: int, what: str = "cbev call"):
+    if rc != 0:
+        msg = lib().cbev_last_error().decode("utf-8", "replace")
+        raise CbevError(f"{what} failed ({rc}): {msg}")
+
+
+EXPORTED_SYMBOLS = ("cbev_abi_version", "cbev_params_size", "cbev_layout_of", "cbev_field_names", "cbev_last_error",
+                    "cbev_create", "cbev_destroy", "cbev_set_map", "cbev_step", "cbev_reset", "cbev_fill_ring",
+                    "cbev_expand_obs", "cbev_profile", "cbev_profile_read")

@@ -1,0 +1,39 @@
+"""Build libcbev.so in-tree for gfx950 (`python -m carlabev_env_amd.build`)."""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+SRC = os.path.join(HERE, "csrc", "cbev.hip")
+OUT = os.path.join(HERE, "libcbev.so")
+DEPS = [SRC, os.path.join(HERE, "csrc", "cbev_device.h"), os.path.join(REPO, "include", "cbev.h"),
+        os.path.join(REPO, "include", "cbev_layout.h")]
+
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+# -ffp-contract=off: hipcc contracts a*b+c into FMA by default, which changes
+# rounding relative to the reference's (and the oracle's) float64 arithmetic.
+FLAGS = ["--offload-arch=gfx950", "-O3", "-fPIC", "-shared", "-std=c++17", "-ffp-contract=off",
+         "-fno-fast-math", "-Wall", "-Wno-unused-function", f"-I{os.path.join(REPO, 'include')}"]
+
+
+def needs_build() -> bool:
+    if not os.path.exists(OUT):
+        return True
+    t = os.path.getmtime(OUT)
+    return any(os.path.getmtime(d) > t for d in DEPS)
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    if force or needs_build():
+        cmd = [HIPCC, *FLAGS, "-o", OUT, SRC]
+        if verbose:
+            print(" ".join(cmd))
+        subprocess.run(cmd, check=True)
+    return OUT
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

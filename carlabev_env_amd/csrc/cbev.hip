@@ -1,0 +1,1250 @@
+// cbev.hip — MI355X (gfx950) kernels and C-ABI of the batched CarlaBEV step.
+//
+// One `CarlaBEV.step()` for N envs is three launches on the caller's stream:
+//
+//   k_dyn      wave64 per env: ego bicycle + Stanley target search (wave
+//              arg-min over the route), scripted actors (lane per actor:
+//              behaviour FSM, PID + Stanley, bicycle), scene clock, dist2goal.
+//              Reference: Scene._scene_step (scene.py:90-98), hero.py:88-187,
+//              actor.py:110-124, behavior/*.py, stanley_controller.py:51-123.
+//   k_raster   256-thread workgroup per env: stage the C x C crop of the padded
+//              class map into LDS (16-B loads), paint vehicles / pedestrians /
+//              visible targets / traffic lights in draw order, then the
+//              pygame rotate (16.16 fixed-point inverse map or exact rotate90)
+//              + compose at the ego anchor + ego overlay, written once to HBM
+//              as one palette id per pixel with 16-B stores.
+//              Reference: BaseMap.draw_fov (world.py:137-157), fov.py:70-99,
+//              actor_manager.py:121-132, hero.py:26-32.
+//   k_collide  wave64 per env: ego tile, rect collisions (last hit in draw
+//              order wins, wave max), target consumption, actors_state/TTC
+//              (wave min), CaRL route progress (wave arg-min over segments),
+//              reward, episode accumulators, termination flags.
+//              Reference: scene.py:110-140, carl_reward_fn.py:149-341,
+//              reward.py:80-278, stats.py:30-56, carlabev.py:177-185.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <string>
+
+#include "../../include/cbev.h"
+#include "cbev_device.h"
+
+__constant__ SgTables c_sg;
+
+// ============================================================== actors
+__device__ __forceinline__ void d_set_target_speed_mps(DRec& r, int a, double s) {
+  s = d_pymax(0.0, s);
+  RAD(r, CBEV_AD_T_SPEED_MPS, a) = s;
+  RAD(r, CBEV_AD_T_SPEED, a) = s / CB_MPP;
+}
+
+__device__ __forceinline__ void d_bset(DRec& r, int a, int st, double speed_mps) {
+  RAI(r, CBEV_AI_BSTATE, a) = st;
+  RAD(r, CBEV_AD_STATE_ELAPSED, a) = 0.0;
+  d_set_target_speed_mps(r, a, speed_mps);
+}
+
+// smooth_and_compute (control/utils.py:200-269) from the actor's current raw
+// route (arx/ary, n points) into its acx/acy/acyaw; returns the smoothed length.
+__device__ int d_smooth_route(DRec& r, int a) {
+  const int RA = r.RA;
+  double* ax = r.arx + (int64_t)a * RA;
+  double* ay = r.ary + (int64_t)a * RA;
+  double* cx = r.acx + (int64_t)a * RA;
+  double* cy = r.acy + (int64_t)a * RA;
+  double* cyaw = r.acyaw + (int64_t)a * RA;
+  const int n_in = RAI(r, CBEV_AI_NRX, a);
+  int n = 0;
+  for (int i = 0; i < n_in; ++i) {  // drop consecutive duplicates (vs the raw predecessor)
+    if (i == 0 || hypot(ax[i] - ax[i - 1], ay[i] - ay[i - 1]) > 1e-9) {
+      cyaw[n] = ax[i];  // cyaw/… used as scratch for the deduplicated input
+      cx[n] = ay[i];
+      ++n;
+    }
+  }
+  // deduplicated x in cyaw[0..n), y in cx[0..n)
+  if (n < 2) {
+    double x0 = cyaw[0], y0 = cx[0];
+    cyaw[0] = x0;
+    cx[0] = y0;
+    cyaw[1] = x0 + 1e-3;
+    cx[1] = y0;
+    n = 2;
+  }
+  int w = 11, p = 3;
+  if (w > n) w = (n % 2 == 1) ? n : n - 1;
+  if (w < 3) w = 3;
+  if (p > w - 1) p = w - 1;
+  (void)p;
+  const int h = w / 2, ti = w / 2;
+  // smooth x (scratch cyaw) -> cx after y is done: process y first into cy from cx scratch
+  if (n >= w) {
+    for (int i = 0; i < n; ++i) {
+      double acc = 0.0;
+      if (i < h) {
+        for (int j = 0; j < w; ++j) acc += c_sg.left[ti][i][j] * cx[j];
+      } else if (i >= n - h) {
+        for (int j = 0; j < w; ++j) acc += c_sg.right[ti][i - (n - h)][j] * cx[n - w + j];
+      } else {
+        for (int j = 0; j < w; ++j) acc += c_sg.conv[ti][j] * cx[i - h + j];
+      }
+      cy[i] = acc;
+    }
+    for (int i = 0; i < n; ++i) {
+      double acc = 0.0;
+      if (i < h) {
+        for (int j = 0; j < w; ++j) acc += c_sg.left[ti][i][j] * cyaw[j];
+      } else if (i >= n - h) {
+        for (int j = 0; j < w; ++j) acc += c_sg.right[ti][i - (n - h)][j] * cyaw[n - w + j];
+      } else {
+        for (int j = 0; j < w; ++j) acc += c_sg.conv[ti][j] * cyaw[i - h + j];
+      }
+      cx[i] = acc;  // overwrite: every read above of cx[] happened in the y pass
+    }
+  } else {
+    for (int i = 0; i < n; ++i) {
+      cy[i] = cx[i];
+      cx[i] = cyaw[i];
+    }
+  }
+  // arc length, gradient wrt s (np.gradient, edge_order 1), heading, unwrap
+  double total = 0.0;
+  for (int i = 1; i < n; ++i) total += hypot(cx[i] - cx[i - 1], cy[i] - cy[i - 1]);
+  if (total <= 1e-9) {
+    for (int i = 0; i < n; ++i) cyaw[i] = 0.0;
+    return n;
+  }
+  double s_prev = 0.0, s_cur = 0.0;
+  double s_next = hypot(cx[1] - cx[0], cy[1] - cy[0]);
+  double acc_corr = 0.0, prev_raw = 0.0;
+  for (int i = 0; i < n; ++i) {
+    double gx, gy;
+    if (i == 0) {
+      gx = (cx[1] - cx[0]) / (s_next - s_cur);
+      gy = (cy[1] - cy[0]) / (s_next - s_cur);
+    } else if (i == n - 1) {
+      gx = (cx[i] - cx[i - 1]) / (s_cur - s_prev);
+      gy = (cy[i] - cy[i - 1]) / (s_cur - s_prev);
+    } else {
+      double dx1 = s_cur - s_prev, dx2 = s_next - s_cur;
+      double ca = -(dx2) / (dx1 * (dx1 + dx2));
+      double cb = (dx2 - dx1) / (dx1 * dx2);
+      double cc = dx1 / (dx2 * (dx1 + dx2));
+      gx = ca * cx[i - 1] + cb * cx[i] + cc * cx[i + 1];
+      gy = ca * cy[i - 1] + cb * cy[i] + cc * cy[i + 1];
+    }
+    double raw = atan2(gy, gx);
+    if (i > 0) {  // np.unwrap
+      double dd = raw - prev_raw;
+      double ddmod = d_remainder(dd + CB_PI, 2.0 * CB_PI) - CB_PI;
+      if (ddmod == -CB_PI && dd > 0) ddmod = CB_PI;
+      double corr = ddmod - dd;
+      if (fabs(dd) < CB_PI) corr = 0.0;
+      acc_corr += corr;
+    }
+    prev_raw = raw;
+    cyaw[i] = raw + acc_corr;
+    s_prev = s_cur;
+    s_cur = s_next;
+    if (i + 2 < n) s_next = s_cur + hypot(cx[i + 2] - cx[i + 1], cy[i + 2] - cy[i + 1]);
+  }
+  return n;
+}
+
+// BaseJaywalkBehavior._start_retreat (jaywalk.py:43-54) + Actor.set_route_surface
+// (actor.py:139-149) + Controller.set_route(jitter_start=False).
+__device__ void d_start_retreat(DRec& r, int a) {
+  const int RA = r.RA;
+  int nrx = RAI(r, CBEV_AI_NRX, a);
+  int cur = RAI(r, CBEV_AI_TIDX, a);
+  if (cur > nrx - 1) cur = nrx - 1;
+  if (cur < 0) cur = 0;
+  int n = cur + 2;
+  if (n > RA) n = RA;
+  const double* ix = r.aix + (int64_t)a * RA;
+  const double* iy = r.aiy + (int64_t)a * RA;
+  double* ax = r.arx + (int64_t)a * RA;
+  double* ay = r.ary + (int64_t)a * RA;
+  ax[0] = RAD(r, CBEV_AD_X, a);
+  ay[0] = RAD(r, CBEV_AD_Y, a);
+  for (int k = 1; k < n; ++k) {
+    ax[k] = ix[cur - (k - 1)];
+    ay[k] = iy[cur - (k - 1)];
+  }
+  RAD(r, CBEV_AD_GOAL_X, a) = ix[0];
+  RAD(r, CBEV_AD_GOAL_Y, a) = iy[0];
+  RAI(r, CBEV_AI_HAS_GOAL, a) = 1;
+  RAI(r, CBEV_AI_NRX, a) = n;
+  int m = d_smooth_route(r, a);
+  RAI(r, CBEV_AI_NROUTE, a) = m;
+  const double* cx = r.acx + (int64_t)a * RA;
+  const double* cy = r.acy + (int64_t)a * RA;
+  const double* cyaw = r.acyaw + (int64_t)a * RA;
+  double v0 = RAD(r, CBEV_AD_V, a);
+  RAD(r, CBEV_AD_X, a) = cx[0];
+  RAD(r, CBEV_AD_Y, a) = cy[0];
+  RAD(r, CBEV_AD_V, a) = v0;
+  int tidx = d_target_index_serial(cx[0], cy[0], RAD(r, CBEV_AD_YAW, a), cx, cy, m, nullptr);
+  RAI(r, CBEV_AI_TIDX, a) = tidx;
+  RAD(r, CBEV_AD_YAW, a) = cyaw[tidx];
+  d_bset(r, a, CBEV_BST_RETREATING, RAD(r, CBEV_AD_CRUISE_MPS, a));
+}
+
+// Behaviour.apply (lead_brake.py:10-15, jaywalk.py:56-138)
+__device__ void d_behavior(DRec& r, int a, double t) {
+  const int beh = RAI(r, CBEV_AI_BEH, a);
+  if (beh == CBEV_BEH_NONE) return;
+  if (beh == CBEV_BEH_LEAD_BRAKE) {
+    if (t >= RAD(r, CBEV_AD_P0, a)) RAI(r, CBEV_AI_BRAKING, a) = 1;
+    if (RAI(r, CBEV_AI_BRAKING, a))
+      d_set_target_speed_mps(r, a, RAD(r, CBEV_AD_T_SPEED_MPS, a) - RAD(r, CBEV_AD_P1, a) * CB_DT);
+    return;
+  }
+  RAD(r, CBEV_AD_ELAPSED, a) += CB_DT;
+  RAD(r, CBEV_AD_STATE_ELAPSED, a) += CB_DT;
+  const int st = RAI(r, CBEV_AI_BSTATE, a);
+  const double cruise = RAD(r, CBEV_AD_CRUISE_MPS, a);
+  const int nrx = RAI(r, CBEV_AI_NRX, a);
+  const int tidx = RAI(r, CBEV_AI_TIDX, a);
+  const bool done = tidx >= nrx - 1;
+  if (beh == CBEV_BEH_CROSS) {
+    if (st == CBEV_BST_WAITING) {
+      d_set_target_speed_mps(r, a, 0.0);
+      if (RAD(r, CBEV_AD_ELAPSED, a) >= RAD(r, CBEV_AD_P0, a)) d_bset(r, a, CBEV_BST_CROSSING, cruise);
+    } else if (st == CBEV_BST_CROSSING) {
+      d_set_target_speed_mps(r, a, cruise);
+      if (done) d_bset(r, a, CBEV_BST_CLEARED, 0.0);
+    } else if (st == CBEV_BST_CLEARED) {
+      d_set_target_speed_mps(r, a, 0.0);
+    }
+    return;
+  }
+  const double trigger = (beh == CBEV_BEH_STOP_MID) ? 0.5 : 1.0 / 3.0;
+  const bool retreat = (beh == CBEV_BEH_YIELD_RETURN);
+  int mid = (int)(trigger * (nrx - 1));
+  if (mid > nrx - 1) mid = nrx - 1;
+  if (mid < 1) mid = 1;
+  if (st == CBEV_BST_WAITING) {
+    d_set_target_speed_mps(r, a, 0.0);
+    if (RAD(r, CBEV_AD_ELAPSED, a) >= RAD(r, CBEV_AD_P0, a)) d_bset(r, a, CBEV_BST_ENTERING, cruise);
+  } else if (st == CBEV_BST_ENTERING) {
+    d_set_target_speed_mps(r, a, cruise);
+    if (tidx >= mid) {
+      d_bset(r, a, retreat ? CBEV_BST_YIELDING : CBEV_BST_STALLED, 0.0);
+    } else if (done) {
+      d_bset(r, a, CBEV_BST_CLEARED, 0.0);
+    }
+  } else if (st == CBEV_BST_YIELDING) {
+    d_set_target_speed_mps(r, a, 0.0);
+    if (retreat && RAD(r, CBEV_AD_STATE_ELAPSED, a) >= RAD(r, CBEV_AD_P1, a)) d_start_retreat(r, a);
+  } else if (st == CBEV_BST_CROSSING) {
+    d_set_target_speed_mps(r, a, cruise);
+    if (done) d_bset(r, a, CBEV_BST_CLEARED, 0.0);
+  } else if (st == CBEV_BST_STALLED) {
+    d_set_target_speed_mps(r, a, 0.0);
+  } else if (st == CBEV_BST_RETREATING) {
+    d_set_target_speed_mps(r, a, cruise);
+    bool goal = false;
+    if (RAI(r, CBEV_AI_HAS_GOAL, a)) {
+      double dx = RAD(r, CBEV_AD_X, a) - RAD(r, CBEV_AD_GOAL_X, a);
+      double dy = RAD(r, CBEV_AD_Y, a) - RAD(r, CBEV_AD_GOAL_Y, a);
+      goal = sqrt(dx * dx + dy * dy) <= 1.0;
+    }
+    if (goal || RAI(r, CBEV_AI_TIDX, a) >= RAI(r, CBEV_AI_NRX, a) - 1) d_bset(r, a, CBEV_BST_RETREATED, 0.0);
+  } else if (st == CBEV_BST_CLEARED || st == CBEV_BST_RETREATED) {
+    d_set_target_speed_mps(r, a, 0.0);
+  }
+}
+
+// Actor.step (actor.py:110-119) + Controller.control_step (stanley_controller.py:51-62)
+__device__ void d_actor_step(DRec& r, int a, double t) {
+  d_behavior(r, a, t);
+  RAD(r, CBEV_AD_CT_SPEED, a) = RAD(r, CBEV_AD_T_SPEED, a);
+  const int n = RAI(r, CBEV_AI_NROUTE, a);
+  if (RAI(r, CBEV_AI_TIDX, a) >= n - 1) {
+    RAD(r, CBEV_AD_CT_SPEED, a) = 0.0;  // frozen at route end
+    return;
+  }
+  const int RA = r.RA;
+  const double* cx = r.acx + (int64_t)a * RA;
+  const double* cy = r.acy + (int64_t)a * RA;
+  const double* cyaw = r.acyaw + (int64_t)a * RA;
+  double s[8] = {RAD(r, CBEV_AD_X, a), RAD(r, CBEV_AD_Y, a), RAD(r, CBEV_AD_YAW, a), RAD(r, CBEV_AD_V, a), 0, 0, 0, 0};
+  const double ts = RAD(r, CBEV_AD_CT_SPEED, a);
+  double ai = 1.0 * (ts - s[3]);
+  int tidx;
+  double di = d_stanley_serial(s[0], s[1], s[2], s[3], cx, cy, cyaw, n, RAI(r, CBEV_AI_TIDX, a), &tidx);
+  RAI(r, CBEV_AI_TIDX, a) = tidx;
+  d_state_update(s, ai, di, ts);
+  RAD(r, CBEV_AD_X, a) = s[0];
+  RAD(r, CBEV_AD_Y, a) = s[1];
+  RAD(r, CBEV_AD_YAW, a) = s[2];
+  RAD(r, CBEV_AD_V, a) = s[3];
+  RAD(r, CBEV_AD_TIME, a) += CB_DT;
+}
+
+// ============================================================== k_dyn
+// One wavefront per env; 4 envs per 256-thread workgroup.
+__global__ __launch_bounds__(256) void k_dyn(KArgs K, uint8_t* __restrict__ recs, int n,
+                                             const void* __restrict__ actions) {
+  const int lane = threadIdx.x & 63;
+  const int e = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (e >= n) return;  // wave-uniform; no workgroup barrier in this kernel
+  DRec r = bind_rec(recs + (int64_t)e * K.L.record_bytes, K.L, K.C);
+  double* hd = r.hd;
+  int32_t* hi = r.hi;
+
+  // decode_action (envs/spaces.py:43-47); continuous: ContinuousAgent clips in float32
+  float g, sa, b;
+  if (K.P.action_kind == 0) {
+    int idx = ((const int32_t*)actions)[e];
+    idx = idx < 0 ? 0 : (idx >= K.P.n_discrete ? K.P.n_discrete - 1 : idx);
+    g = K.P.action_table[idx][0];
+    sa = K.P.action_table[idx][1];
+    b = K.P.action_table[idx][2];
+  } else {
+    const float* a3 = (const float*)actions + 3 * (int64_t)e;
+    g = a3[0];
+    sa = a3[1];
+    b = a3[2];
+    g = (g != g) ? g : (g < 0.0f ? 0.0f : (g > 1.0f ? 1.0f : g));
+    sa = (sa != sa) ? sa : (sa < -1.0f ? -1.0f : (sa > 1.0f ? 1.0f : sa));
+    b = (b != b) ? b : (b < 0.0f ? 0.0f : (b > 1.0f ? 1.0f : b));
+  }
+
+  const double t = hd[CBEV_HD_T] + CB_DT;  // Scene._t += dt
+
+  // ---- hero Stanley target search: wave arg-min over the smoothed route
+  double s[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) s[k] = hd[CBEV_HD_X + k];
+  const double fx = s[0] + CB_WHEELBASE * cos(s[2]);
+  const double fy = s[1] + CB_WHEELBASE * sin(s[2]);
+  const int nroute = hi[CBEV_HI_NROUTE];
+  double bd = INFINITY;
+  int bi = 0x7fffffff;
+  for (int i = lane; i < nroute; i += 64) {
+    double d = hypot(fx - r.cx[i], fy - r.cy[i]);
+    if (bi == 0x7fffffff || d < bd) {  // first minimum within the lane's stride
+      bd = d;
+      bi = i;
+    }
+  }
+  wave_argmin(bd, bi);
+
+  if (lane == 0) {
+    // stanley_control: monotone target index (its steering output is unused by the hero)
+    int tidx = hi[CBEV_HI_TIDX] >= bi ? hi[CBEV_HI_TIDX] : bi;
+    hi[CBEV_HI_TIDX] = tidx;
+    const double v = s[3];
+    const int scale = K.P.scale;
+    // BaseAgent.accelerate / steering / brake (hero.py:140-162)
+    double acc_val = (g > 0.0f) ? (double)((g * 1.0f) * (float)scale) : 0.0;
+    double delta;
+    if (fabs(v) < 0.1) {
+      delta = 0.0;
+    } else {
+      double steer_deg = 18.0 / (1.0 + 0.35 * fabs(v));
+      steer_deg = d_clip(steer_deg, 8.0, 18.0);
+      delta = d_radians((double)sa * steer_deg);
+    }
+    double sf = d_clip(fabs(v) / 5.0, 0.3, 1.0);
+    double brake_val = (b > 0.0f) ? (double)((b * 0.6f) * (float)scale) * sf : 0.0 * 0.6 * scale * sf;
+    double target_acc = acc_val - brake_val - 0.05 * v;
+    const double alpha = 0.2;
+    double acc = (1 - alpha) * hd[CBEV_HD_ACC] + alpha * target_acc;
+    hd[CBEV_HD_ACC] = acc;
+    d_state_update(s, acc, delta, hd[CBEV_HD_TSPEED]);
+    s[3] *= 0.9999;
+    if (fabs(s[3]) < 0.05) s[3] = 0.0;
+    s[3] *= 0.985;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) hd[CBEV_HD_X + k] = s[k];
+    hd[CBEV_HD_U_GAS] = (double)g;
+    hd[CBEV_HD_U_STEER] = (double)sa;
+    hd[CBEV_HD_U_BRAKE] = (double)b;
+    hd[CBEV_HD_U_DELTA] = delta;
+    // compute_comfort_kinematics (comfort.py:17-61)
+    const int has_prev = hi[CBEV_HI_HAS_PREV_COMFORT];
+    double speed_mps = s[3] * CB_MPP, prev_speed_mps = s[7] * CB_MPP;
+    double dyaw = s[2] - s[6];
+    double yr_rad = atan2(sin(dyaw), cos(dyaw)) / CB_DT;
+    double yr_deg = d_degrees(yr_rad);
+    double al = (speed_mps - prev_speed_mps) / CB_DT;
+    double alat = speed_mps * yr_rad;
+    hd[CBEV_HD_C_SPEED] = speed_mps;
+    hd[CBEV_HD_C_AL] = al;
+    hd[CBEV_HD_C_ALAT] = alat;
+    hd[CBEV_HD_C_JL] = has_prev ? (al - hd[CBEV_HD_PREV_AL]) / CB_DT : 0.0;
+    hd[CBEV_HD_C_JLAT] = has_prev ? (alat - hd[CBEV_HD_PREV_ALAT]) / CB_DT : 0.0;
+    hd[CBEV_HD_C_YR] = yr_deg;
+    hd[CBEV_HD_C_YACC] = has_prev ? (yr_deg - hd[CBEV_HD_PREV_YR]) / CB_DT : 0.0;
+    hd[CBEV_HD_PREV_AL] = al;
+    hd[CBEV_HD_PREV_ALAT] = alat;
+    hd[CBEV_HD_PREV_YR] = yr_deg;
+    hi[CBEV_HI_HAS_PREV_COMFORT] = 1;
+    hd[CBEV_HD_T] = t;
+  }
+
+  // ---- scripted actors, one lane each (vehicles then pedestrians)
+  const int nact = hi[CBEV_HI_NACT];
+  for (int a = lane; a < nact; a += 64) d_actor_step(r, a, t);
+
+  if (lane == 0) {  // Scene dist2goal bookkeeping (scene.py:97-98,175-177)
+    hd[CBEV_HD_D2G_T1] = hd[CBEV_HD_D2G];
+    double dx = s[0] - hd[CBEV_HD_GOAL_X], dy = s[1] - hd[CBEV_HD_GOAL_Y];
+    hd[CBEV_HD_D2G] = sqrt(dx * dx + dy * dy);
+  }
+}
+
+// ============================================================== k_raster
+__device__ __forceinline__ void d_crop_origin(const cbev_params& P, double x, double y, int* xm, int* ym) {
+  const double C = (double)P.crop;
+  double offx = trunc(((double)P.pad + x) + (-C / 2));  // Follow.scroll int() (camera.py:39-42)
+  double offy = trunc(((double)P.pad + y) + (-C / 2));
+  int cxc = (int)rint(offx + C / 2.0);  // round() half-even (fov.py:70-79)
+  int cyc = (int)rint(offy + C / 2.0);
+  int xmin = cxc - P.crop / 2, ymin = cyc - P.crop / 2;
+  int maxx = P.render_w - P.crop, maxy = P.render_h - P.crop;
+  maxx = maxx < 0 ? 0 : maxx;
+  maxy = maxy < 0 ? 0 : maxy;
+  *xm = xmin < 0 ? 0 : (xmin > maxx ? maxx : xmin);
+  *ym = ymin < 0 ? 0 : (ymin > maxy ? maxy : ymin);
+}
+
+// rect_from_world_center (transforms.py:46-51): centre rounded half-even, x = c - w/2
+__device__ __forceinline__ int d_rect_lo(double w, int pad, int size) { return (int)rint((double)pad + w * 1.0) - size / 2; }
+
+// paint one group of rects (same colour) into the LDS crop; thread t handles pixel
+// (t & 15) of rect base + (t >> 4); rect side <= 4 for actors and targets
+__device__ __forceinline__ void lds_paint_px(uint8_t* lds, int stride, int shift, int C, int rx, int ry, int sz, int p,
+                                             uint8_t col) {
+  if (p >= sz * sz) return;
+  int px = rx + (p % sz), py = ry + (p / sz);
+  if (px < 0 || py < 0 || px >= C || py >= C) return;
+  lds[py * stride + shift + px] = col;
+}
+
+template <bool RESET>
+__global__ __launch_bounds__(256) void k_raster(KArgs K, uint8_t* __restrict__ recs, int n, uint8_t* __restrict__ frames,
+                                                const uint8_t* __restrict__ mask) {
+  extern __shared__ __align__(16) uint8_t lds[];
+  const int e = blockIdx.x;
+  if (e >= n) return;
+  if (mask != nullptr && mask[e] == 0) return;  // uniform per workgroup
+  DRec r = bind_rec(recs + (int64_t)e * K.L.record_bytes, K.L, K.C);
+  const cbev_params& P = K.P;
+  const int C = P.crop, S = P.size, pitch = P.map_pitch;
+  const double x = r.hd[CBEV_HD_X], y = r.hd[CBEV_HD_Y], yaw = r.hd[CBEV_HD_YAW];
+  int xmin, ymin;
+  d_crop_origin(P, x, y, &xmin, &ymin);
+  const int shift = xmin & 15;
+  const int W16 = (C + 30) / 16;  // 16-B chunks per staged row: covers shift (<=15) + C
+  const int stride = W16 * 16;
+
+  // ---- stage the crop window (rows of the padded map) into LDS
+  const uint8_t* src0 = K.map + (int64_t)ymin * pitch + (xmin - shift);
+  const int nchunks = C * W16;
+  for (int q = threadIdx.x; q < nchunks; q += 256) {
+    int row = q / W16, col = q - row * W16;
+    uint4 v = *(const uint4*)(src0 + (int64_t)row * pitch + col * 16);
+    *(uint4*)(lds + row * stride + col * 16) = v;
+  }
+  __syncthreads();
+
+  // ---- paint actors / visible targets / traffic lights in draw order
+  if (!RESET) {
+    const int nact = r.hi[CBEV_HI_NACT], nveh = r.hi[CBEV_HI_NVEH];
+    for (int pass = 0; pass < 2; ++pass) {  // vehicles, then pedestrians
+      const int a0 = pass == 0 ? 0 : nveh, a1 = pass == 0 ? nveh : nact;
+      for (int base = a0; base < a1; base += 16) {
+        int a = base + (threadIdx.x >> 4);
+        if (a < a1) {
+          int sz = RAI(r, CBEV_AI_SIZE, a);
+          int rx = d_rect_lo(RAD(r, CBEV_AD_X, a), P.pad, sz) - xmin;
+          int ry = d_rect_lo(RAD(r, CBEV_AD_Y, a), P.pad, sz) - ymin;
+          lds_paint_px(lds, stride, shift, C, rx, ry, sz, threadIdx.x & 15,
+                       pass == 0 ? CBEV_PX_VEHICLE : CBEV_PX_PEDESTRIAN);
+        }
+      }
+      __syncthreads();
+    }
+    const int nt = r.hi[CBEV_HI_NROUTE];
+    for (int base = 0; base < nt; base += 16) {
+      int i = base + (threadIdx.x >> 4);
+      if (i < nt && ((r.vis[i >> 5] >> (i & 31)) & 1u)) {
+        int sz = (i < nt - 1) ? 2 : 4;  // checkpoints 2x2, goal 4x4 (scenes/utils.py:114-122)
+        int rx = d_rect_lo(r.cx[i], P.pad, sz) - xmin;
+        int ry = d_rect_lo(r.cy[i], P.pad, sz) - ymin;
+        lds_paint_px(lds, stride, shift, C, rx, ry, sz, threadIdx.x & 15, CBEV_PX_ROUTE);
+      }
+    }
+    __syncthreads();
+    const int ntl = r.hi[CBEV_HI_NTL];
+    for (int k = 0; k < ntl; ++k) {  // traffic lights one at a time (colours may differ)
+      int rx = r.ti[CBEV_TI_RX * r.T + k] - xmin, ry = r.ti[CBEV_TI_RY * r.T + k] - ymin;
+      int rw = r.ti[CBEV_TI_RW * r.T + k], rh = r.ti[CBEV_TI_RH * r.T + k];
+      uint8_t col = (uint8_t)r.ti[CBEV_TI_COLOR * r.T + k];
+      for (int p = threadIdx.x; p < rw * rh; p += 256) {
+        int px = rx + p % rw, py = ry + p / rw;
+        if (px >= 0 && py >= 0 && px < C && py < C) lds[py * stride + shift + px] = col;
+      }
+      __syncthreads();
+    }
+  }
+
+  // ---- rotate (pygame transform.rotate / rotate90) + compose + ego overlay
+  const uint8_t bg = lds[shift];  // crop top-left pixel after painting
+  const float angle = RESET ? 90.0f : (float)(d_degrees(yaw) + 90);
+  const bool r90 = fmod((double)angle, (double)90.0f) == 0.0;
+  int nx = C, ny = C, numturns = 0;
+  int isin = 0, icos = 0, axf = 0, ayf = 0, xd = 0, yd = 0, icy = 0;
+  if (r90) {
+    numturns = ((int)angle / 90) % 4;
+    if (numturns < 0) numturns += 4;
+  } else {
+    double rad = angle * .01745329251994329;
+    double sn = sin(rad), cs = cos(rad);
+    double xw = C, yh = C;
+    double cxw = cs * xw, cyh = cs * yh, sxw = sn * xw, syh = sn * yh;
+    double m1 = fmax(fmax(fmax(fabs(cxw + syh), fabs(cxw - syh)), fabs(-cxw + syh)), fabs(-cxw - syh));
+    double m2 = fmax(fmax(fmax(fabs(sxw + cyh), fabs(sxw - cyh)), fabs(-sxw + cyh)), fabs(-sxw - cyh));
+    nx = (int)m1;
+    ny = (int)m2;
+    icy = ny / 2;
+    xd = (C - nx) * 32768;
+    yd = (C - ny) * 32768;
+    isin = (int)(sn * 65536);
+    icos = (int)(cs * 65536);
+    axf = (nx << 15) - (int)(cs * ((nx - 1) << 15));
+    ayf = (ny << 15) - (int)(sn * ((nx - 1) << 15));
+  }
+  const int xmaxv = (C << 16) - 1, ymaxv = (C << 16) - 1;
+  const int rx0 = P.anchor_x - nx / 2, ry0 = P.anchor_y - ny / 2;
+  const int hx0 = P.anchor_x - P.hero_w / 2, hy0 = P.anchor_y - P.hero_w / 2;
+  const int hx1 = hx0 + P.hero_w, hy1 = hy0 + P.hero_w;
+  const int cpr = S / 16;  // 16-pixel chunks per output row
+  uint8_t* out = frames + (int64_t)e * S * S;
+  for (int q = threadIdx.x; q < S * cpr; q += 256) {
+    const int v = q / cpr, u0 = (q - v * cpr) * 16;
+    uint32_t w[4] = {0, 0, 0, 0};
+    const int yy = v - ry0;
+    const bool row_in = (yy >= 0 && yy < ny);
+    const bool hrow = (v >= hy0 && v < hy1);
+    int dxr = 0, dyr = 0;
+    if (!r90) {
+      dxr = (axf + (isin * (icy - yy))) + xd;
+      dyr = (ayf - (icos * (icy - yy))) + yd;
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int u = u0 + k;
+      const int xx = u - rx0;
+      uint32_t px = CBEV_PX_BLACK;
+      if (row_in && xx >= 0 && xx < nx) {
+        if (r90) {
+          int ri, ci;
+          if (numturns == 0) { ri = yy; ci = xx; }
+          else if (numturns == 1) { ri = xx; ci = C - 1 - yy; }
+          else if (numturns == 2) { ri = C - 1 - yy; ci = C - 1 - xx; }
+          else { ri = C - 1 - xx; ci = yy; }
+          px = lds[ri * stride + shift + ci];
+        } else {
+          int dx = dxr + xx * icos, dy = dyr + xx * isin;
+          px = (dx < 0 || dy < 0 || dx > xmaxv || dy > ymaxv) ? bg : lds[(dy >> 16) * stride + shift + (dx >> 16)];
+        }
+      }
+      if (hrow && u >= hx0 && u < hx1) px = CBEV_PX_BLACK;
+      w[k >> 2] |= px << (8 * (k & 3));
+    }
+    *(uint4*)(out + v * S + u0) = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+}
+
+// ============================================================== k_collide
+__device__ __forceinline__ double d_lateral_error(double px, double py, const double* wx, const double* wy, int n) {
+  double min_error = INFINITY;
+  for (int i = 0; i < n - 1; ++i) {
+    double abx = wx[i + 1] - wx[i], aby = wy[i + 1] - wy[i];
+    double apx = px - wx[i], apy = py - wy[i];
+    double tt = (apx * abx + apy * aby) / (abx * abx + aby * aby);
+    tt = d_clip(tt, 0.0, 1.0);
+    double ex = px - (wx[i] + tt * abx), ey = py - (wy[i] + tt * aby);
+    double err = sqrt(ex * ex + ey * ey);
+    double cross = abx * apy - aby * apx;
+    if (cross != 0) err *= (cross > 0) ? 1.0 : ((cross < 0) ? -1.0 : cross);
+    if (fabs(err) < fabs(min_error)) min_error = err;
+  }
+  return min_error;
+}
+
+__global__ __launch_bounds__(256) void k_collide(KArgs K, uint8_t* __restrict__ recs, int n, double* __restrict__ reward_out,
+                                                 uint8_t* __restrict__ term_out, uint8_t* __restrict__ trunc_out,
+                                                 int32_t* __restrict__ cause_out, float* __restrict__ info_out) {
+  const int lane = threadIdx.x & 63;
+  const int e = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (e >= n) return;
+  DRec r = bind_rec(recs + (int64_t)e * K.L.record_bytes, K.L, K.C);
+  const cbev_params& P = K.P;
+  double* hd = r.hd;
+  int32_t* hi = r.hi;
+  const double x = hd[CBEV_HD_X], y = hd[CBEV_HD_Y], yaw = hd[CBEV_HD_YAW], v = hd[CBEV_HD_V];
+
+  // ---- ego tile (world.py:159-165)
+  int tx = (int)d_clip(rint(x), 0, P.map_w - 1), ty = (int)d_clip(rint(y), 0, P.map_h - 1);
+  const int tile = K.map[(int64_t)(ty + P.pad) * P.map_pitch + tx + P.pad];
+
+  // ---- collisions (scene.py:110-140): hero rect vs vehicles, pedestrians, visible targets
+  const int hw = P.hero_w;
+  const int hrx = d_rect_lo(x, P.pad, hw), hry = d_rect_lo(y, P.pad, hw);
+  const int nact = hi[CBEV_HI_NACT];
+  const int nt = hi[CBEV_HI_NROUTE];
+  int last_hit = -1, nas = 0;
+  double ttc_carl = INFINITY, ttc_sh = INFINITY;
+  const double hx_m = x * CB_MPP, hy_m = y * CB_MPP, hv_m = v * CB_MPP;
+  const double hvx_m = hv_m * cos(yaw), hvy_m = hv_m * sin(yaw);
+  const double hvx = v * cos(yaw), hvy = v * sin(yaw);
+  for (int a = lane; a < nact; a += 64) {
+    const int sz = RAI(r, CBEV_AI_SIZE, a);
+    const double ax = RAD(r, CBEV_AD_X, a), ay = RAD(r, CBEV_AD_Y, a);
+    const int arx = d_rect_lo(ax, P.pad, sz), ary = d_rect_lo(ay, P.pad, sz);
+    const bool hit = hw > 0 && sz > 0 && hrx < arx + sz && hry < ary + sz && hrx + hw > arx && hry + hw > ary;
+    const int ddx = (hrx + hw / 2) - (arx + sz / 2), ddy = (hry + hw / 2) - (ary + sz / 2);
+    const double dist = hypot((double)ddx, (double)ddy);
+    if (fabs(dist) < P.collide_min_dist) {  // actors_state entry
+      ++nas;
+      const double av = RAD(r, CBEV_AD_V, a), ayaw = RAD(r, CBEV_AD_YAW, a);
+      const double avx = av * cos(ayaw), avy = av * sin(ayaw);
+      {  // compute_ttc_raw (reward_signals.py:46-94)
+        double rx_ = ax * CB_MPP - hx_m, ry_ = ay * CB_MPP - hy_m;
+        double rvx = avx * CB_MPP - hvx_m, rvy = avy * CB_MPP - hvy_m;
+        double nrm = sqrt(rx_ * rx_ + ry_ * ry_);
+        double rel = (rvx * rx_ + rvy * ry_) / (nrm + 1e-6);
+        if (!(rel >= 0)) {
+          double ttc = fabs(nrm / rel);
+          ttc_carl = ttc < ttc_carl ? ttc : ttc_carl;
+        }
+      }
+      {  // compute_ttc (reward_signals.py:15-42)
+        double rx_ = ax - x, ry_ = ay - y;
+        double rvx = avx - hvx, rvy = avy - hvy;
+        double nrm = sqrt(rx_ * rx_ + ry_ * ry_);
+        double rel = (rvx * rx_ + rvy * ry_) / (nrm + 1e-6);
+        if (!(rel >= 0)) {
+          double ttc = fabs(nrm / rel);
+          ttc_sh = ttc < ttc_sh ? ttc : ttc_sh;
+        }
+      }
+    }
+    if (hit) last_hit = a;
+  }
+  for (int i = lane; i < nt; i += 64) {
+    if (!((r.vis[i >> 5] >> (i & 31)) & 1u)) continue;
+    const int sz = (i < nt - 1) ? 2 : 4;
+    const int trx = d_rect_lo(r.cx[i], P.pad, sz), try_ = d_rect_lo(r.cy[i], P.pad, sz);
+    if (hrx < trx + sz && hry < try_ + sz && hrx + hw > trx && hry + hw > try_) {
+      atomicAnd(&r.vis[i >> 5], ~(1u << (i & 31)));  // every visible target hit is consumed
+      last_hit = nact + i;
+    }
+  }
+  last_hit = wave_max_i(last_hit);
+  nas = wave_sum_i(nas);
+  ttc_carl = wave_min(ttc_carl);
+  ttc_sh = wave_min(ttc_sh);
+
+  // ---- CaRL route progress: arg-min over raw-route segments (carl_reward_fn.py:29-58)
+  const int nraw = hi[CBEV_HI_NRAW];
+  double bdist = 1e9;
+  int bseg = 0x7fffffff;
+  for (int i = lane; i < nraw - 1; i += 64) {
+    const int abx_i = r.raw_x[i + 1] - r.raw_x[i], aby_i = r.raw_y[i + 1] - r.raw_y[i];
+    const double ax = r.raw_x[i], ay = r.raw_y[i];
+    const double apx = x - ax, apy = y - ay;
+    const double tt = d_clip((apx * abx_i + apy * aby_i) / ((double)(abx_i * abx_i + aby_i * aby_i) + 1e-9), 0, 1);
+    const double ex = x - (ax + tt * abx_i), ey = y - (ay + tt * aby_i);
+    const double dist = sqrt(ex * ex + ey * ey);
+    if (dist < bdist) {
+      bdist = dist;
+      bseg = i;
+    }
+  }
+  wave_argmin(bdist, bseg);
+
+  if (lane != 0) return;
+
+  int result = CBEV_COLL_NONE, coll_id = -1;
+  if (last_hit >= 0) {
+    if (last_hit < nact) {
+      const int kind = RAI(r, CBEV_AI_KIND, last_hit);
+      result = kind == 1 ? CBEV_COLL_VEHICLE : CBEV_COLL_PEDESTRIAN;
+      coll_id = kind == 1 ? 0 : 1;
+    } else {
+      const int i = last_hit - nact;
+      result = CBEV_COLL_TARGET;
+      coll_id = (i < nt - 1) ? i : -2;
+    }
+  }
+  hi[CBEV_HI_TILE] = tile;
+  hi[CBEV_HI_COLLIDED] = result;
+  hi[CBEV_HI_ACTOR_ID] = coll_id;
+  hi[CBEV_HI_NACTSTATE] = nas;
+
+  // scene_info / controller_info (scene.py:206-225, stanley_controller.py:125-163)
+  const int tidx = hi[CBEV_HI_TIDX];
+  const double spx = r.cx[tidx], spy = r.cy[tidx], spyaw = r.cyaw[tidx];
+  double dist2wp;
+  {
+    double dx = x - spx, dy = y - spy;
+    dist2wp = sqrt(dx * dx + dy * dy);
+  }
+  hd[CBEV_HD_DIST2WP] = dist2wp;
+  const int wend = (tidx + 5 <= nt) ? tidx + 5 : nt - 1;
+  const int nw = wend > tidx ? wend - tidx : 0;
+  const double al = hd[CBEV_HD_C_AL], alat = hd[CBEV_HD_C_ALAT], yr = hd[CBEV_HD_C_YR];
+  const double jl = hd[CBEV_HD_C_JL], jlat = hd[CBEV_HD_C_JLAT], yacc = hd[CBEV_HD_C_YACC];
+  const int nviol = (fabs(al) > 2.0) + (fabs(alat) > 2.0) + (fabs(yr) > 20.0) + (fabs(jl) > 3.0) + (fabs(jlat) > 3.0) +
+                    (fabs(yacc) > 120.0);
+
+  int cause = CBEV_CAUSE_NONE;
+  double reward;
+  if (P.reward_kind == 0) {  // ---- CaRLRewardFn.step
+    hd[CBEV_HD_RC] = 0.0;
+    hd[CBEV_HD_P_LANE] = hd[CBEV_HD_P_OFF] = hd[CBEV_HD_P_SPEED] = hd[CBEV_HD_P_TTC] = hd[CBEV_HD_P_COMFORT] = 1.0;
+    if (tile == 0) {
+      cause = CBEV_CAUSE_COLLISION;
+      reward = -1.0;
+    } else if (coll_id == -2) {
+      cause = CBEV_CAUSE_SUCCESS;
+      reward = 1.0;
+    } else if (result == CBEV_COLL_TARGET && coll_id != -1) {
+      cause = CBEV_CAUSE_CKPT;
+      reward = 0.1;
+    } else if (result == CBEV_COLL_VEHICLE || result == CBEV_COLL_PEDESTRIAN) {
+      cause = CBEV_CAUSE_COLLISION;
+      reward = -1.0;
+    } else if (dist2wp > 50) {
+      cause = CBEV_CAUSE_OUT_OF_BOUNDS;
+      reward = -1.0;
+    } else {
+      double s_t = 0.0;
+      if (bdist < 1e9) {  // recompute the winning segment's arc position
+        const int i = bseg;
+        const int abx_i = r.raw_x[i + 1] - r.raw_x[i], aby_i = r.raw_y[i + 1] - r.raw_y[i];
+        const double ax = r.raw_x[i], ay = r.raw_y[i];
+        const double tt = d_clip(((x - ax) * abx_i + (y - ay) * aby_i) / ((double)(abx_i * abx_i + aby_i * aby_i) + 1e-9), 0, 1);
+        s_t = r.raw_cum[i] + tt * sqrt((double)(abx_i * abx_i + aby_i * aby_i));
+      }
+      if (!hi[CBEV_HI_S_PREV_VALID]) {
+        hd[CBEV_HD_S_PREV] = s_t;
+        hi[CBEV_HI_S_PREV_VALID] = 1;
+      }
+      double rc_raw = d_pymax(0.0, s_t - hd[CBEV_HD_S_PREV]);
+      hd[CBEV_HD_S_PREV] = s_t;
+      double total = r.raw_cum[nraw - 1];
+      double RC = total > 0 ? rc_raw / total : 0.0;
+      RC = d_clip(RC * 100, 0.0, 1.0);
+      double d2r = d_lateral_error(x, y, r.cx + tidx, r.cy + tidx, nw);
+      double dist_m = fabs(d2r) * CB_MPP;
+      double p_route = dist_m <= 0.0 ? 1.0 : d_pymax(P.lane_center_floor, 1.0 - pow(dist_m / 3.0, P.lane_center_exponent));
+      bool off_lane = (tile == 2) || (dist_m > (1.5 * 3.0));
+      double p_off = off_lane ? P.off_lane_penalty : 1.0;
+      double speed_mps = v * CB_MPP;
+      double limit = 35.0 / 3.6;
+      double over = d_pymax(speed_mps - limit, 0.0);
+      double p_speed = over <= 0.0 ? 1.0 : d_pymax(P.speed_penalty_floor, exp(-over / P.speed_penalty_scale));
+      double p_ttc = ttc_carl < P.ttc_threshold ? 0.5 : 1.0;
+      p_ttc = d_pymax(P.ttc_penalty_floor, p_ttc);
+      double p_comfort = nviol > 0 ? 1.0 - 0.5 * (nviol / 6.0) : 1.0;
+      double Pt = 1.0;
+      Pt *= p_route;
+      Pt *= p_off;
+      Pt *= p_speed;
+      Pt *= p_ttc;
+      Pt *= p_comfort;
+      reward = d_clip(RC * Pt, 0.0, 1.0);
+      hd[CBEV_HD_RC] = RC;
+      hd[CBEV_HD_P_LANE] = p_route;
+      hd[CBEV_HD_P_OFF] = p_off;
+      hd[CBEV_HD_P_SPEED] = p_speed;
+      hd[CBEV_HD_P_TTC] = p_ttc;
+      hd[CBEV_HD_P_COMFORT] = p_comfort;
+      hd[CBEV_HD_TTC] = ttc_carl;
+      hd[CBEV_HD_DIST2ROUTE] = d2r;
+    }
+  } else {  // ---- RewardFn.step (shaping)
+    int k = hi[CBEV_HI_KSTEPS] + 1;
+    hi[CBEV_HI_KSTEPS] = k;
+    reward = -0.002;
+    if (k >= P.max_actions) {
+      reward = 0.0;
+      cause = CBEV_CAUSE_MAX_ACTIONS;
+    } else if (dist2wp > 60) {
+      reward = -1.0;
+      cause = CBEV_CAUSE_OUT_OF_BOUNDS;
+    } else if (tile == 0) {
+      reward = -1.0;
+      cause = CBEV_CAUSE_COLLISION;
+    } else if (result != CBEV_COLL_NONE) {
+      if (result == CBEV_COLL_PEDESTRIAN) { reward = -20.0; cause = CBEV_CAUSE_COLLISION; }
+      else if (result == CBEV_COLL_VEHICLE) { reward = -12.0; cause = CBEV_CAUSE_COLLISION; }
+      else if (coll_id == -2) { reward = 18.0; cause = CBEV_CAUSE_SUCCESS; }
+      else { reward = 0.7; cause = CBEV_CAUSE_CKPT; }
+    } else {
+      const bool on_sw = tile == 2;
+      int off = hi[CBEV_HI_OFFROAD];
+      if (on_sw) {
+        off += 1;
+        reward += (P.sidewalk_step_penalty + P.sidewalk_penalty_scale * off);
+      } else {
+        off = 0;
+      }
+      hi[CBEV_HI_OFFROAD] = off;
+      if (P.offroad_terminate_after && off >= P.offroad_terminate_after) {
+        reward -= 0.7;
+        cause = CBEV_CAUSE_OFF_ROAD;
+      } else {
+        double rr = 0.0;
+        const double yaw1 = hd[CBEV_HD_YAW1], v1 = hd[CBEV_HD_V1];
+        double yaw_error = atan2(sin(spyaw - yaw), cos(spyaw - yaw));
+        double align = cos(yaw_error);
+        double d2r = d_lateral_error(x, y, r.cx + tidx, r.cy + tidx, nw);
+        double ee = d_clip(fabs(d2r), 0.0, P.lat_clip);
+        rr -= P.k_lat_quadratic * (ee * ee);
+        if (dist2wp > P.route_dev_start) rr -= P.k_route_dev * (dist2wp - P.route_dev_start);
+        double dprog = hd[CBEV_HD_D2G_T1] - hd[CBEV_HD_D2G];
+        if (dprog > 0 && !(on_sw && P.zero_progress_reward_offroad)) rr += P.k_progress * dprog * d_pymax(0.0, align);
+        if (v > 0.3 && !(on_sw && P.zero_speed_reward_offroad))
+          rr += P.k_flow * (v < P.max_speed_for_flow ? v : P.max_speed_for_flow) * d_pymax(0.0, align);
+        if (ee < P.lat_small && fabs(yaw_error) < P.yaw_small) rr += P.k_align_bonus;
+        double ttc_term = ttc_sh < INFINITY ? -exp(-ttc_sh / 30) : 0.0;
+        rr += P.k_ttc * ttc_term;
+        if (v < -0.1) rr += -P.k_reverse * fabs(v);
+        double dyaw = yaw1 - yaw;
+        double jerk = fabs(dyaw - hd[CBEV_HD_LAST_DYAW]);
+        hd[CBEV_HD_LAST_DYAW] = dyaw;
+        rr -= P.k_steer_smooth * fabs(dyaw);
+        rr -= P.k_steer_jerk * jerk;
+        rr += -P.k_smooth * (fabs(v1 - v) + fabs(dyaw));
+        rr += P.alive_bias;
+        reward += tanh(rr * 1.2);
+      }
+      reward = d_clip(reward, -1.0, 1.0);
+    }
+  }
+  hd[CBEV_HD_REWARD] = reward;
+  // Stats.step accumulators (stats.py:30-56)
+  hd[CBEV_HD_EP_RETURN] += reward;
+  hd[CBEV_HD_EP_SPEED] += v;
+  hd[CBEV_HD_EP_ABS_AL] += fabs(al);
+  hd[CBEV_HD_EP_ABS_ALAT] += fabs(alat);
+  hd[CBEV_HD_EP_ABS_JL] += fabs(jl);
+  hd[CBEV_HD_EP_ABS_JLAT] += fabs(jlat);
+  hd[CBEV_HD_EP_ABS_YR] += fabs(yr);
+  hd[CBEV_HD_EP_ABS_YACC] += fabs(yacc);
+  hd[CBEV_HD_EP_VIOL] += nviol > 0 ? 1.0 : 0.0;
+  hd[CBEV_HD_EP_HARSH] += al < -2.0 ? 1.0 : 0.0;
+  hi[CBEV_HI_EP_LEN] += 1;
+  if (cause != CBEV_CAUSE_NONE) hi[CBEV_HI_CAUSE] = cause;
+  // _check_termination (carlabev.py:177-185)
+  const int terminal = cause == CBEV_CAUSE_MAX_ACTIONS || cause == CBEV_CAUSE_COLLISION || cause == CBEV_CAUSE_SUCCESS ||
+                       cause == CBEV_CAUSE_OUT_OF_BOUNDS || cause == CBEV_CAUSE_OFF_ROAD;
+  hi[CBEV_HI_TERM] = terminal;
+  hi[CBEV_HI_TRUNC] = terminal && cause == CBEV_CAUSE_MAX_ACTIONS;
+  hi[CBEV_HI_STEP] += 1;
+  reward_out[e] = reward;
+  term_out[e] = (uint8_t)terminal;
+  trunc_out[e] = (uint8_t)(terminal && cause == CBEV_CAUSE_MAX_ACTIONS);
+  cause_out[e] = cause;
+  if (info_out != nullptr) {
+    float* o = info_out + (int64_t)e * CBEV_INFO_FLOATS;
+    for (int k = 0; k < 7; ++k) o[k] = (float)hd[CBEV_HD_C_SPEED + k];
+    for (int k = 0; k < 4; ++k) o[7 + k] = (float)hd[CBEV_HD_U_GAS + k];
+    o[11] = (float)reward;
+    o[12] = (float)dist2wp;
+    o[13] = (float)tile;
+    o[14] = (float)result;
+    o[15] = (float)nas;
+  }
+}
+
+// ============================================================== reset / ring / expansion
+__global__ __launch_bounds__(256) void k_copy_records(uint8_t* __restrict__ recs, int n, const uint8_t* __restrict__ bank,
+                                                      int n_bank, const uint8_t* __restrict__ mask,
+                                                      const int32_t* __restrict__ bank_idx, int64_t rb) {
+  const int e = blockIdx.x;
+  if (e >= n) return;
+  if (mask != nullptr && mask[e] == 0) return;
+  int b = bank_idx[e];
+  b = b < 0 ? 0 : (b >= n_bank ? n_bank - 1 : b);
+  const uint4* src = (const uint4*)(bank + (int64_t)b * rb);
+  uint4* dst = (uint4*)(recs + (int64_t)e * rb);
+  for (int64_t i = threadIdx.x; i < rb / 16; i += 256) dst[i] = src[i];
+}
+
+__global__ __launch_bounds__(256) void k_fill_ring(uint8_t* __restrict__ ring, int n, int F, const uint8_t* __restrict__ frames,
+                                                   const uint8_t* __restrict__ mask, int SS) {
+  const int e = blockIdx.x;
+  if (e >= n) return;
+  if (mask != nullptr && mask[e] == 0) return;
+  const uint4* src = (const uint4*)(frames + (int64_t)e * SS);
+  for (int f = 0; f < F; ++f) {
+    uint4* dst = (uint4*)(ring + ((int64_t)f * n + e) * SS);
+    if ((const uint8_t*)dst == (const uint8_t*)src) continue;
+    for (int i = threadIdx.x; i < SS / 16; i += 256) dst[i] = src[i];
+  }
+}
+
+// semantic one-hot + frame stack + flatten: out[e][f*C + c][p] (rgb_to_semantic.py:65-142,256-272)
+__global__ __launch_bounds__(256) void k_expand_semantic(const uint8_t* __restrict__ ring, int n, int F, int head, int C,
+                                                         int SS, const uint32_t* __restrict__ lut,
+                                                         float* __restrict__ out) {
+  const int64_t total4 = (int64_t)n * F * (SS / 4);
+  for (int64_t q = blockIdx.x * 256ll + threadIdx.x; q < total4; q += (int64_t)gridDim.x * 256) {
+    const int64_t p4 = q % (SS / 4);
+    const int64_t ef = q / (SS / 4);
+    const int f = (int)(ef % F);
+    const int64_t e = ef / F;
+    const int slot = (head + 1 + f) % F;  // oldest first
+    const uint32_t ids = *(const uint32_t*)(ring + ((int64_t)slot * n + e) * SS + p4 * 4);
+    uint32_t m[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) m[k] = lut[(ids >> (8 * k)) & 15];
+    float* o = out + ((e * F + f) * C) * (int64_t)SS + p4 * 4;
+    for (int c = 0; c < C; ++c) {
+      float4 v4 = make_float4((float)((m[0] >> c) & 1), (float)((m[1] >> c) & 1), (float)((m[2] >> c) & 1),
+                              (float)((m[3] >> c) & 1));
+      *(float4*)(o + (int64_t)c * SS) = v4;
+    }
+  }
+}
+
+// grayscale + frame stack: out[e][f][p] (uint8)
+__global__ __launch_bounds__(256) void k_expand_gray(const uint8_t* __restrict__ ring, int n, int F, int head, int SS,
+                                                     const uint32_t* __restrict__ lut, uint8_t* __restrict__ out) {
+  const int64_t total16 = (int64_t)n * F * (SS / 16);
+  for (int64_t q = blockIdx.x * 256ll + threadIdx.x; q < total16; q += (int64_t)gridDim.x * 256) {
+    const int64_t p16 = q % (SS / 16);
+    const int64_t ef = q / (SS / 16);
+    const int f = (int)(ef % F);
+    const int64_t e = ef / F;
+    const int slot = (head + 1 + f) % F;
+    uint4 ids = *(const uint4*)(ring + ((int64_t)slot * n + e) * SS + p16 * 16);
+    uint32_t in[4] = {ids.x, ids.y, ids.z, ids.w}, o[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      o[k] = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[k] |= (lut[(in[k] >> (8 * j)) & 15] & 255u) << (8 * j);
+    }
+    *(uint4*)(out + (e * F + f) * (int64_t)SS + p16 * 16) = make_uint4(o[0], o[1], o[2], o[3]);
+  }
+}
+
+// RGB of the newest frame: out[e][p][3]
+__global__ __launch_bounds__(256) void k_expand_rgb(const uint8_t* __restrict__ ring, int n, int head, int SS,
+                                                    const uint32_t* __restrict__ lut, uint8_t* __restrict__ out) {
+  const int64_t total = (int64_t)n * SS;
+  for (int64_t q = blockIdx.x * 256ll + threadIdx.x; q < total; q += (int64_t)gridDim.x * 256) {
+    const int64_t e = q / SS, p = q % SS;
+    const uint32_t c = lut[ring[((int64_t)head * n + e) * SS + p] & 15];
+    uint8_t* o = out + q * 3;
+    o[0] = (uint8_t)(c >> 16);
+    o[1] = (uint8_t)(c >> 8);
+    o[2] = (uint8_t)c;
+  }
+}
+
+// ============================================================== host side
+#define CBEV_PROF_MAX 8192
+struct cbev_ctx {
+  cbev_params P;
+  cbev_caps C;
+  cbev_layout L;
+  int device;
+  uint8_t* map_dev;
+  int64_t map_bytes;
+  uint32_t* lut_dev;  // 16 entries
+  int prof_on;
+  int64_t prof_n;
+  hipEvent_t* prof_ev;  // 4 per recorded step
+};
+
+static thread_local std::string g_err;
+
+static int set_err(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                          \
+  do {                                                                                         \
+    hipError_t _e = (expr);                                                                    \
+    if (_e != hipSuccess) return set_err(CBEV_EHIP, "%s: %s", #expr, hipGetErrorString(_e)); \
+  } while (0)
+
+// hat-matrix row of the degree-p least-squares polynomial through w samples at
+// 0..w-1, evaluated at `pos` (normal equations in long double, host only)
+static void lsq_row(int w, int p, double pos, double* row) {
+  long double A[4][4] = {{0}};
+  for (int i = 0; i < w; ++i) {
+    long double xp[8];
+    xp[0] = 1.0L;
+    for (int k = 1; k < 8; ++k) xp[k] = xp[k - 1] * (long double)i;
+    for (int r = 0; r <= p; ++r)
+      for (int c = 0; c <= p; ++c) A[r][c] += xp[r + c];
+  }
+  const int m = p + 1;
+  long double inv[4][4] = {{0}};
+  for (int i = 0; i < m; ++i) inv[i][i] = 1.0L;
+  for (int col = 0; col < m; ++col) {
+    int piv = col;
+    for (int r2 = col + 1; r2 < m; ++r2)
+      if (fabsl(A[r2][col]) > fabsl(A[piv][col])) piv = r2;
+    for (int c = 0; c < m; ++c) {
+      long double t = A[col][c]; A[col][c] = A[piv][c]; A[piv][c] = t;
+      t = inv[col][c]; inv[col][c] = inv[piv][c]; inv[piv][c] = t;
+    }
+    long double d = A[col][col];
+    for (int c = 0; c < m; ++c) { A[col][c] /= d; inv[col][c] /= d; }
+    for (int r2 = 0; r2 < m; ++r2) {
+      if (r2 == col) continue;
+      long double f = A[r2][col];
+      for (int c = 0; c < m; ++c) { A[r2][c] -= f * A[col][c]; inv[r2][c] -= f * inv[col][c]; }
+    }
+  }
+  long double pp[4];
+  pp[0] = 1.0L;
+  for (int k = 1; k < 4; ++k) pp[k] = pp[k - 1] * (long double)pos;
+  for (int j = 0; j < w; ++j) {
+    long double xj[4];
+    xj[0] = 1.0L;
+    for (int k = 1; k < 4; ++k) xj[k] = xj[k - 1] * (long double)j;
+    long double acc = 0.0L;
+    for (int a = 0; a < m; ++a)
+      for (int b = 0; b < m; ++b) acc += pp[a] * inv[a][b] * xj[b];
+    row[j] = (double)acc;
+  }
+}
+
+static void build_sg_tables(SgTables* T) {
+  memset(T, 0, sizeof *T);
+  for (int w = 3; w <= 11; w += 2) {
+    const int ti = w / 2, h = w / 2, p = w - 1 < 3 ? w - 1 : 3;
+    lsq_row(w, p, (double)h, T->conv[ti]);
+    for (int i = 0; i < h; ++i) lsq_row(w, p, (double)i, T->left[ti][i]);
+    for (int k = 0; k < h; ++k) lsq_row(w, p, (double)(w - h + k), T->right[ti][k]);
+  }
+}
+
+static KArgs kargs(const cbev_ctx* c) {
+  KArgs K;
+  K.P = c->P;
+  K.C = c->C;
+  K.L = c->L;
+  K.map = c->map_dev;
+  return K;
+}
+
+static size_t raster_lds_bytes(const cbev_params& P) { return (size_t)P.crop * (size_t)((P.crop + 30) / 16) * 16; }
+
+extern "C" {
+
+int cbev_abi_version(void) { return CBEV_ABI_VERSION; }
+int cbev_params_size(void) { return (int)sizeof(cbev_params); }
+const char* cbev_last_error(void) { return g_err.c_str(); }
+
+int cbev_layout_of(const cbev_caps* caps, cbev_layout* out) {
+  if (!caps || !out) return set_err(CBEV_EINVAL, "null argument");
+  *out = cbev_make_layout(*caps);
+  return CBEV_OK;
+}
+
+#define CBEV_NAME_STR(n) #n ","
+const char* cbev_field_names(int group) {
+  static const char* hd = CBEV_HD_FIELDS(CBEV_NAME_STR);
+  static const char* hi = CBEV_HI_FIELDS(CBEV_NAME_STR);
+  static const char* ad = CBEV_AD_FIELDS(CBEV_NAME_STR);
+  static const char* ai = CBEV_AI_FIELDS(CBEV_NAME_STR);
+  static const char* ti = CBEV_TI_FIELDS(CBEV_NAME_STR);
+  switch (group) {
+    case 0: return hd;
+    case 1: return hi;
+    case 2: return ad;
+    case 3: return ai;
+    case 4: return ti;
+    default: return "";
+  }
+}
+
+int cbev_create(const cbev_params* params, const cbev_caps* caps, int device, cbev_ctx** out) {
+  if (!params || !caps || !out) return set_err(CBEV_EINVAL, "null argument");
+  const cbev_params& P = *params;
+  if (P.size <= 0 || P.size % 16 != 0) return set_err(CBEV_EINVAL, "size %d must be a positive multiple of 16", P.size);
+  if (P.crop < P.size || P.crop > 400) return set_err(CBEV_EINVAL, "crop %d out of range", P.crop);
+  if (P.map_pitch % 16 != 0 || P.map_pitch < P.render_w) return set_err(CBEV_EINVAL, "bad map pitch %d", P.map_pitch);
+  if (P.render_w != P.map_w + 2 * P.pad || P.render_h != P.map_h + 2 * P.pad) return set_err(CBEV_EINVAL, "bad render shape");
+  if (P.action_kind == 0 && (P.n_discrete < 1 || P.n_discrete > 16)) return set_err(CBEV_EINVAL, "bad n_discrete");
+  if (caps->route_cap < 2 || caps->actor_cap < 0 || caps->actor_route_cap < 0 || caps->tl_cap < 0)
+    return set_err(CBEV_EINVAL, "bad capacities");
+  if (caps->actor_cap > 0 && caps->actor_route_cap < 2) return set_err(CBEV_EINVAL, "actor_route_cap < 2");
+  if (raster_lds_bytes(P) > 160 * 1024) return set_err(CBEV_EINVAL, "crop %d needs more LDS than a CU has", P.crop);
+  HIP_TRY(hipSetDevice(device));
+  cbev_ctx* c = (cbev_ctx*)calloc(1, sizeof(cbev_ctx));
+  c->P = P;
+  c->C = *caps;
+  c->L = cbev_make_layout(*caps);
+  c->device = device;
+  SgTables T;
+  build_sg_tables(&T);
+  hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(c_sg), &T, sizeof T);
+  if (e == hipSuccess) e = hipMalloc(&c->lut_dev, 64 * sizeof(uint32_t));
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute((const void*)k_raster<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)raster_lds_bytes(P));
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute((const void*)k_raster<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)raster_lds_bytes(P));
+  if (e != hipSuccess) {
+    free(c);
+    return set_err(CBEV_EHIP, "cbev_create: %s", hipGetErrorString(e));
+  }
+  *out = c;
+  return CBEV_OK;
+}
+
+int cbev_profile(cbev_ctx* c, int enable) {
+  if (!c) return set_err(CBEV_EINVAL, "null argument");
+  HIP_TRY(hipSetDevice(c->device));
+  if (enable && !c->prof_ev) {
+    c->prof_ev = (hipEvent_t*)calloc(4 * CBEV_PROF_MAX, sizeof(hipEvent_t));
+    for (int i = 0; i < 4 * CBEV_PROF_MAX; ++i) HIP_TRY(hipEventCreate(&c->prof_ev[i]));
+  }
+  c->prof_on = enable ? 1 : 0;
+  c->prof_n = 0;
+  return CBEV_OK;
+}
+
+int cbev_profile_read(cbev_ctx* c, double* ms3, int64_t* steps) {
+  if (!c || !ms3) return set_err(CBEV_EINVAL, "null argument");
+  ms3[0] = ms3[1] = ms3[2] = 0.0;
+  if (steps) *steps = c->prof_n;
+  if (!c->prof_ev || c->prof_n == 0) return CBEV_OK;
+  HIP_TRY(hipEventSynchronize(c->prof_ev[4 * (c->prof_n - 1) + 3]));
+  for (int64_t i = 0; i < c->prof_n; ++i) {
+    for (int k = 0; k < 3; ++k) {
+      float ms = 0.f;
+      HIP_TRY(hipEventElapsedTime(&ms, c->prof_ev[4 * i + k], c->prof_ev[4 * i + k + 1]));
+      ms3[k] += ms;
+    }
+  }
+  return CBEV_OK;
+}
+
+void cbev_destroy(cbev_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  if (c->prof_ev) {
+    for (int i = 0; i < 4 * CBEV_PROF_MAX; ++i) (void)hipEventDestroy(c->prof_ev[i]);
+    free(c->prof_ev);
+  }
+  if (c->map_dev) (void)hipFree(c->map_dev);
+  if (c->lut_dev) (void)hipFree(c->lut_dev);
+  free(c);
+}
+
+int cbev_set_map(cbev_ctx* c, const uint8_t* map_host, int64_t bytes) {
+  if (!c || !map_host) return set_err(CBEV_EINVAL, "null argument");
+  const int64_t need = (int64_t)c->P.map_pitch * c->P.render_h;
+  if (bytes != need) return set_err(CBEV_EINVAL, "map bytes %lld != pitch*render_h %lld", (long long)bytes, (long long)need);
+  HIP_TRY(hipSetDevice(c->device));
+  if (c->map_dev) HIP_TRY(hipFree(c->map_dev));
+  c->map_dev = nullptr;
+  // slack after the last row: the 16-B staging loads of the last crop row may run
+  // up to 30 bytes past render_w
+  HIP_TRY(hipMalloc(&c->map_dev, need + 4096));
+  HIP_TRY(hipMemset(c->map_dev, 0, need + 4096));
+  HIP_TRY(hipMemcpy(c->map_dev, map_host, need, hipMemcpyHostToDevice));
+  c->map_bytes = need;
+  return CBEV_OK;
+}
+
+int cbev_step(cbev_ctx* c, void* records, int n, const void* actions, uint8_t* frames, double* reward, uint8_t* term,
+              uint8_t* trunc, int32_t* cause, float* info, void* stream) {
+  if (!c || !records || !actions || !frames || !reward || !term || !trunc || !cause)
+    return set_err(CBEV_EINVAL, "null argument");
+  if (!c->map_dev) return set_err(CBEV_ESTATE, "cbev_set_map not called");
+  if (n <= 0) return CBEV_OK;
+  hipStream_t s = (hipStream_t)stream;
+  KArgs K = kargs(c);
+  const int wg4 = (n + 3) / 4;
+  hipEvent_t* ev = nullptr;
+  if (c->prof_on && c->prof_n < CBEV_PROF_MAX) ev = c->prof_ev + 4 * c->prof_n++;
+  if (ev) HIP_TRY(hipEventRecord(ev[0], s));
+  hipLaunchKernelGGL(k_dyn, dim3(wg4), dim3(256), 0, s, K, (uint8_t*)records, n, actions);
+  if (ev) HIP_TRY(hipEventRecord(ev[1], s));
+  hipLaunchKernelGGL(k_raster<false>, dim3(n), dim3(256), raster_lds_bytes(c->P), s, K, (uint8_t*)records, n, frames,
+                     (const uint8_t*)nullptr);
+  if (ev) HIP_TRY(hipEventRecord(ev[2], s));
+  hipLaunchKernelGGL(k_collide, dim3(wg4), dim3(256), 0, s, K, (uint8_t*)records, n, reward, term, trunc, cause, info);
+  if (ev) HIP_TRY(hipEventRecord(ev[3], s));
+  HIP_TRY(hipGetLastError());
+  return CBEV_OK;
+}
+
+int cbev_reset(cbev_ctx* c, void* records, int n, const void* bank, int n_bank, const uint8_t* mask,
+               const int32_t* bank_idx, uint8_t* frames, void* stream) {
+  if (!c || !records || !frames) return set_err(CBEV_EINVAL, "null argument");
+  if (!c->map_dev) return set_err(CBEV_ESTATE, "cbev_set_map not called");
+  if (bank && (!bank_idx || n_bank <= 0)) return set_err(CBEV_EINVAL, "bank without bank_idx");
+  if (n <= 0) return CBEV_OK;
+  hipStream_t s = (hipStream_t)stream;
+  KArgs K = kargs(c);
+  if (bank)
+    hipLaunchKernelGGL(k_copy_records, dim3(n), dim3(256), 0, s, (uint8_t*)records, n, (const uint8_t*)bank, n_bank, mask,
+                       bank_idx, (int64_t)c->L.record_bytes);
+  hipLaunchKernelGGL(k_raster<true>, dim3(n), dim3(256), raster_lds_bytes(c->P), s, K, (uint8_t*)records, n, frames, mask);
+  HIP_TRY(hipGetLastError());
+  return CBEV_OK;
+}
+
+int cbev_fill_ring(cbev_ctx* c, uint8_t* ring, int n, int n_frames, const uint8_t* frames, const uint8_t* mask,
+                   void* stream) {
+  if (!c || !ring || !frames || n_frames < 1) return set_err(CBEV_EINVAL, "bad argument");
+  if (n <= 0) return CBEV_OK;
+  const int SS = c->P.size * c->P.size;
+  hipLaunchKernelGGL(k_fill_ring, dim3(n), dim3(256), 0, (hipStream_t)stream, ring, n, n_frames, frames, mask, SS);
+  HIP_TRY(hipGetLastError());
+  return CBEV_OK;
+}
+
+int cbev_expand_obs(cbev_ctx* c, const uint8_t* ring, int n, int n_frames, int head, int kind, int n_channels,
+                    const uint32_t* lut_host, void* out, void* stream) {
+  if (!c || !ring || !out || !lut_host) return set_err(CBEV_EINVAL, "null argument");
+  if (n_frames < 1 || head < 0 || head >= n_frames) return set_err(CBEV_EINVAL, "bad frame ring");
+  if (kind == 0 && (n_channels < 1 || n_channels > 16)) return set_err(CBEV_EINVAL, "bad channel count");
+  if (n <= 0) return CBEV_OK;
+  hipStream_t s = (hipStream_t)stream;
+  HIP_TRY(hipMemcpyAsync(c->lut_dev, lut_host, 16 * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+  const int SS = c->P.size * c->P.size;
+  const int grid = 2048;
+  if (kind == 0)
+    hipLaunchKernelGGL(k_expand_semantic, dim3(grid), dim3(256), 0, s, ring, n, n_frames, head, n_channels, SS, c->lut_dev,
+                       (float*)out);
+  else if (kind == 1)
+    hipLaunchKernelGGL(k_expand_gray, dim3(grid), dim3(256), 0, s, ring, n, n_frames, head, SS, c->lut_dev, (uint8_t*)out);
+  else if (kind == 2)
+    hipLaunchKernelGGL(k_expand_rgb, dim3(grid), dim3(256), 0, s, ring, n, head, SS, c->lut_dev, (uint8_t*)out);
+  else
+    return set_err(CBEV_EINVAL, "unknown expansion kind %d", kind);
+  HIP_TRY(hipGetLastError());
+  return CBEV_OK;
+}
+
+}  // extern "C"

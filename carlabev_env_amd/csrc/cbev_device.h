@@ -1,0 +1,189 @@
+// cbev_device.h — device-side arithmetic of the batched CarlaBEV step (gfx950).
+//
+// Second, independent restatement (the first is the CPU oracle, oracle/) of
+// the reference's per-env arithmetic, written for wave64 execution: one
+// wavefront per environment, scalar hero math on lane 0, one lane per actor,
+// wave-wide reductions for the route arg-min searches. Float64 throughout like
+// the reference (Python/NumPy doubles); compiled with -ffp-contract=off so the
+// operation order below is the rounding order.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/cbev_layout.h"
+
+#define CB_DT 0.1
+#define CB_WHEELBASE 2.9
+#define CB_MPP 0.3125  /* 40/128, exact */
+#define CB_PI 3.141592653589793
+
+struct KArgs {
+  cbev_params P;
+  cbev_caps C;
+  cbev_layout L;
+  const uint8_t* map;  // padded class map, render_h rows x map_pitch bytes
+};
+
+// Savitzky-Golay hat-matrix rows for window w = 3,5,..,11 (index w/2),
+// polyorder min(3, w-1): interior centre weights and the rows that evaluate
+// the edge polynomial fits (scipy savgol_filter mode='interp').
+struct SgTables {
+  double conv[6][11];
+  double left[6][5][11];
+  double right[6][5][11];
+};
+extern __constant__ SgTables c_sg;
+
+struct DRec {
+  double* hd;
+  int32_t* hi;
+  double *cx, *cy, *cyaw, *raw_cum;
+  int32_t *raw_x, *raw_y;
+  uint32_t* vis;
+  double* ad;
+  int32_t* ai;
+  double *acx, *acy, *acyaw, *aix, *aiy, *arx, *ary;
+  int32_t* ti;
+  int A, RA, T;
+};
+
+__device__ __forceinline__ DRec bind_rec(uint8_t* base, const cbev_layout& L, const cbev_caps& C) {
+  DRec r;
+  r.hd = (double*)(base + L.hd);
+  r.hi = (int32_t*)(base + L.hi);
+  r.cx = (double*)(base + L.cx);
+  r.cy = (double*)(base + L.cy);
+  r.cyaw = (double*)(base + L.cyaw);
+  r.raw_x = (int32_t*)(base + L.raw_x);
+  r.raw_y = (int32_t*)(base + L.raw_y);
+  r.raw_cum = (double*)(base + L.raw_cum);
+  r.vis = (uint32_t*)(base + L.vis);
+  r.ad = (double*)(base + L.ad);
+  r.ai = (int32_t*)(base + L.ai);
+  r.acx = (double*)(base + L.acx);
+  r.acy = (double*)(base + L.acy);
+  r.acyaw = (double*)(base + L.acyaw);
+  r.aix = (double*)(base + L.aix);
+  r.aiy = (double*)(base + L.aiy);
+  r.arx = (double*)(base + L.arx);
+  r.ary = (double*)(base + L.ary);
+  r.ti = (int32_t*)(base + L.ti);
+  r.A = C.actor_cap;
+  r.RA = C.actor_route_cap;
+  r.T = C.tl_cap;
+  return r;
+}
+
+#define RAD(r, f, a) ((r).ad[(f) * (r).A + (a)])
+#define RAI(r, f, a) ((r).ai[(f) * (r).A + (a)])
+
+// ---------------------------------------------------------------- NumPy semantics
+// npy_remainder: Python-style modulo (sign of the divisor)
+__device__ __forceinline__ double d_remainder(double a, double b) {
+  double m = fmod(a, b);
+  if (m != 0.0) {
+    if ((b < 0) != (m < 0)) m += b;
+  } else {
+    m = copysign(0.0, b);
+  }
+  return m;
+}
+// control/utils.py:66-86
+__device__ __forceinline__ double d_angle_mod(double x) { return d_remainder(x + CB_PI, 2.0 * CB_PI) - CB_PI; }
+// np.clip = minimum(maximum(a, lo), hi)
+__device__ __forceinline__ double d_clip(double a, double lo, double hi) {
+  double t = (a != a) ? a : (a < lo ? lo : a);
+  return (t != t) ? t : (t > hi ? hi : t);
+}
+__device__ __forceinline__ double d_pymax(double a, double b) { return (b > a) ? b : a; }
+__device__ __forceinline__ double d_degrees(double r) { return r * (180.0 / CB_PI); }
+__device__ __forceinline__ double d_radians(double d) { return d * (CB_PI / 180.0); }
+
+// ---------------------------------------------------------------- wave reductions
+// lexicographic (value, index) minimum across the 64 lanes: the global
+// first-occurrence minimum, i.e. np.argmin semantics
+__device__ __forceinline__ void wave_argmin(double& v, int& i) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    double ov = __shfl_xor(v, off, 64);
+    int oi = __shfl_xor(i, off, 64);
+    if (ov < v || (ov == v && oi < i)) {
+      v = ov;
+      i = oi;
+    }
+  }
+}
+__device__ __forceinline__ double wave_min(double v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    double o = __shfl_xor(v, off, 64);
+    v = o < v ? o : v;
+  }
+  return v;
+}
+__device__ __forceinline__ int wave_max_i(int v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    int o = __shfl_xor(v, off, 64);
+    v = o > v ? o : v;
+  }
+  return v;
+}
+__device__ __forceinline__ int wave_sum_i(int v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+// ---------------------------------------------------------------- kinematics
+// State.update (src/control/state.py:29-51); s = x,y,yaw,v,x1,y1,yaw1,v1
+__device__ __forceinline__ void d_state_update(double* s, double acc, double delta, double ts) {
+  const double max_steer = 30.0 * (CB_PI / 180.0);
+  delta = d_clip(delta, -max_steer, max_steer);
+  s[4] = s[0];
+  s[5] = s[1];
+  s[6] = s[2];
+  s[7] = s[3];
+  s[0] += s[3] * cos(s[2]) * CB_DT;
+  s[1] += s[3] * sin(s[2]) * CB_DT;
+  s[2] += s[3] / CB_WHEELBASE * tan(delta) * CB_DT;
+  s[3] += acc * CB_DT;
+  s[2] = d_angle_mod(s[2]);
+  s[3] = d_clip(s[3], -1.0 * ts, ts);
+}
+
+// Controller.calc_target_index on one lane (serial over the route)
+__device__ __forceinline__ int d_target_index_serial(double x, double y, double yaw, const double* cx,
+                                                     const double* cy, int n, double* err) {
+  double fx = x + CB_WHEELBASE * cos(yaw);
+  double fy = y + CB_WHEELBASE * sin(yaw);
+  int best = 0;
+  double bd = 0.0;
+  for (int i = 0; i < n; ++i) {
+    double d = hypot(fx - cx[i], fy - cy[i]);
+    if (i == 0 || d < bd) {
+      bd = d;
+      best = i;
+    }
+  }
+  if (err) {
+    double fa0 = -cos(yaw + CB_PI / 2.0), fa1 = -sin(yaw + CB_PI / 2.0);
+    *err = (fx - cx[best]) * fa0 + (fy - cy[best]) * fa1;
+  }
+  return best;
+}
+
+// Controller.stanley_control (stanley_controller.py:64-89), serial
+__device__ __forceinline__ double d_stanley_serial(double x, double y, double yaw, double v, const double* cx,
+                                                   const double* cy, const double* cyaw, int n, int tidx,
+                                                   int* idx_out) {
+  double err;
+  int cur = d_target_index_serial(x, y, yaw, cx, cy, n, &err);
+  if (tidx >= cur) cur = tidx;
+  double theta_e = d_angle_mod(cyaw[cur] - yaw);
+  double theta_d = atan2(2.0 * err, d_pymax(v, 1e-3));
+  const double max_steer = 30.0 * (CB_PI / 180.0);
+  *idx_out = cur;
+  return d_clip(theta_e + theta_d, -max_steer, max_steer);
+}

@@ -81,13 +81,14 @@ def _rng_state(g: np.random.Generator) -> dict:
 class RoadGrid:
     """Road-centre cell graph over the 128-scale Town01 class map."""
 
-    def __init__(self, map_name: str = "Town01", cell: int = 12, margin: float = 8.0, n_sources: int = 96,
-                 seed: int = 12345):
+    def __init__(self, map_name: str = "Town01", cell: int = 4, margin: float = 6.0, stride: int = 3,
+                 n_sources: int = 128, seed: int = 12345):
         classes = load_class_map(map_name, 128)
         self.h, self.w = classes.shape
         drivable = classes == 1
         dist = ndimage.distance_transform_edt(drivable)
         self.cell = cell
+        self.stride = stride  # waypoint every stride*cell px (12.5 px lane-graph spacing in the reference)
         gh, gw = self.h // cell, self.w // cell
         cy = (np.arange(gh) * cell + cell // 2)
         cx = (np.arange(gw) * cell + cell // 2)
@@ -128,7 +129,11 @@ class RoadGrid:
             out.append(node)
             node = int(self.pred[si, node])
         out.append(src)
-        return self.node_xy[np.array(out[::-1])]
+        nodes = out[::-1]
+        keep = nodes[::self.stride]
+        if keep[-1] != nodes[-1]:
+            keep.append(nodes[-1])
+        return self.node_xy[np.array(keep)]
 
     def route_in_range(self, rng: random.Random, min_m: float, max_m: float, max_attempts: int = 100):
         """Random ego route whose length is within [min_m, max_m] meters
@@ -148,10 +153,11 @@ class RoadGrid:
                 return pts
         return None
 
-    def random_route(self, rng: random.Random, min_points: int = 6, max_points: int = 64):
+    def random_route(self, rng: random.Random, min_points: int = 6, max_points: int = 48):
         si = rng.randrange(len(self.sources))
         d = self.dist[si]
-        cand = np.flatnonzero(np.isfinite(d) & (d >= min_points - 1) & (d <= max_points - 1))
+        hops = self.stride
+        cand = np.flatnonzero(np.isfinite(d) & (d >= (min_points - 1) * hops) & (d <= (max_points - 2) * hops))
         if len(cand) == 0:
             return None
         target = int(cand[rng.randrange(len(cand))])

@@ -1,0 +1,368 @@
+"""Drop-in batched replacement of the reference's vector env.
+
+`make_env(cfg)` mirrors `CarlaBEV.envs.make_env` (`envs/__init__.py:108-120`):
+the reference returns a single-process `gymnasium.vector.SyncVectorEnv` over
+`num_envs` copies of `CarlaBEV` wrapped by `wrap_env` (Resize -> SemanticMask
+/ Grayscale -> FrameStack -> Flatten -> RecordEpisodeStatistics), with
+autoreset DISABLED. `CarlaBEVVectorEnv` exposes the same surface —
+`reset(seed, options)` with `options["reset_mask"]` partial resets,
+`step(actions) -> (obs, rewards, terminations, truncations, infos)`,
+`render()`, `close()`, `num_envs`, single/batched observation and action
+spaces — but every env's state lives in HBM and one step is three HIP
+launches through libcbev.so (include/cbev.h).
+
+Host/device split: scene generation and reset-time packing run on the host
+(`scene_gen`, `scene_pack`, as the reference's `src/managers/` does); the step,
+the observation raster, rewards, termination and the wrapper stack run on the
+GPU. Observations, rewards and flags are returned as torch tensors on the
+env's device (no host round trip); `infos` follow gymnasium's vector-info
+convention (`infos[key]` arrays + `infos["_key"]` masks).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import time
+from collections import deque
+
+import numpy as np
+import torch
+
+from . import layout as LY
+from ._lib import check, lib
+from .config import EnvConfig, RunConfig, validate_run_config, get_action_profile_spec
+from .params import CbevParams, build_params, load_class_map, padded_map
+from .host_reset import HostResetBuilder, route_length_m
+from .scene_gen import SceneGenerator
+from .semantics import gray_lut, rgb_lut, semantic_lut, semantic_mask_channels, PALETTE
+from .spaces import batch_space, make_box, make_discrete
+
+DEFAULT_CAPS = dict(route_cap=128, actor_cap=32, actor_route_cap=64, tl_cap=4)
+
+
+def _ptr(t: torch.Tensor | None):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+class _EpisodeHistory:
+    """Per-env mirror of `Stats` history (stats.py:87-125), updated only at termination."""
+
+    def __init__(self, maxlen: int = 200):
+        self.causes = deque(maxlen=maxlen)
+        self.returns = deque(maxlen=maxlen)
+        self.episode = 0
+
+
+class CarlaBEVVectorEnv:
+    metadata = {"autoreset_mode": "disabled", "render_modes": ["rgb_array"], "render_fps": 60}
+
+    def __init__(self, cfg, *, num_envs: int | None = None, device=None, caps: dict | None = None,
+                 info_mode: str = "full", scene_generator=None):
+        if isinstance(cfg, EnvConfig):
+            run = validate_run_config({"env": cfg})
+        elif isinstance(cfg, RunConfig):
+            run = validate_run_config(cfg)
+        elif isinstance(cfg, dict) and "env" in cfg:
+            run = validate_run_config(cfg)
+        else:
+            run = validate_run_config({"env": cfg})
+        self.run_cfg = run
+        self.cfg: EnvConfig = run.env
+        self.num_envs = int(num_envs if num_envs is not None else run.num_envs)
+        if tuple(self.cfg.obs_size) != (self.cfg.size, self.cfg.size):
+            raise NotImplementedError(
+                f"obs_size={tuple(self.cfg.obs_size)} != (size, size): the INTER_AREA resize wrapper is not "
+                "implemented on the device yet; use obs_size=(size, size)")
+        if self.cfg.temporal_fusion_mode != "stack":
+            raise NotImplementedError("temporal_fusion_mode other than 'stack' is not implemented on the device yet")
+        if self.cfg.fov_masked:
+            raise NotImplementedError("fov_masked=True is not implemented on the device yet")
+        self.info_mode = info_mode
+        if device is None:
+            if not torch.cuda.is_available():
+                raise RuntimeError("CarlaBEVVectorEnv needs a ROCm GPU (torch.cuda); there is no CPU fallback")
+            device = torch.device("cuda", torch.cuda.current_device())
+        self.device = torch.device(device)
+        self.S = int(self.cfg.size)
+        self.F = int(self.cfg.frame_stack)
+        self.classes = load_class_map(self.cfg.map_name, self.S)
+        self.params: CbevParams = build_params(self.cfg, self.classes)
+        self.map_host, pitch = padded_map(self.classes, self.params.pad)
+        assert pitch == self.params.map_pitch
+        c = dict(DEFAULT_CAPS)
+        c.update(caps or {})
+        self.caps = LY.Caps(**c)
+        self.layout = LY.Layout.make(self.caps)
+        self.rb = self.layout.record_bytes
+        L = lib()
+        ctx = ctypes.c_void_p()
+        check(L.cbev_create(ctypes.byref(self.params), ctypes.byref(self.caps.c()), self.device.index or 0,
+                            ctypes.byref(ctx)), "cbev_create")
+        self._ctx = ctx
+        check(L.cbev_set_map(ctx, self.map_host.ctypes.data_as(ctypes.c_void_p), self.map_host.nbytes), "cbev_set_map")
+        N, S, F = self.num_envs, self.S, self.F
+        dev = self.device
+        self.records = torch.zeros((N, self.rb), dtype=torch.uint8, device=dev)
+        self.ring = torch.zeros((F, N, S, S), dtype=torch.uint8, device=dev)
+        self.head = 0
+        self.reward = torch.zeros(N, dtype=torch.float64, device=dev)
+        self.term = torch.zeros(N, dtype=torch.uint8, device=dev)
+        self.trunc = torch.zeros(N, dtype=torch.uint8, device=dev)
+        self.cause = torch.zeros(N, dtype=torch.int32, device=dev)
+        self.info = torch.zeros((N, 16), dtype=torch.float32, device=dev)
+        # spaces (envs/spaces.py:27-61 + wrapper spaces)
+        aspec = get_action_profile_spec(self.cfg.action_profile_id)
+        self.discrete = aspec["action_mode"] == "discrete"
+        if self.discrete:
+            self.single_action_space = make_discrete(len(aspec["discrete_actions"]))
+        else:
+            self.single_action_space = make_box(np.asarray(aspec["low"], np.float32),
+                                                np.asarray(aspec["high"], np.float32), (3,), np.float32)
+        if self.cfg.masked:
+            self.channels = semantic_mask_channels(self.cfg.semantic_mask_ch)
+            C = len(self.channels)
+            self.single_observation_space = make_box(0.0, 1.0, (F * C, S, S), np.float32)
+            self._obs_kind, self._obs_lut, self._obs_ch = 0, semantic_lut(self.cfg.semantic_mask_ch), C
+            self.obs_buf = torch.zeros((N, F * C, S, S), dtype=torch.float32, device=dev)
+        else:
+            self.single_observation_space = make_box(0, 255, (F, S, S), np.uint8)
+            self._obs_kind, self._obs_lut, self._obs_ch = 1, gray_lut(), 1
+            self.obs_buf = torch.zeros((N, F, S, S), dtype=torch.uint8, device=dev)
+        self.observation_space = batch_space(self.single_observation_space, N)
+        self.action_space = batch_space(self.single_action_space, N)
+        seed = getattr(run, "seed", self.cfg.seed)
+        self.single_action_space.seed(seed)
+        self.generator = scene_generator or SceneGenerator(self.cfg, self.cfg.map_name)
+        self.builder = HostResetBuilder(self.cfg, self.classes, self.params, self.layout, self.generator)
+        self.history = [_EpisodeHistory() for _ in range(N)]
+        self.scene_context = [dict() for _ in range(N)]
+        self.num_vehicles = np.zeros(N, dtype=np.int64)
+        self.len_ego_route = np.zeros(N, dtype=np.float64)
+        self._t0 = np.full(N, time.perf_counter())
+        self.bank = None
+        self._bank_cursor = 0
+        self._closed = False
+
+    # ------------------------------------------------------------------ helpers
+    def _stream(self):
+        return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    def _new_record_buffer(self, n: int) -> np.ndarray:
+        return np.zeros((n, self.rb), dtype=np.uint8)
+
+    def build_reset_record(self, buf: np.ndarray, seed, options: dict, env_index: int = 0):
+        return self.builder.build(buf, seed, options)
+
+    def _mask_array(self, mask) -> np.ndarray:
+        if mask is None:
+            return np.ones(self.num_envs, dtype=bool)
+        if isinstance(mask, torch.Tensor):
+            mask = mask.detach().to("cpu").numpy()
+        m = np.asarray(mask, dtype=bool).reshape(-1)
+        if m.size != self.num_envs:
+            raise ValueError(f"reset_mask has {m.size} entries, expected {self.num_envs}")
+        return m
+
+    # ------------------------------------------------------------------ scene bank (device-side reset)
+    def attach_bank(self, bank_records: torch.Tensor, contexts=None):
+        """Use a pre-built scene bank (B packed records on this device) for partial resets
+        without per-reset host work."""
+        if bank_records.device != self.device or bank_records.dtype != torch.uint8 or bank_records.shape[1] != self.rb:
+            raise ValueError("bank must be a (B, record_bytes) uint8 tensor on the env device")
+        self.bank = bank_records.contiguous()
+        self.bank_contexts = contexts
+
+    def build_bank(self, seeds, options: dict | None = None) -> torch.Tensor:
+        options = dict(options or {})
+        host = self._new_record_buffer(len(seeds))
+        for k, s in enumerate(seeds):
+            self.build_reset_record(host[k], s, dict(options, scene_seed=int(s)))
+        return torch.from_numpy(host).to(self.device)
+
+    def reset_from_bank(self, mask: torch.Tensor | None = None, bank_idx: torch.Tensor | None = None):
+        """Device-only partial reset: env i (mask[i]) <- bank[bank_idx[i]]; no host sync."""
+        if self.bank is None:
+            raise RuntimeError("no scene bank attached")
+        N, B = self.num_envs, self.bank.shape[0]
+        if bank_idx is None:
+            bank_idx = (torch.arange(N, device=self.device, dtype=torch.int64) + self._bank_cursor) % B
+            bank_idx = bank_idx.to(torch.int32)
+            self._bank_cursor = (self._bank_cursor + N) % B
+        m = None if mask is None else mask.to(device=self.device, dtype=torch.uint8).contiguous()
+        s = self._stream()
+        frames = self.ring[self.head]
+        check(lib().cbev_reset(self._ctx, _ptr(self.records), N, _ptr(self.bank), B, _ptr(m), _ptr(bank_idx),
+                               _ptr(frames), s), "cbev_reset")
+        check(lib().cbev_fill_ring(self._ctx, _ptr(self.ring), N, self.F, _ptr(frames), _ptr(m), s), "cbev_fill_ring")
+        return self._obs()
+
+    # ------------------------------------------------------------------ gymnasium surface
+    def reset(self, seed=None, options=None):
+        options = dict(options or {})
+        mask = self._mask_array(options.pop("reset_mask", None))
+        N = self.num_envs
+        if seed is None:
+            seeds = [None] * N
+        elif isinstance(seed, (int, np.integer)):
+            seeds = [int(seed) + i for i in range(N)]
+        else:
+            seeds = list(seed)
+        idx = np.flatnonzero(mask)
+        host = self._new_record_buffer(max(len(idx), 1))
+        spawn_infos = []
+        for k, i in enumerate(idx):
+            info, spec, ctx = self.builder.build(host[k], seeds[i], options)
+            spawn_infos.append(info)
+            self.scene_context[i] = ctx
+            self.num_vehicles[i] = len(spec.vehicles)
+            self.len_ego_route[i] = route_length_m(spec)
+            self._t0[i] = time.perf_counter()
+        if len(idx):
+            staging = torch.from_numpy(host[:len(idx)]).to(self.device)
+            bank_idx = np.zeros(N, dtype=np.int32)
+            bank_idx[idx] = np.arange(len(idx), dtype=np.int32)
+            bidx = torch.from_numpy(bank_idx).to(self.device)
+            m = torch.from_numpy(mask.astype(np.uint8)).to(self.device)
+            s = self._stream()
+            frames = self.ring[self.head]
+            check(lib().cbev_reset(self._ctx, _ptr(self.records), N, _ptr(staging), len(idx), _ptr(m), _ptr(bidx),
+                                   _ptr(frames), s), "cbev_reset")
+            check(lib().cbev_fill_ring(self._ctx, _ptr(self.ring), N, self.F, _ptr(frames), _ptr(m), s),
+                  "cbev_fill_ring")
+        obs = self._obs()
+        infos = {}
+        if len(idx):
+            infos["spawn_validation"] = np.array([None] * N, dtype=object)
+            infos["_spawn_validation"] = mask.copy()
+            infos["scenario"] = np.array([None] * N, dtype=object)
+            infos["_scenario"] = mask.copy()
+            for k, i in enumerate(idx):
+                infos["spawn_validation"][i] = spawn_infos[k]
+                infos["scenario"][i] = self.scene_context[i]
+        return obs, infos
+
+    def _actions_tensor(self, actions) -> torch.Tensor:
+        a = torch.as_tensor(actions, device=self.device)
+        if self.discrete:
+            a = a.reshape(self.num_envs).to(torch.int32).contiguous()
+        else:
+            a = a.reshape(self.num_envs, 3).to(torch.float32).contiguous()
+        return a
+
+    def step_async_only(self, actions):
+        """Enqueue one step; returns nothing and never synchronises (bench path)."""
+        a = self._actions_tensor(actions)
+        self.head = (self.head + 1) % self.F
+        frames = self.ring[self.head]
+        check(lib().cbev_step(self._ctx, _ptr(self.records), self.num_envs, _ptr(a), _ptr(frames), _ptr(self.reward),
+                              _ptr(self.term), _ptr(self.trunc), _ptr(self.cause), _ptr(self.info), self._stream()),
+              "cbev_step")
+        return a
+
+    def step(self, actions):
+        self.step_async_only(actions)
+        obs = self._obs()
+        rew = self.reward.clone()
+        term = self.term.bool()
+        trunc = self.trunc.bool()
+        infos = self._step_infos(term) if self.info_mode == "full" else {}
+        if self.info_mode == "device":
+            infos = {"cause": self.cause.clone(), "comfort": self.info[:, :11].clone()}
+        return obs, rew, term, trunc, infos
+
+    def _obs(self):
+        check(lib().cbev_expand_obs(self._ctx, _ptr(self.ring), self.num_envs, self.F, self.head, self._obs_kind,
+                                    self._obs_ch, self._obs_lut.ctypes.data_as(ctypes.c_void_p), _ptr(self.obs_buf),
+                                    self._stream()), "cbev_expand_obs")
+        return self.obs_buf
+
+    def _step_infos(self, term: torch.Tensor) -> dict:
+        done = term.to("cpu").numpy()
+        if not done.any():
+            return {}
+        idx = np.flatnonzero(done)
+        rec = self.records[torch.from_numpy(idx).to(self.device)].to("cpu").numpy()
+        N = self.num_envs
+        ep = {}
+        cause_names = {v: k for k, v in LY.CAUSE.items()}
+        keys = ("episode", "termination", "return", "length", "mean_reward", "success_rate", "collision_rate",
+                "unfinished_rate", "mean_speed", "mean_ttc", "mean_progress", "mean_abs_accel_long",
+                "mean_abs_accel_lat", "mean_abs_jerk_long", "mean_abs_jerk_lat", "mean_abs_yaw_rate",
+                "mean_abs_yaw_acc", "comfort_violation_rate", "harsh_brake_rate", "num_vehicles", "len_ego_route")
+        for k in keys:
+            ep[k] = np.zeros(N, dtype=object if k == "termination" else np.float64)
+        r_ep = np.zeros(N)
+        l_ep = np.zeros(N, dtype=np.int64)
+        t_ep = np.zeros(N)
+        now = time.perf_counter()
+        for j, i in enumerate(idx):
+            v = LY.RecordView(rec[j], self.layout)
+            n = max(v.i("EP_LEN"), 1)
+            h = self.history[i]
+            # Stats.terminated(): summary over the history *before* this episode
+            hist_c = list(h.causes)
+            hist_r = list(h.returns)
+            cause = cause_names.get(v.i("CAUSE"))
+            ret = float(v.h("EP_RETURN"))
+            vals = {
+                "episode": h.episode, "termination": cause, "return": ret, "length": v.i("EP_LEN"),
+                "mean_reward": float(np.mean(hist_r)) if hist_r else 0.0,
+                "success_rate": hist_c.count("success") / len(hist_c) if hist_c else 0.0,
+                "collision_rate": hist_c.count("collision") / len(hist_c) if hist_c else 0.0,
+                "unfinished_rate": hist_c.count("off_road") / len(hist_c) if hist_c else 0.0,
+                "mean_speed": float(v.h("EP_SPEED")) / n, "mean_ttc": 0.0, "mean_progress": 0.0,
+                "mean_abs_accel_long": float(v.h("EP_ABS_AL")) / n, "mean_abs_accel_lat": float(v.h("EP_ABS_ALAT")) / n,
+                "mean_abs_jerk_long": float(v.h("EP_ABS_JL")) / n, "mean_abs_jerk_lat": float(v.h("EP_ABS_JLAT")) / n,
+                "mean_abs_yaw_rate": float(v.h("EP_ABS_YR")) / n, "mean_abs_yaw_acc": float(v.h("EP_ABS_YACC")) / n,
+                "comfort_violation_rate": float(v.h("EP_VIOL")) / n, "harsh_brake_rate": float(v.h("EP_HARSH")) / n,
+                "num_vehicles": float(self.num_vehicles[i]), "len_ego_route": float(self.len_ego_route[i]),
+            }
+            for k in keys:
+                ep[k][i] = vals[k]
+            h.causes.append(cause)
+            h.returns.append(ret)
+            h.episode += 1
+            r_ep[i], l_ep[i], t_ep[i] = ret, v.i("EP_LEN"), round(now - self._t0[i], 6)
+        return {"episode_info": ep, "_episode_info": done.astype(bool),
+                "episode": {"r": r_ep, "l": l_ep, "t": t_ep}, "_episode": done.astype(bool)}
+
+    def render(self):
+        """Tuple of per-env (S, S, 3) uint8 RGB frames, like SyncVectorEnv.render()."""
+        ids = self.ring[self.head].to("cpu").numpy()
+        rgb = PALETTE[ids]
+        return tuple(rgb[i] for i in range(self.num_envs))
+
+    def render_device(self) -> torch.Tensor:
+        out = torch.empty((self.num_envs, self.S, self.S, 3), dtype=torch.uint8, device=self.device)
+        check(lib().cbev_expand_obs(self._ctx, _ptr(self.ring), self.num_envs, self.F, self.head, 2, 3,
+                                    rgb_lut().ctypes.data_as(ctypes.c_void_p), _ptr(out), self._stream()),
+              "cbev_expand_obs")
+        return out
+
+    def frames(self) -> torch.Tensor:
+        """Newest palette-id frames (N, S, S) uint8 (compact observation)."""
+        return self.ring[self.head]
+
+    def records_host(self) -> np.ndarray:
+        return self.records.to("cpu").numpy()
+
+    def close(self):
+        if not self._closed and getattr(self, "_ctx", None):
+            torch.cuda.synchronize(self.device)
+            lib().cbev_destroy(self._ctx)
+            self._ctx = None
+            self._closed = True
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001
+            pass
+
+
+def make_env(cfg, eval: bool = False, **kwargs) -> CarlaBEVVectorEnv:  # noqa: A002 - reference signature
+    """Mirror of `CarlaBEV.envs.make_env(cfg, eval=False)` (envs/__init__.py:108-120)."""
+    env = CarlaBEVVectorEnv(cfg, **kwargs)
+    if eval:
+        env.single_action_space.seed(999)
+    return env

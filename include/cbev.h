@@ -1,0 +1,101 @@
+/*
+ * cbev.h — C-ABI of the MI355X batched CarlaBEV step (libcbev.so).
+ *
+ * The reference has no FFI: its "operator API" for this path is the Gymnasium
+ * surface of `CarlaBEV.envs.carlabev.CarlaBEV` wrapped by `make_env`
+ * (`CarlaBEV/envs/__init__.py:108-120`, a `SyncVectorEnv`). Each entry point
+ * below replaces the per-env Python call chain named next to it, batched over
+ * N environments whose state lives in device memory as fixed-size records
+ * (include/cbev_layout.h). The Python facade (carlabev_env_amd/vector_env.py)
+ * binds these symbols with ctypes; INTEGRATION.md shows the binding.
+ *
+ * Conventions: every buffer argument is a plain device pointer (HBM) unless
+ * named *_host; sizes are element counts; `stream` is a hipStream_t passed as
+ * void* (NULL = default stream). All launches are asynchronous on `stream`.
+ * Functions return 0 on success and a negative code on error; the message is
+ * available from cbev_last_error() (thread-local). Calls on one context are
+ * not re-entrant.
+ */
+#ifndef CBEV_H
+#define CBEV_H
+
+#include <stdint.h>
+
+#include "cbev_layout.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CBEV_ABI_VERSION 1
+
+typedef struct cbev_ctx cbev_ctx;
+
+/* error codes */
+enum { CBEV_OK = 0, CBEV_EINVAL = -1, CBEV_EHIP = -2, CBEV_ESTATE = -3 };
+
+int cbev_abi_version(void);
+int cbev_params_size(void);                         /* sizeof(cbev_params) */
+int cbev_layout_of(const cbev_caps* caps, cbev_layout* out);
+/* comma-separated field names of a record group: 0 HD, 1 HI, 2 AD, 3 AI, 4 TI */
+const char* cbev_field_names(int group);
+const char* cbev_last_error(void);
+
+/* Context = the static world of `CarlaBEV._setup` (carlabev.py:56-72):
+ * renderer geometry, action table, reward parameters, record capacities.
+ * Replaces `BaseMap.__init__` (world.py:33-67) + `build_reward_fn`. */
+int cbev_create(const cbev_params* params, const cbev_caps* caps, int device, cbev_ctx** out);
+void cbev_destroy(cbev_ctx* ctx);
+
+/* Upload the padded class map (render surface of world.py:_build_padded_render_map,
+ * one palette id per texel, render_h rows of map_pitch bytes). Host pointer,
+ * copied into context-owned HBM. Replaces load_map (envs/utils.py:49-62). */
+int cbev_set_map(cbev_ctx* ctx, const uint8_t* padded_map_host, int64_t bytes);
+
+/* One `CarlaBEV.step(action)` (carlabev.py:223-231) for n envs:
+ *   records      n state records (record_bytes each), updated in place
+ *   actions      int32[n] discrete indices, or float32[n][3] continuous
+ *   frames       uint8[n][S][S] palette-id observation (render(), carlabev.py:233-249)
+ *   reward       float64[n]; term, trunc uint8[n]; cause int32[n] (CBEV_CAUSE_*)
+ *   info         float32[n][CBEV_INFO_FLOATS] per-step comfort/control export or NULL */
+#define CBEV_INFO_FLOATS 16
+int cbev_step(cbev_ctx* ctx, void* records, int n, const void* actions, uint8_t* frames, double* reward,
+              uint8_t* term, uint8_t* trunc, int32_t* cause, float* info, void* stream);
+
+/* Reset the envs selected by mask (uint8[n], NULL = all):
+ *   if bank != NULL: records[i] = bank[bank_idx[i]] (device-side scene bank; bank_idx int32[n])
+ *   then render the reset observation (BaseMap.reset: theta = 0, no actors,
+ *   world.py:92-100) into frames[i].
+ * Replaces `CarlaBEV.reset` after scene generation (carlabev.py:96-148). */
+int cbev_reset(cbev_ctx* ctx, void* records, int n, const void* bank, int n_bank, const uint8_t* mask,
+               const int32_t* bank_idx, uint8_t* frames, void* stream);
+
+/* Copy frames[i] into every slot of a frame-stack ring for masked envs
+ * (FrameStackObservation padding_type="reset"). ring: uint8[F][n][S][S]. */
+int cbev_fill_ring(cbev_ctx* ctx, uint8_t* ring, int n, int n_frames, const uint8_t* frames, const uint8_t* mask,
+                   void* stream);
+
+/* Wrapper stack on the device (envs/__init__.py:62-83):
+ *   kind 0: semantic one-hot (rgb_to_semantic.py:65-142) + FrameStack + Flatten
+ *           -> float32[n][F*C][S][S]; channel_lut[id] = bitmask of channels set
+ *   kind 1: grayscale (gymnasium GrayscaleObservation) + FrameStack
+ *           -> uint8[n][F][S][S]; channel_lut[id] = gray value
+ *   kind 2: RGB (render(), no wrappers) -> uint8[n][S][S][3] of the newest frame;
+ *           channel_lut[id] = 0xRRGGBB
+ * ring holds F frames per env, slot `head` is the newest. */
+int cbev_expand_obs(cbev_ctx* ctx, const uint8_t* ring, int n, int n_frames, int head, int kind, int n_channels,
+                    const uint32_t* channel_lut_host, void* out, void* stream);
+
+/* Kernel timing with HIP events recorded on the step's own stream around each
+ * of the three step kernels (used by bench.py for the roofline figure).
+ * cbev_profile(ctx, 1) resets the counters and starts recording (up to 8192
+ * steps); cbev_profile_read synchronises on the last event and returns the
+ * summed milliseconds of [k_dyn, k_raster, k_collide] and the step count. */
+int cbev_profile(cbev_ctx* ctx, int enable);
+int cbev_profile_read(cbev_ctx* ctx, double* ms3, int64_t* steps);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* CBEV_H */

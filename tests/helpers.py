@@ -1,0 +1,63 @@
+"""Shared builders for the CPU and GPU tests (no GPU needed here)."""
+from __future__ import annotations
+
+import numpy as np
+
+from carlabev_env_amd import layout as LY
+from carlabev_env_amd.config import EnvConfig, RandomNavigationReset, build_random_navigation_options
+from carlabev_env_amd.host_reset import HostResetBuilder
+from carlabev_env_amd.params import build_params, load_class_map, padded_map
+from carlabev_env_amd.scene_gen import SceneGenerator
+
+CAPS_FULL = LY.Caps(128, 32, 64, 4)
+
+_GEN = {}
+
+
+def world(size=128, action_profile="discrete9_v1", reward_profile="carl_base_v1", anchor_y=0.5, caps=CAPS_FULL,
+          obs_mode="bev_semantic"):
+    action_mode = "continuous" if action_profile.startswith("continuous") else "discrete"
+    reward_mode = "carl" if reward_profile.startswith("carl") else "shaping"
+    cfg = EnvConfig(size=size, obs_size=(size, size), render_mode="rgb_array", action_mode=action_mode,
+                    action_profile_id=action_profile, reward_mode=reward_mode, reward_profile_id=reward_profile,
+                    ego_anchor_y_frac=anchor_y, obs_mode=obs_mode)
+    classes = load_class_map(cfg.map_name, size)
+    P = build_params(cfg, classes)
+    padded, pitch = padded_map(classes, P.pad)
+    assert pitch == P.map_pitch
+    layout = LY.Layout.make(caps)
+    if "gen" not in _GEN:
+        _GEN["gen"] = SceneGenerator(cfg, cfg.map_name)
+    builder = HostResetBuilder(cfg, classes, P, layout, _GEN["gen"])
+    return cfg, P, padded, layout, builder
+
+
+def scene_options(kind: str, k: int = 0) -> dict:
+    if kind in ("rt_no_traffic_v1", "rt_easy_v1", "rt_medium_v1", "rt_hard_v1"):
+        return build_random_navigation_options(RandomNavigationReset(difficulty_id=kind))
+    if kind == "mix3":  # config 5 scenario mix by env id
+        return {"scene": ("lead_brake", "jaywalk", "red_light_runner")[k % 3]}
+    return {"scene": kind}
+
+
+def build_records(builder, n: int, kinds, seed0: int = 0):
+    kinds = list(kinds)
+    return builder.build_many([seed0 + i for i in range(n)],
+                              lambda k, s: dict(scene_options(kinds[k % len(kinds)], k), scene_seed=s))
+
+
+def action_stream(P, n_envs: int, n_steps: int, seed: int = 1234, gas_bias: float = 4.0):
+    """Discrete indices (int32) or continuous float32 triplets, seeded per env."""
+    out = []
+    for e in range(n_envs):
+        rng = np.random.default_rng(seed + e)
+        if P.action_kind == 0:
+            p = np.ones(P.n_discrete)
+            p[1] += gas_bias
+            p /= p.sum()
+            out.append(rng.choice(P.n_discrete, size=n_steps, p=p).astype(np.int32))
+        else:
+            a = rng.uniform([0, -1, 0], [1, 1, 1], size=(n_steps, 3)).astype(np.float32)
+            a[:, 2] *= rng.random(n_steps) < 0.2
+            out.append(a)
+    return np.stack(out, axis=1)  # (steps, envs[, 3])

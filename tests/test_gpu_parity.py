@@ -1,0 +1,203 @@
+"""GPU parity: the HIP path (through the C-ABI) against the CPU oracle on the
+same seeded scenes and action streams.
+
+Bar: palette frames, termination/truncation flags, causes, collision results,
+tile ids, target indices, visibility bits and behaviour states bit-exact;
+float64 kinematic state and rewards within 1e-9 relative (device libm vs
+glibc may differ by one ulp in sin/cos/atan2/hypot; expression order and
+no-FMA compilation are identical on both sides).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+import oracle as O
+from carlabev_env_amd import layout as LY
+from carlabev_env_amd._lib import check, lib
+from carlabev_env_amd.semantics import gray_lut, rgb_lut, semantic_lut, rgb_to_semantic_mask_ids, PALETTE
+from helpers import CAPS_FULL, action_stream, build_records, world
+
+pytestmark = pytest.mark.gpu
+
+P_ = ctypes.c_void_p
+
+
+def ptr(t):
+    return P_(t.data_ptr()) if t is not None else None
+
+
+class DevWorld:
+    def __init__(self, P, padded, caps):
+        L = lib()
+        self.ctx = P_()
+        check(L.cbev_create(ctypes.byref(P), ctypes.byref(caps.c()), 0, ctypes.byref(self.ctx)), "create")
+        check(L.cbev_set_map(self.ctx, padded.ctypes.data_as(P_), padded.nbytes), "set_map")
+
+    def __del__(self):
+        lib().cbev_destroy(self.ctx)
+
+
+def compare_records(a: np.ndarray, b: np.ndarray, layout, tag=""):
+    va, vb = LY.RecordView(a, layout), LY.RecordView(b, layout)
+    ints = ("TIDX", "NROUTE", "NACT", "TILE", "COLLIDED", "ACTOR_ID", "CAUSE", "TERM", "TRUNC", "EP_LEN",
+            "HAS_PREV_COMFORT", "S_PREV_VALID", "KSTEPS", "OFFROAD", "NACTSTATE")
+    for k in ints:
+        assert va.i(k) == vb.i(k), (tag, k, va.i(k), vb.i(k))
+    assert np.array_equal(va.vis, vb.vis), (tag, "vis")
+    assert np.allclose(va.hd, vb.hd, rtol=1e-9, atol=1e-9, equal_nan=True), (
+        tag, [(n, va.hd[i], vb.hd[i]) for n, i in LY.HD.items()
+              if not np.isclose(va.hd[i], vb.hd[i], rtol=1e-9, atol=1e-9, equal_nan=True)])
+    n = va.i("NACT")
+    assert np.array_equal(va.ai[:, :n], vb.ai[:, :n]), (tag, "actor ints")
+    assert np.allclose(va.ad[:, :n], vb.ad[:, :n], rtol=1e-9, atol=1e-9), (tag, "actor doubles")
+
+
+def run_parity(kinds, n_envs, steps, size=128, profile="discrete9_v1", reward="carl_base_v1", seed0=0, anchor_y=0.5,
+               act_seed=1234):
+    cfg, P, padded, layout, builder = world(size, profile, reward, anchor_y)
+    recs, _ = build_records(builder, n_envs, kinds, seed0=seed0)
+    dw = DevWorld(P, padded, CAPS_FULL)
+    L = lib()
+    S = P.size
+    d_recs = torch.from_numpy(recs.copy()).cuda()
+    d_frames = torch.zeros((n_envs, S, S), dtype=torch.uint8, device="cuda")
+    check(L.cbev_reset(dw.ctx, ptr(d_recs), n_envs, None, 0, None, None, ptr(d_frames), None), "reset")
+    orc = O.Oracle(P, padded, CAPS_FULL.c(), layout.record_bytes)
+    h_frames = np.zeros((n_envs, S, S), np.uint8)
+    for e in range(n_envs):
+        orc.reset_obs(recs[e], h_frames[e])
+    torch.cuda.synchronize()
+    assert np.array_equal(d_frames.cpu().numpy(), h_frames), "reset frames differ"
+    acts = action_stream(P, n_envs, steps, seed=act_seed)
+    rew = torch.zeros(n_envs, dtype=torch.float64, device="cuda")
+    term = torch.zeros(n_envs, dtype=torch.uint8, device="cuda")
+    trunc = torch.zeros_like(term)
+    cause = torch.zeros(n_envs, dtype=torch.int32, device="cuda")
+    info = torch.zeros((n_envs, 16), dtype=torch.float32, device="cuda")
+    n_term = 0
+    for t in range(steps):
+        a = torch.from_numpy(np.ascontiguousarray(acts[t])).cuda()
+        check(L.cbev_step(dw.ctx, ptr(d_recs), n_envs, ptr(a), ptr(d_frames), ptr(rew), ptr(term), ptr(trunc),
+                          ptr(cause), ptr(info), None), "step")
+        for e in range(n_envs):
+            orc.step_one(recs[e], np.ascontiguousarray(acts[t, e]), h_frames[e])
+        torch.cuda.synchronize()
+        df = d_frames.cpu().numpy()
+        bad = np.argwhere(df != h_frames)
+        assert bad.size == 0, (t, bad[:8], df[tuple(bad[0])], h_frames[tuple(bad[0])])
+        dr = d_recs.cpu().numpy()
+        for e in range(n_envs):
+            compare_records(dr[e], recs[e], layout, tag=(t, e))
+        views = [LY.RecordView(recs[e], layout) for e in range(n_envs)]
+        assert np.array_equal(term.cpu().numpy(), np.array([v.i("TERM") for v in views], np.uint8))
+        assert np.array_equal(trunc.cpu().numpy(), np.array([v.i("TRUNC") for v in views], np.uint8))
+        assert np.allclose(rew.cpu().numpy(), [v.h("REWARD") for v in views], rtol=1e-9, atol=1e-12)
+        n_term += int(term.sum())
+    return n_term
+
+
+def test_parity_ego_only_config2():
+    assert run_parity(["rt_no_traffic_v1"], 48, 150, seed0=10_000) >= 0
+
+
+def test_parity_random_traffic_config3():
+    run_parity(["rt_hard_v1"], 32, 120, seed0=20_000, act_seed=7)
+
+
+def test_parity_continuous_medium_config4():
+    run_parity(["rt_medium_v1"], 24, 100, profile="continuous_gsb_v1", seed0=40_000, act_seed=99)
+
+
+def test_parity_scenarios_size256_config5():
+    run_parity(["mix3"], 24, 100, size=256, seed0=30_000)
+
+
+def test_parity_shaping_reward_and_offcentre_anchor():
+    run_parity(["rt_easy_v1", "jaywalk"], 16, 80, reward="shaping_base_v1", anchor_y=0.2, seed0=5)
+
+
+def test_bank_reset_and_wrapper_expansion():
+    cfg, P, padded, layout, builder = world()
+    n, B, F = 40, 7, 4
+    recs, _ = build_records(builder, n, ["rt_medium_v1"], seed0=300)
+    bank, _ = build_records(builder, B, ["rt_hard_v1", "jaywalk"], seed0=900)
+    dw = DevWorld(P, padded, CAPS_FULL)
+    L = lib()
+    S = P.size
+    d_recs = torch.from_numpy(recs.copy()).cuda()
+    d_bank = torch.from_numpy(bank.copy()).cuda()
+    ring = torch.zeros((F, n, S, S), dtype=torch.uint8, device="cuda")
+    mask = (torch.arange(n) % 3 == 0).to(torch.uint8).cuda()
+    bidx = (torch.arange(n) % B).to(torch.int32).cuda()
+    check(L.cbev_reset(dw.ctx, ptr(d_recs), n, ptr(d_bank), B, ptr(mask), ptr(bidx), ptr(ring[2]), None), "reset")
+    check(L.cbev_fill_ring(dw.ctx, ptr(ring), n, F, ptr(ring[2]), ptr(mask), None), "fill")
+    torch.cuda.synchronize()
+    dr = d_recs.cpu().numpy()
+    orc = O.Oracle(P, padded, CAPS_FULL.c(), layout.record_bytes)
+    m = mask.cpu().numpy().astype(bool)
+    for e in range(n):
+        if m[e]:
+            assert np.array_equal(dr[e], bank[e % B])
+            f = np.zeros((S, S), np.uint8)
+            orc.reset_obs(bank[e % B].copy(), f)
+            for s in range(F):
+                assert np.array_equal(ring[s, e].cpu().numpy(), f)
+        else:
+            assert np.array_equal(dr[e], recs[e])
+    # expansion kinds against host restatements
+    ring_h = torch.randint(0, 10, (F, n, S, S), dtype=torch.uint8)
+    ring_d = ring_h.cuda()
+    head = 1
+    order = [(head + 1 + f) % F for f in range(F)]
+    for mode in ("6-class", "7-class", "binary", "5-class"):
+        lut = semantic_lut(mode)
+        C = int(max(1, max(int(x).bit_length() for x in lut)))
+        C = {"6-class": 6, "7-class": 7, "binary": 1, "5-class": 5}[mode]
+        out = torch.zeros((n, F * C, S, S), dtype=torch.float32, device="cuda")
+        check(L.cbev_expand_obs(dw.ctx, ptr(ring_d), n, F, head, 0, C, lut.ctypes.data_as(P_), ptr(out), None), "exp")
+        torch.cuda.synchronize()
+        o = out.cpu().numpy()
+        for e in (0, 5, n - 1):
+            ref = np.concatenate([rgb_to_semantic_mask_ids(ring_h[s, e].numpy(), mode) for s in order])
+            assert np.array_equal(o[e], ref), mode
+    g = torch.zeros((n, F, S, S), dtype=torch.uint8, device="cuda")
+    check(L.cbev_expand_obs(dw.ctx, ptr(ring_d), n, F, head, 1, 1, gray_lut().ctypes.data_as(P_), ptr(g), None), "g")
+    rgb = torch.zeros((n, S, S, 3), dtype=torch.uint8, device="cuda")
+    check(L.cbev_expand_obs(dw.ctx, ptr(ring_d), n, F, head, 2, 3, rgb_lut().ctypes.data_as(P_), ptr(rgb), None), "r")
+    torch.cuda.synchronize()
+    gl = gray_lut()
+    assert np.array_equal(g.cpu().numpy(), gl[ring_h.numpy()[order].transpose(1, 0, 2, 3)].astype(np.uint8))
+    assert np.array_equal(rgb.cpu().numpy(), PALETTE[ring_h[head].numpy()])
+
+
+def test_vector_env_surface_and_partial_reset():
+    from carlabev_env_amd import EnvConfig, make_env, build_random_navigation_options, RandomNavigationReset
+    cfg = EnvConfig(size=128, obs_size=(128, 128), render_mode="rgb_array", obs_mode="bev_semantic")
+    env = make_env({"env": cfg, "num_envs": 8})
+    assert env.single_observation_space.shape == (24, 128, 128)
+    assert env.single_action_space.n == 9
+    obs, infos = env.reset(seed=3, options=build_random_navigation_options(
+        RandomNavigationReset(difficulty_id="rt_medium_v1")))
+    assert tuple(obs.shape) == (8, 24, 128, 128) and obs.dtype == torch.float32
+    assert all(i["valid"] for i in infos["spawn_validation"])
+    # the reset stack repeats the reset frame (FrameStackObservation padding "reset")
+    o = obs.cpu().numpy()
+    assert np.array_equal(o[:, 0:6], o[:, 18:24])
+    saw_term = False
+    for t in range(200):
+        a = np.random.default_rng(t).integers(0, 9, 8)
+        obs, r, term, trunc, infos = env.step(a)
+        assert r.dtype == torch.float64 and term.dtype == torch.bool
+        if term.any():
+            saw_term = True
+            assert "episode_info" in infos and infos["_episode_info"].any()
+            obs, _ = env.reset(options={"reset_mask": term.cpu().numpy(), "scene_seed": 1000 + t})
+    rgb = env.render()
+    assert len(rgb) == 8 and rgb[0].shape == (128, 128, 3)
+    assert saw_term
+    env.close()
