@@ -98,6 +98,7 @@ def build_env(cfgd, n, rank, device):
     env.attach_bank(torch.from_numpy(bank).to(device))
     # initial reset: records = seeded scenes, reset observation rendered on device
     env.attach_bank(recs)
+    env.auto_obs = False
     env.reset_from_bank(mask=None, bank_idx=torch.arange(n, dtype=torch.int32, device=device))
     env.attach_bank(torch.from_numpy(bank).to(device))
     return env, host
@@ -158,13 +159,15 @@ def main():
     gather = cfgd.get("gather", False) and world > 1
     gbuf = [torch.empty_like(env.frames()) for _ in range(world)] if gather and rank == 0 else None
 
+    env.auto_obs = False
+
     def one_step(t, wire):
         env.step_async_only(acts[t])
-        if wire:
-            env._obs()
         if gather:
             dist.gather(env.frames(), gbuf, dst=0)
-        env.reset_from_bank(mask=env.term)
+        env.reset_from_bank(mask=env.term)  # canonical loop: reset(reset_mask=terminated)
+        if wire:
+            env._obs()
 
     def timed(wire, profile):
         for t in range(args.warmup):
@@ -177,6 +180,7 @@ def main():
         t0 = time.perf_counter()
         for t in range(args.warmup, total_steps):
             one_step(t, wire)
+        host_enqueue = time.perf_counter() - t0
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
@@ -192,16 +196,16 @@ def main():
             check(lib().cbev_profile_read(env._ctx, buf, ctypes.byref(cnt)), "profile_read")
             check(lib().cbev_profile(env._ctx, 0), "profile")
             ms3 = [buf[i] / max(cnt.value, 1) for i in range(3)]
-        return el, ms3
+        return el, ms3, host_enqueue
 
-    el, ms3 = timed(False, True)
+    el, ms3, host_enq = timed(False, True)
     value = world * n * args.steps / el
     wire_value = None
     if not args.no_wire:
         # re-seed the state so the second pass replays a comparable workload
         env.attach_bank(torch.from_numpy(host_recs).to(device))
         env.reset_from_bank(mask=None, bank_idx=torch.arange(n, dtype=torch.int32, device=device))
-        el_w, _ = timed(True, False)
+        el_w, _, _ = timed(True, False)
         wire_value = world * n * args.steps / el_w
 
     S = P.size
@@ -235,6 +239,7 @@ def main():
             "config": {"workload": cfgd["workload"], "config_id": args.config, "envs_per_gpu": n,
                        "global_envs": n * world, "obs_size": S, "obs_mode": cfgd["obs_mode"],
                        "parallelism": f"env-sharded x{world}" + (" + RCCL gather" if gather else "")},
+            "host_enqueue_ms_per_step": round(host_enq / args.steps * 1e3, 4),
             "kernel_ms": {"k_dyn": round(ms3[0], 5), "k_raster": round(ms3[1], 5), "k_collide": round(ms3[2], 5)},
             "roofline": {"bound": "hbm", "kernel": "k_raster", "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),

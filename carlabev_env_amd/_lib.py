@@ -45,10 +45,8 @@ def lib():
     L.cbev_set_map.restype = _I
     L.cbev_step.argtypes = [_P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P]
     L.cbev_step.restype = _I
-    L.cbev_reset.argtypes = [_P, _P, _I, _P, _I, _P, _P, _P, _P]
+    L.cbev_reset.argtypes = [_P, _P, _I, _P, _I, _P, _P, _I, _P, _I, _P]
     L.cbev_reset.restype = _I
-    L.cbev_fill_ring.argtypes = [_P, _P, _I, _I, _P, _P, _P]
-    L.cbev_fill_ring.restype = _I
     L.cbev_expand_obs.argtypes = [_P, _P, _I, _I, _I, _I, _I, _P, _P, _P]
     L.cbev_expand_obs.restype = _I
     L.cbev_profile.argtypes = [_P, _I]
@@ -66,5 +64,5 @@ def check(rc: int, what: str = "cbev call"):
 
 
 EXPORTED_SYMBOLS = ("cbev_abi_version", "cbev_params_size", "cbev_layout_of", "cbev_field_names", "cbev_last_error",
-                    "cbev_create", "cbev_destroy", "cbev_set_map", "cbev_step", "cbev_reset", "cbev_fill_ring",
+                    "cbev_create", "cbev_destroy", "cbev_set_map", "cbev_step", "cbev_reset",
                     "cbev_expand_obs", "cbev_profile", "cbev_profile_read")

@@ -429,14 +429,12 @@ __device__ __forceinline__ void lds_paint_px(uint8_t* lds, int stride, int shift
   lds[py * stride + shift + px] = col;
 }
 
+// Render one env's observation (whole workgroup). RESET: BaseMap.reset's
+// frame (theta = 0, no actors drawn, world.py:92-100). The frame is written to
+// `nout` destinations out + k*out_stride (the frame-stack ring on reset).
 template <bool RESET>
-__global__ __launch_bounds__(256) void k_raster(KArgs K, uint8_t* __restrict__ recs, int n, uint8_t* __restrict__ frames,
-                                                const uint8_t* __restrict__ mask) {
-  extern __shared__ __align__(16) uint8_t lds[];
-  const int e = blockIdx.x;
-  if (e >= n) return;
-  if (mask != nullptr && mask[e] == 0) return;  // uniform per workgroup
-  DRec r = bind_rec(recs + (int64_t)e * K.L.record_bytes, K.L, K.C);
+__device__ __forceinline__ void raster_env(const KArgs& K, const DRec& r, uint8_t* __restrict__ out, int nout,
+                                           int64_t out_stride, uint8_t* __restrict__ lds) {
   const cbev_params& P = K.P;
   const int C = P.crop, S = P.size, pitch = P.map_pitch;
   const double x = r.hd[CBEV_HD_X], y = r.hd[CBEV_HD_Y], yaw = r.hd[CBEV_HD_YAW];
@@ -528,7 +526,6 @@ __global__ __launch_bounds__(256) void k_raster(KArgs K, uint8_t* __restrict__ r
   const int hx0 = P.anchor_x - P.hero_w / 2, hy0 = P.anchor_y - P.hero_w / 2;
   const int hx1 = hx0 + P.hero_w, hy1 = hy0 + P.hero_w;
   const int cpr = S / 16;  // 16-pixel chunks per output row
-  uint8_t* out = frames + (int64_t)e * S * S;
   for (int q = threadIdx.x; q < S * cpr; q += 256) {
     const int v = q / cpr, u0 = (q - v * cpr) * 16;
     uint32_t w[4] = {0, 0, 0, 0};
@@ -561,8 +558,47 @@ __global__ __launch_bounds__(256) void k_raster(KArgs K, uint8_t* __restrict__ r
       if (hrow && u >= hx0 && u < hx1) px = CBEV_PX_BLACK;
       w[k >> 2] |= px << (8 * (k & 3));
     }
-    *(uint4*)(out + v * S + u0) = make_uint4(w[0], w[1], w[2], w[3]);
+    const uint4 val = make_uint4(w[0], w[1], w[2], w[3]);
+    for (int k = 0; k < nout; ++k) *(uint4*)(out + k * out_stride + v * S + u0) = val;
   }
+}
+
+__global__ __launch_bounds__(256) void k_raster(KArgs K, uint8_t* __restrict__ recs, int n,
+                                                uint8_t* __restrict__ frames) {
+  extern __shared__ __align__(16) uint8_t lds[];
+  const int e = blockIdx.x;
+  if (e >= n) return;
+  DRec r = bind_rec(recs + (int64_t)e * K.L.record_bytes, K.L, K.C);
+  raster_env<false>(K, r, frames + (int64_t)e * K.P.size * K.P.size, 1, 0, lds);
+}
+
+// Partial reset (SyncVectorEnv.reset with reset_mask -> CarlaBEV.reset):
+// records[e] <- bank[b] (device scene bank) and the reset observation into
+// every slot of the frame-stack ring (FrameStackObservation padding "reset").
+// The frame is rendered from the bank record itself, so no other workgroup's
+// stores need to be visible.
+__global__ __launch_bounds__(256) void k_reset(KArgs K, uint8_t* __restrict__ recs, int n,
+                                               const uint8_t* __restrict__ bank, int n_bank,
+                                               const uint8_t* __restrict__ mask, const int32_t* __restrict__ bank_idx,
+                                               int bank_offset, uint8_t* __restrict__ ring, int n_frames) {
+  extern __shared__ __align__(16) uint8_t lds[];
+  const int e = blockIdx.x;
+  if (e >= n) return;
+  if (mask != nullptr && mask[e] == 0) return;  // uniform per workgroup
+  const int64_t rb = K.L.record_bytes;
+  uint8_t* dst = recs + (int64_t)e * rb;
+  const uint8_t* src = dst;
+  if (bank != nullptr) {
+    int b = bank_idx ? bank_idx[e] : (int)(((int64_t)e + bank_offset) % n_bank);
+    b = b < 0 ? 0 : (b >= n_bank ? n_bank - 1 : b);
+    src = bank + (int64_t)b * rb;
+    const uint4* s4 = (const uint4*)src;
+    uint4* d4 = (uint4*)dst;
+    for (int64_t i = threadIdx.x; i < rb / 16; i += 256) d4[i] = s4[i];
+  }
+  DRec r = bind_rec((uint8_t*)src, K.L, K.C);  // read-only use below
+  const int64_t SS = (int64_t)K.P.size * K.P.size;
+  raster_env<true>(K, r, ring + (int64_t)e * SS, n_frames, (int64_t)n * SS, lds);
 }
 
 // ============================================================== k_collide
@@ -872,32 +908,6 @@ __global__ __launch_bounds__(256) void k_collide(KArgs K, uint8_t* __restrict__ 
 }
 
 // ============================================================== reset / ring / expansion
-__global__ __launch_bounds__(256) void k_copy_records(uint8_t* __restrict__ recs, int n, const uint8_t* __restrict__ bank,
-                                                      int n_bank, const uint8_t* __restrict__ mask,
-                                                      const int32_t* __restrict__ bank_idx, int64_t rb) {
-  const int e = blockIdx.x;
-  if (e >= n) return;
-  if (mask != nullptr && mask[e] == 0) return;
-  int b = bank_idx[e];
-  b = b < 0 ? 0 : (b >= n_bank ? n_bank - 1 : b);
-  const uint4* src = (const uint4*)(bank + (int64_t)b * rb);
-  uint4* dst = (uint4*)(recs + (int64_t)e * rb);
-  for (int64_t i = threadIdx.x; i < rb / 16; i += 256) dst[i] = src[i];
-}
-
-__global__ __launch_bounds__(256) void k_fill_ring(uint8_t* __restrict__ ring, int n, int F, const uint8_t* __restrict__ frames,
-                                                   const uint8_t* __restrict__ mask, int SS) {
-  const int e = blockIdx.x;
-  if (e >= n) return;
-  if (mask != nullptr && mask[e] == 0) return;
-  const uint4* src = (const uint4*)(frames + (int64_t)e * SS);
-  for (int f = 0; f < F; ++f) {
-    uint4* dst = (uint4*)(ring + ((int64_t)f * n + e) * SS);
-    if ((const uint8_t*)dst == (const uint8_t*)src) continue;
-    for (int i = threadIdx.x; i < SS / 16; i += 256) dst[i] = src[i];
-  }
-}
-
 // semantic one-hot + frame stack + flatten: out[e][f*C + c][p] (rgb_to_semantic.py:65-142,256-272)
 __global__ __launch_bounds__(256) void k_expand_semantic(const uint8_t* __restrict__ ring, int n, int F, int head, int C,
                                                          int SS, const uint32_t* __restrict__ lut,
@@ -1108,9 +1118,9 @@ int cbev_create(const cbev_params* params, const cbev_caps* caps, int device, cb
   hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(c_sg), &T, sizeof T);
   if (e == hipSuccess) e = hipMalloc(&c->lut_dev, 64 * sizeof(uint32_t));
   if (e == hipSuccess)
-    e = hipFuncSetAttribute((const void*)k_raster<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)raster_lds_bytes(P));
+    e = hipFuncSetAttribute((const void*)k_raster, hipFuncAttributeMaxDynamicSharedMemorySize, (int)raster_lds_bytes(P));
   if (e == hipSuccess)
-    e = hipFuncSetAttribute((const void*)k_raster<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)raster_lds_bytes(P));
+    e = hipFuncSetAttribute((const void*)k_reset, hipFuncAttributeMaxDynamicSharedMemorySize, (int)raster_lds_bytes(P));
   if (e != hipSuccess) {
     free(c);
     return set_err(CBEV_EHIP, "cbev_create: %s", hipGetErrorString(e));
@@ -1189,8 +1199,7 @@ int cbev_step(cbev_ctx* c, void* records, int n, const void* actions, uint8_t* f
   if (ev) HIP_TRY(hipEventRecord(ev[0], s));
   hipLaunchKernelGGL(k_dyn, dim3(wg4), dim3(256), 0, s, K, (uint8_t*)records, n, actions);
   if (ev) HIP_TRY(hipEventRecord(ev[1], s));
-  hipLaunchKernelGGL(k_raster<false>, dim3(n), dim3(256), raster_lds_bytes(c->P), s, K, (uint8_t*)records, n, frames,
-                     (const uint8_t*)nullptr);
+  hipLaunchKernelGGL(k_raster, dim3(n), dim3(256), raster_lds_bytes(c->P), s, K, (uint8_t*)records, n, frames);
   if (ev) HIP_TRY(hipEventRecord(ev[2], s));
   hipLaunchKernelGGL(k_collide, dim3(wg4), dim3(256), 0, s, K, (uint8_t*)records, n, reward, term, trunc, cause, info);
   if (ev) HIP_TRY(hipEventRecord(ev[3], s));
@@ -1199,27 +1208,15 @@ int cbev_step(cbev_ctx* c, void* records, int n, const void* actions, uint8_t* f
 }
 
 int cbev_reset(cbev_ctx* c, void* records, int n, const void* bank, int n_bank, const uint8_t* mask,
-               const int32_t* bank_idx, uint8_t* frames, void* stream) {
+               const int32_t* bank_idx, int bank_offset, uint8_t* frames, int n_frames, void* stream) {
   if (!c || !records || !frames) return set_err(CBEV_EINVAL, "null argument");
   if (!c->map_dev) return set_err(CBEV_ESTATE, "cbev_set_map not called");
-  if (bank && (!bank_idx || n_bank <= 0)) return set_err(CBEV_EINVAL, "bank without bank_idx");
+  if (bank && n_bank <= 0) return set_err(CBEV_EINVAL, "empty bank");
+  if (n_frames < 1) return set_err(CBEV_EINVAL, "n_frames < 1");
   if (n <= 0) return CBEV_OK;
-  hipStream_t s = (hipStream_t)stream;
   KArgs K = kargs(c);
-  if (bank)
-    hipLaunchKernelGGL(k_copy_records, dim3(n), dim3(256), 0, s, (uint8_t*)records, n, (const uint8_t*)bank, n_bank, mask,
-                       bank_idx, (int64_t)c->L.record_bytes);
-  hipLaunchKernelGGL(k_raster<true>, dim3(n), dim3(256), raster_lds_bytes(c->P), s, K, (uint8_t*)records, n, frames, mask);
-  HIP_TRY(hipGetLastError());
-  return CBEV_OK;
-}
-
-int cbev_fill_ring(cbev_ctx* c, uint8_t* ring, int n, int n_frames, const uint8_t* frames, const uint8_t* mask,
-                   void* stream) {
-  if (!c || !ring || !frames || n_frames < 1) return set_err(CBEV_EINVAL, "bad argument");
-  if (n <= 0) return CBEV_OK;
-  const int SS = c->P.size * c->P.size;
-  hipLaunchKernelGGL(k_fill_ring, dim3(n), dim3(256), 0, (hipStream_t)stream, ring, n, n_frames, frames, mask, SS);
+  hipLaunchKernelGGL(k_reset, dim3(n), dim3(256), raster_lds_bytes(c->P), (hipStream_t)stream, K, (uint8_t*)records, n,
+                     (const uint8_t*)bank, n_bank, mask, bank_idx, bank_offset, frames, n_frames);
   HIP_TRY(hipGetLastError());
   return CBEV_OK;
 }

@@ -141,6 +141,7 @@ class CarlaBEVVectorEnv:
         self._t0 = np.full(N, time.perf_counter())
         self.bank = None
         self._bank_cursor = 0
+        self.auto_obs = True  # reset_from_bank also expands the wire observation
         self._closed = False
 
     # ------------------------------------------------------------------ helpers
@@ -180,21 +181,20 @@ class CarlaBEVVectorEnv:
         return torch.from_numpy(host).to(self.device)
 
     def reset_from_bank(self, mask: torch.Tensor | None = None, bank_idx: torch.Tensor | None = None):
-        """Device-only partial reset: env i (mask[i]) <- bank[bank_idx[i]]; no host sync."""
+        """Device-only partial reset: env i (mask[i]) <- bank[bank_idx[i]] (default: a rotating
+        offset into the bank), reset frame into every frame-stack slot. One launch, no host sync."""
         if self.bank is None:
             raise RuntimeError("no scene bank attached")
         N, B = self.num_envs, self.bank.shape[0]
+        offset = 0
         if bank_idx is None:
-            bank_idx = (torch.arange(N, device=self.device, dtype=torch.int64) + self._bank_cursor) % B
-            bank_idx = bank_idx.to(torch.int32)
+            offset = self._bank_cursor
             self._bank_cursor = (self._bank_cursor + N) % B
-        m = None if mask is None else mask.to(device=self.device, dtype=torch.uint8).contiguous()
-        s = self._stream()
-        frames = self.ring[self.head]
-        check(lib().cbev_reset(self._ctx, _ptr(self.records), N, _ptr(self.bank), B, _ptr(m), _ptr(bank_idx),
-                               _ptr(frames), s), "cbev_reset")
-        check(lib().cbev_fill_ring(self._ctx, _ptr(self.ring), N, self.F, _ptr(frames), _ptr(m), s), "cbev_fill_ring")
-        return self._obs()
+        if mask is not None and (mask.dtype != torch.uint8 or mask.device != self.device):
+            mask = mask.to(device=self.device, dtype=torch.uint8)
+        check(lib().cbev_reset(self._ctx, _ptr(self.records), N, _ptr(self.bank), B, _ptr(mask), _ptr(bank_idx),
+                               offset, _ptr(self.ring), self.F, self._stream()), "cbev_reset")
+        return self._obs() if self.auto_obs else None
 
     # ------------------------------------------------------------------ gymnasium surface
     def reset(self, seed=None, options=None):
@@ -223,12 +223,8 @@ class CarlaBEVVectorEnv:
             bank_idx[idx] = np.arange(len(idx), dtype=np.int32)
             bidx = torch.from_numpy(bank_idx).to(self.device)
             m = torch.from_numpy(mask.astype(np.uint8)).to(self.device)
-            s = self._stream()
-            frames = self.ring[self.head]
-            check(lib().cbev_reset(self._ctx, _ptr(self.records), N, _ptr(staging), len(idx), _ptr(m), _ptr(bidx),
-                                   _ptr(frames), s), "cbev_reset")
-            check(lib().cbev_fill_ring(self._ctx, _ptr(self.ring), N, self.F, _ptr(frames), _ptr(m), s),
-                  "cbev_fill_ring")
+            check(lib().cbev_reset(self._ctx, _ptr(self.records), N, _ptr(staging), len(idx), _ptr(m), _ptr(bidx), 0,
+                                   _ptr(self.ring), self.F, self._stream()), "cbev_reset")
         obs = self._obs()
         infos = {}
         if len(idx):
@@ -242,6 +238,9 @@ class CarlaBEVVectorEnv:
         return obs, infos
 
     def _actions_tensor(self, actions) -> torch.Tensor:
+        if isinstance(actions, torch.Tensor) and actions.device == self.device and actions.is_contiguous() and (
+                actions.dtype == (torch.int32 if self.discrete else torch.float32)):
+            return actions
         a = torch.as_tensor(actions, device=self.device)
         if self.discrete:
             a = a.reshape(self.num_envs).to(torch.int32).contiguous()

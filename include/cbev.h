@@ -63,17 +63,16 @@ int cbev_step(cbev_ctx* ctx, void* records, int n, const void* actions, uint8_t*
               uint8_t* term, uint8_t* trunc, int32_t* cause, float* info, void* stream);
 
 /* Reset the envs selected by mask (uint8[n], NULL = all):
- *   if bank != NULL: records[i] = bank[bank_idx[i]] (device-side scene bank; bank_idx int32[n])
+ *   if bank != NULL: records[i] = bank[b] with b = bank_idx[i], or, when
+ *   bank_idx == NULL, b = (i + bank_offset) % n_bank (device-side scene bank);
  *   then render the reset observation (BaseMap.reset: theta = 0, no actors,
- *   world.py:92-100) into frames[i].
- * Replaces `CarlaBEV.reset` after scene generation (carlabev.py:96-148). */
+ *   world.py:92-100) into every slot of frames = uint8[n_frames][n][S][S]
+ *   (the frame-stack ring: FrameStackObservation pads with the reset frame;
+ *   n_frames = 1 for a plain frame buffer).
+ * Replaces `CarlaBEV.reset` after scene generation (carlabev.py:96-148) and the
+ * wrappers' reset path. One launch. */
 int cbev_reset(cbev_ctx* ctx, void* records, int n, const void* bank, int n_bank, const uint8_t* mask,
-               const int32_t* bank_idx, uint8_t* frames, void* stream);
-
-/* Copy frames[i] into every slot of a frame-stack ring for masked envs
- * (FrameStackObservation padding_type="reset"). ring: uint8[F][n][S][S]. */
-int cbev_fill_ring(cbev_ctx* ctx, uint8_t* ring, int n, int n_frames, const uint8_t* frames, const uint8_t* mask,
-                   void* stream);
+               const int32_t* bank_idx, int bank_offset, uint8_t* frames, int n_frames, void* stream);
 
 /* Wrapper stack on the device (envs/__init__.py:62-83):
  *   kind 0: semantic one-hot (rgb_to_semantic.py:65-142) + FrameStack + Flatten

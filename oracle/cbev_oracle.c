@@ -1164,8 +1164,10 @@ int orc_step(const cbev_params* P, const uint8_t* padded_map, const cbev_caps* c
     hd[CBEV_HD_P_SPEED] = f[3];
     hd[CBEV_HD_P_TTC] = f[4];
     hd[CBEV_HD_P_COMFORT] = f[5];
-    hd[CBEV_HD_TTC] = ttc;
-    hd[CBEV_HD_DIST2ROUTE] = d2r;
+    if (cause == CBEV_CAUSE_NONE) { /* debug fields exist only on the full path (carl_reward_fn.py:313-325) */
+      hd[CBEV_HD_TTC] = ttc;
+      hd[CBEV_HD_DIST2ROUTE] = d2r;
+    }
   } else {
     orc_shaping_state ss = {hi[CBEV_HI_KSTEPS], hi[CBEV_HI_OFFROAD], hd[CBEV_HD_LAST_DYAW]};
     reward = orc_shaping_step(P, &ss, &in, &cause, &term);

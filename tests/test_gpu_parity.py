@@ -66,7 +66,7 @@ def run_parity(kinds, n_envs, steps, size=128, profile="discrete9_v1", reward="c
     S = P.size
     d_recs = torch.from_numpy(recs.copy()).cuda()
     d_frames = torch.zeros((n_envs, S, S), dtype=torch.uint8, device="cuda")
-    check(L.cbev_reset(dw.ctx, ptr(d_recs), n_envs, None, 0, None, None, ptr(d_frames), None), "reset")
+    check(L.cbev_reset(dw.ctx, ptr(d_recs), n_envs, None, 0, None, None, 0, ptr(d_frames), 1, None), "reset")
     orc = O.Oracle(P, padded, CAPS_FULL.c(), layout.record_bytes)
     h_frames = np.zeros((n_envs, S, S), np.uint8)
     for e in range(n_envs):
@@ -134,8 +134,7 @@ def test_bank_reset_and_wrapper_expansion():
     ring = torch.zeros((F, n, S, S), dtype=torch.uint8, device="cuda")
     mask = (torch.arange(n) % 3 == 0).to(torch.uint8).cuda()
     bidx = (torch.arange(n) % B).to(torch.int32).cuda()
-    check(L.cbev_reset(dw.ctx, ptr(d_recs), n, ptr(d_bank), B, ptr(mask), ptr(bidx), ptr(ring[2]), None), "reset")
-    check(L.cbev_fill_ring(dw.ctx, ptr(ring), n, F, ptr(ring[2]), ptr(mask), None), "fill")
+    check(L.cbev_reset(dw.ctx, ptr(d_recs), n, ptr(d_bank), B, ptr(mask), ptr(bidx), 0, ptr(ring), F, None), "reset")
     torch.cuda.synchronize()
     dr = d_recs.cpu().numpy()
     orc = O.Oracle(P, padded, CAPS_FULL.c(), layout.record_bytes)
@@ -149,6 +148,14 @@ def test_bank_reset_and_wrapper_expansion():
                 assert np.array_equal(ring[s, e].cpu().numpy(), f)
         else:
             assert np.array_equal(dr[e], recs[e])
+    # rotating-offset bank assignment (bank_idx NULL): b = (e + offset) % B
+    d2 = torch.from_numpy(recs.copy()).cuda()
+    ring2 = torch.zeros((1, n, S, S), dtype=torch.uint8, device="cuda")
+    check(L.cbev_reset(dw.ctx, ptr(d2), n, ptr(d_bank), B, None, None, 5, ptr(ring2), 1, None), "reset2")
+    torch.cuda.synchronize()
+    d2h = d2.cpu().numpy()
+    for e in range(n):
+        assert np.array_equal(d2h[e], bank[(e + 5) % B])
     # expansion kinds against host restatements
     ring_h = torch.randint(0, 10, (F, n, S, S), dtype=torch.uint8)
     ring_d = ring_h.cuda()
