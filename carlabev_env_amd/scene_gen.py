@@ -81,9 +81,11 @@ def _rng_state(g: np.random.Generator) -> dict:
 class RoadGrid:
     """Road-centre cell graph over the 128-scale Town01 class map."""
 
-    def __init__(self, map_name: str = "Town01", cell: int = 4, margin: float = 6.0, stride: int = 3,
-                 n_sources: int = 128, seed: int = 12345):
-        classes = load_class_map(map_name, 128)
+    def __init__(self, map_name: str = "Town01", size: int = 128, cell: int = 4, margin: float = 6.0,
+                 stride: int = 3, n_sources: int = 128, seed: int = 12345):
+        # routes live in 128-surface coordinates for every map size (scene_generator.py:71-75), so
+        # plan on the part of the size-S map those coordinates cover (the whole map at S=128)
+        classes = window_128(load_class_map(map_name, size))
         self.h, self.w = classes.shape
         drivable = classes == 1
         dist = ndimage.distance_transform_edt(drivable)
@@ -167,10 +169,43 @@ class RoadGrid:
 _GRIDS: dict = {}
 
 
-def road_grid(map_name: str = "Town01") -> RoadGrid:
-    if map_name not in _GRIDS:
-        _GRIDS[map_name] = RoadGrid(map_name)
-    return _GRIDS[map_name]
+def window_128(classes: np.ndarray) -> np.ndarray:
+    """The region of a size-S class map addressed by 128-surface coordinates."""
+    return classes[:1280, :1024]
+
+
+def road_grid(map_name: str = "Town01", size: int = 128) -> RoadGrid:
+    key = (map_name, size)
+    if key not in _GRIDS:
+        _GRIDS[key] = RoadGrid(map_name, size)
+    return _GRIDS[key]
+
+
+def _all_drivable(ii, y0, y1, x0, x1) -> bool:
+    return ii[y1, x1] - ii[y0, x1] - ii[y1, x0] + ii[y0, x0] == (y1 - y0) * (x1 - x0)
+
+
+def scenario_anchors(map_name: str, size: int):
+    """Anchors for the authored-geometry scenarios on a size-S map (S != 128).
+
+    The reference samplers place the ego at x = 850, y in [900, 1000) in 128-surface
+    coordinates (lead_brake.py:30-41, jaywalk.py:38-53). With the literal S=256
+    semantics (256 map queried at 128-scale positions) that spot is NON_DRIVABLE,
+    every spawn is rejected and CarlaBEV.reset raises after 10 attempts; the
+    samplers accept anchor_x/anchor_y, so the generator passes anchors that are
+    drivable on the size-S map: a 120 px northbound road for lead_brake/jaywalk,
+    a 250 px one for the red-light runner's ego approach."""
+    c = window_128(load_class_map(map_name, size)) == 1
+    ii = np.pad(c.astype(np.int64).cumsum(0).cumsum(1), ((1, 0), (1, 0)))
+    h, w = c.shape
+    north, long_north = [], []
+    for y in range(260, h - 20, 10):
+        for x in range(20, w - 20, 2):
+            if _all_drivable(ii, y - 110, y + 10, x - 4, x + 5):
+                north.append((x, y))
+                if _all_drivable(ii, y - 250, y + 10, x - 4, x + 5):
+                    long_north.append((x, y - 125))
+    return north, long_north
 
 
 def _m2s(m: float) -> float:
@@ -183,7 +218,9 @@ class SceneGenerator:
     def __init__(self, cfg=None, map_name: str = "Town01"):
         self.cfg = cfg
         self.map_name = map_name
-        self.grid = road_grid(map_name)
+        self.size = int(getattr(cfg, "size", 128)) if cfg is not None else 128
+        self.grid = road_grid(map_name, self.size)
+        self._anchors = scenario_anchors(map_name, self.size) if self.size != 128 else None
         self.max_vehicles = getattr(cfg, "max_vehicles", 25) if cfg is not None else 25
         self.traffic_enabled = getattr(cfg, "traffic_enabled", True) if cfg is not None else True
 
@@ -295,8 +332,11 @@ class SceneGenerator:
         idx = kw.get("intersection_index")
         if idx is None:
             idx = int(g.integers(0, len(self.INTERSECTIONS_RAW)))
-        ry_raw, rx_raw = self.INTERSECTIONS_RAW[int(idx)]
-        cx, cy = rx_raw / 8.0, ry_raw / 8.0
+        if "center" in kw:
+            cx, cy = (float(v) for v in kw["center"])
+        else:
+            ry_raw, rx_raw = self.INTERSECTIONS_RAW[int(idx)]
+            cx, cy = rx_raw / 8.0, ry_raw / 8.0
         span = 950.0 / 8.0
         n = 20
         ego_ry = list(np.linspace(cy + span, cy - span, n))
@@ -332,6 +372,12 @@ class SceneGenerator:
                 level = bundle.scenario_rng.choice([1, 2, 3, 4])
             g = bundle.scenario_np_rng
             kw = {k: v for k, v in options.items() if k not in ("scene", "level", "reset_mask")}
+            if self._anchors is not None:
+                north, cross = self._anchors
+                if scene == "red_light_runner" and "center" not in kw and cross:
+                    kw["center"] = cross[bundle.scene_seed % len(cross)]
+                elif scene != "red_light_runner" and "anchor_x" not in kw and north:
+                    kw["anchor_x"], kw["anchor_y"] = north[bundle.scene_seed % len(north)]
             spec = getattr(self, scene)(int(level), g, kw)
             spec.hero_rng_state = _rng_state(bundle.route_np_rng)
             spec.actor_rng_state = _rng_state(g)  # actors share the sampler's generator (deep-copied)

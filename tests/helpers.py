@@ -26,9 +26,9 @@ def world(size=128, action_profile="discrete9_v1", reward_profile="carl_base_v1"
     padded, pitch = padded_map(classes, P.pad)
     assert pitch == P.map_pitch
     layout = LY.Layout.make(caps)
-    if "gen" not in _GEN:
-        _GEN["gen"] = SceneGenerator(cfg, cfg.map_name)
-    builder = HostResetBuilder(cfg, classes, P, layout, _GEN["gen"])
+    if size not in _GEN:
+        _GEN[size] = SceneGenerator(cfg, cfg.map_name)
+    builder = HostResetBuilder(cfg, classes, P, layout, _GEN[size])
     return cfg, P, padded, layout, builder
 
 
