@@ -90,6 +90,8 @@ class CarlaBEVVectorEnv:
         self.map_host, pitch = padded_map(self.classes, self.params.pad)
         assert pitch == self.params.map_pitch
         c = dict(DEFAULT_CAPS)
+        # rdm scenes default to EnvConfig.max_vehicles vehicles (scene_generator.py:100); scenarios add <= 3
+        c["actor_cap"] = max(c["actor_cap"], int(self.cfg.max_vehicles) + 4)
         c.update(caps or {})
         self.caps = LY.Caps(**c)
         self.layout = LY.Layout.make(self.caps)
