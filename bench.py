@@ -240,7 +240,7 @@ def main():
                        "global_envs": n * world, "obs_size": S, "obs_mode": cfgd["obs_mode"],
                        "parallelism": f"env-sharded x{world}" + (" + RCCL gather" if gather else "")},
             "host_enqueue_ms_per_step": round(host_enq / args.steps * 1e3, 4),
-            "kernel_ms": {"k_dyn": round(ms3[0], 5), "k_raster": round(ms3[1], 5), "k_collide": round(ms3[2], 5)},
+            "kernel_ms": {"k_hero+k_actors": round(ms3[0], 5), "k_raster": round(ms3[1], 5), "k_collide": round(ms3[2], 5)},
             "roofline": {"bound": "hbm", "kernel": "k_raster", "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic, "algorithmic_bytes_per_env": algo_bytes},

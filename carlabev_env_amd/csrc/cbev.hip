@@ -1,10 +1,11 @@
 // cbev.hip — MI355X (gfx950) kernels and C-ABI of the batched CarlaBEV step.
 //
-// One `CarlaBEV.step()` for N envs is three launches on the caller's stream:
+// One `CarlaBEV.step()` for N envs is three or four launches on the caller's stream:
 //
-//   k_dyn      wave64 per env: ego bicycle + Stanley target search (wave
-//              arg-min over the route), scripted actors (lane per actor:
-//              behaviour FSM, PID + Stanley, bicycle), scene clock, dist2goal.
+//   k_hero     one thread per env: ego bicycle + Stanley target search,
+//              comfort kinematics, scene clock, dist2goal.
+//   k_actors   wave64 per env, lane per actor: behaviour FSM, PID + Stanley,
+//              bicycle (launched only when the record has actor slots).
 //              Reference: Scene._scene_step (scene.py:90-98), hero.py:88-187,
 //              actor.py:110-124, behavior/*.py, stanley_controller.py:51-123.
 //   k_raster   256-thread workgroup per env: stage the C x C crop of the padded
@@ -15,10 +16,10 @@
 //              as one palette id per pixel with 16-B stores.
 //              Reference: BaseMap.draw_fov (world.py:137-157), fov.py:70-99,
 //              actor_manager.py:121-132, hero.py:26-32.
-//   k_collide  wave64 per env: ego tile, rect collisions (last hit in draw
-//              order wins, wave max), target consumption, actors_state/TTC
-//              (wave min), CaRL route progress (wave arg-min over segments),
-//              reward, episode accumulators, termination flags.
+//   k_collide  one thread per env: ego tile, rect collisions (last hit in
+//              draw order wins), target consumption, actors_state/TTC, CaRL
+//              route progress (arg-min over raw segments), reward, episode
+//              accumulators, termination flags.
 //              Reference: scene.py:110-140, carl_reward_fn.py:149-341,
 //              reward.py:80-278, stats.py:30-56, carlabev.py:177-185.
 #include <hip/hip_runtime.h>
@@ -287,13 +288,13 @@ __device__ void d_actor_step(DRec& r, int a, double t) {
   RAD(r, CBEV_AD_TIME, a) += CB_DT;
 }
 
-// ============================================================== k_dyn
-// One wavefront per env; 4 envs per 256-thread workgroup.
-__global__ __launch_bounds__(256) void k_dyn(KArgs K, uint8_t* __restrict__ recs, int n,
+// ============================================================== k_hero / k_actors
+// Ego update: one thread per env, so all 64 lanes of a wave carry the float64
+// scalar chain of 64 envs (BaseAgent.physics_step, hero.py:88-138).
+__global__ __launch_bounds__(64) void k_hero(KArgs K, uint8_t* __restrict__ recs, int n,
                                              const void* __restrict__ actions) {
-  const int lane = threadIdx.x & 63;
-  const int e = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (e >= n) return;  // wave-uniform; no workgroup barrier in this kernel
+  const int e = blockIdx.x * 64 + threadIdx.x;
+  if (e >= n) return;
   DRec r = bind_rec(recs + (int64_t)e * K.L.record_bytes, K.L, K.C);
   double* hd = r.hd;
   int32_t* hi = r.hi;
@@ -315,90 +316,80 @@ __global__ __launch_bounds__(256) void k_dyn(KArgs K, uint8_t* __restrict__ recs
     sa = (sa != sa) ? sa : (sa < -1.0f ? -1.0f : (sa > 1.0f ? 1.0f : sa));
     b = (b != b) ? b : (b < 0.0f ? 0.0f : (b > 1.0f ? 1.0f : b));
   }
+  hd[CBEV_HD_T] += CB_DT;  // Scene._t += dt (scene.py:91)
 
-  const double t = hd[CBEV_HD_T] + CB_DT;  // Scene._t += dt
-
-  // ---- hero Stanley target search: wave arg-min over the smoothed route
   double s[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) s[k] = hd[CBEV_HD_X + k];
-  const double fx = s[0] + CB_WHEELBASE * cos(s[2]);
-  const double fy = s[1] + CB_WHEELBASE * sin(s[2]);
-  const int nroute = hi[CBEV_HI_NROUTE];
-  double bd = INFINITY;
-  int bi = 0x7fffffff;
-  for (int i = lane; i < nroute; i += 64) {
-    double d = hypot(fx - r.cx[i], fy - r.cy[i]);
-    if (bi == 0x7fffffff || d < bd) {  // first minimum within the lane's stride
-      bd = d;
-      bi = i;
-    }
+  // stanley_control's target search; its steering output is unused by the hero
+  const int bi = d_target_index_serial(s[0], s[1], s[2], r.cx, r.cy, hi[CBEV_HI_NROUTE], nullptr);
+  hi[CBEV_HI_TIDX] = hi[CBEV_HI_TIDX] >= bi ? hi[CBEV_HI_TIDX] : bi;
+  const double v = s[3];
+  const int scale = K.P.scale;
+  // BaseAgent.accelerate / steering / brake (hero.py:140-162)
+  const double acc_val = (g > 0.0f) ? (double)((g * 1.0f) * (float)scale) : 0.0;
+  double delta;
+  if (fabs(v) < 0.1) {
+    delta = 0.0;
+  } else {
+    double steer_deg = 18.0 / (1.0 + 0.35 * fabs(v));
+    steer_deg = d_clip(steer_deg, 8.0, 18.0);
+    delta = d_radians((double)sa * steer_deg);
   }
-  wave_argmin(bd, bi);
-
-  if (lane == 0) {
-    // stanley_control: monotone target index (its steering output is unused by the hero)
-    int tidx = hi[CBEV_HI_TIDX] >= bi ? hi[CBEV_HI_TIDX] : bi;
-    hi[CBEV_HI_TIDX] = tidx;
-    const double v = s[3];
-    const int scale = K.P.scale;
-    // BaseAgent.accelerate / steering / brake (hero.py:140-162)
-    double acc_val = (g > 0.0f) ? (double)((g * 1.0f) * (float)scale) : 0.0;
-    double delta;
-    if (fabs(v) < 0.1) {
-      delta = 0.0;
-    } else {
-      double steer_deg = 18.0 / (1.0 + 0.35 * fabs(v));
-      steer_deg = d_clip(steer_deg, 8.0, 18.0);
-      delta = d_radians((double)sa * steer_deg);
-    }
-    double sf = d_clip(fabs(v) / 5.0, 0.3, 1.0);
-    double brake_val = (b > 0.0f) ? (double)((b * 0.6f) * (float)scale) * sf : 0.0 * 0.6 * scale * sf;
-    double target_acc = acc_val - brake_val - 0.05 * v;
-    const double alpha = 0.2;
-    double acc = (1 - alpha) * hd[CBEV_HD_ACC] + alpha * target_acc;
-    hd[CBEV_HD_ACC] = acc;
-    d_state_update(s, acc, delta, hd[CBEV_HD_TSPEED]);
-    s[3] *= 0.9999;
-    if (fabs(s[3]) < 0.05) s[3] = 0.0;
-    s[3] *= 0.985;
+  const double sf = d_clip(fabs(v) / 5.0, 0.3, 1.0);
+  // NEP 50: float32(brake * 0.6) * scale in float32, then * float64 speed factor
+  const double brake_val = (b > 0.0f) ? (double)((b * 0.6f) * (float)scale) * sf : 0.0 * 0.6 * scale * sf;
+  const double target_acc = acc_val - brake_val - 0.05 * v;
+  const double alpha = 0.2;
+  const double acc = (1 - alpha) * hd[CBEV_HD_ACC] + alpha * target_acc;
+  hd[CBEV_HD_ACC] = acc;
+  d_state_update(s, acc, delta, hd[CBEV_HD_TSPEED]);
+  s[3] *= 0.9999;
+  if (fabs(s[3]) < 0.05) s[3] = 0.0;
+  s[3] *= 0.985;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) hd[CBEV_HD_X + k] = s[k];
-    hd[CBEV_HD_U_GAS] = (double)g;
-    hd[CBEV_HD_U_STEER] = (double)sa;
-    hd[CBEV_HD_U_BRAKE] = (double)b;
-    hd[CBEV_HD_U_DELTA] = delta;
-    // compute_comfort_kinematics (comfort.py:17-61)
-    const int has_prev = hi[CBEV_HI_HAS_PREV_COMFORT];
-    double speed_mps = s[3] * CB_MPP, prev_speed_mps = s[7] * CB_MPP;
-    double dyaw = s[2] - s[6];
-    double yr_rad = atan2(sin(dyaw), cos(dyaw)) / CB_DT;
-    double yr_deg = d_degrees(yr_rad);
-    double al = (speed_mps - prev_speed_mps) / CB_DT;
-    double alat = speed_mps * yr_rad;
-    hd[CBEV_HD_C_SPEED] = speed_mps;
-    hd[CBEV_HD_C_AL] = al;
-    hd[CBEV_HD_C_ALAT] = alat;
-    hd[CBEV_HD_C_JL] = has_prev ? (al - hd[CBEV_HD_PREV_AL]) / CB_DT : 0.0;
-    hd[CBEV_HD_C_JLAT] = has_prev ? (alat - hd[CBEV_HD_PREV_ALAT]) / CB_DT : 0.0;
-    hd[CBEV_HD_C_YR] = yr_deg;
-    hd[CBEV_HD_C_YACC] = has_prev ? (yr_deg - hd[CBEV_HD_PREV_YR]) / CB_DT : 0.0;
-    hd[CBEV_HD_PREV_AL] = al;
-    hd[CBEV_HD_PREV_ALAT] = alat;
-    hd[CBEV_HD_PREV_YR] = yr_deg;
-    hi[CBEV_HI_HAS_PREV_COMFORT] = 1;
-    hd[CBEV_HD_T] = t;
-  }
+  for (int k = 0; k < 8; ++k) hd[CBEV_HD_X + k] = s[k];
+  hd[CBEV_HD_U_GAS] = (double)g;
+  hd[CBEV_HD_U_STEER] = (double)sa;
+  hd[CBEV_HD_U_BRAKE] = (double)b;
+  hd[CBEV_HD_U_DELTA] = delta;
+  // compute_comfort_kinematics (comfort.py:17-61)
+  const int has_prev = hi[CBEV_HI_HAS_PREV_COMFORT];
+  const double speed_mps = s[3] * CB_MPP, prev_speed_mps = s[7] * CB_MPP;
+  const double dyaw = s[2] - s[6];
+  const double yr_rad = atan2(sin(dyaw), cos(dyaw)) / CB_DT;
+  const double yr_deg = d_degrees(yr_rad);
+  const double al = (speed_mps - prev_speed_mps) / CB_DT;
+  const double alat = speed_mps * yr_rad;
+  hd[CBEV_HD_C_SPEED] = speed_mps;
+  hd[CBEV_HD_C_AL] = al;
+  hd[CBEV_HD_C_ALAT] = alat;
+  hd[CBEV_HD_C_JL] = has_prev ? (al - hd[CBEV_HD_PREV_AL]) / CB_DT : 0.0;
+  hd[CBEV_HD_C_JLAT] = has_prev ? (alat - hd[CBEV_HD_PREV_ALAT]) / CB_DT : 0.0;
+  hd[CBEV_HD_C_YR] = yr_deg;
+  hd[CBEV_HD_C_YACC] = has_prev ? (yr_deg - hd[CBEV_HD_PREV_YR]) / CB_DT : 0.0;
+  hd[CBEV_HD_PREV_AL] = al;
+  hd[CBEV_HD_PREV_ALAT] = alat;
+  hd[CBEV_HD_PREV_YR] = yr_deg;
+  hi[CBEV_HI_HAS_PREV_COMFORT] = 1;
+  // Scene dist2goal bookkeeping (scene.py:97-98,175-177)
+  hd[CBEV_HD_D2G_T1] = hd[CBEV_HD_D2G];
+  const double gx = s[0] - hd[CBEV_HD_GOAL_X], gy = s[1] - hd[CBEV_HD_GOAL_Y];
+  hd[CBEV_HD_D2G] = sqrt(gx * gx + gy * gy);
+}
 
-  // ---- scripted actors, one lane each (vehicles then pedestrians)
-  const int nact = hi[CBEV_HI_NACT];
+// Scripted actors (ActorManager.step_all, actor_manager.py:111-119): one
+// wavefront per env, one lane per actor (vehicles then pedestrians). Runs after
+// k_hero, so the scene clock hd[T] is already advanced.
+__global__ __launch_bounds__(256) void k_actors(KArgs K, uint8_t* __restrict__ recs, int n) {
+  const int lane = threadIdx.x & 63;
+  const int e = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (e >= n) return;
+  DRec r = bind_rec(recs + (int64_t)e * K.L.record_bytes, K.L, K.C);
+  const int nact = r.hi[CBEV_HI_NACT];
+  if (nact == 0) return;
+  const double t = r.hd[CBEV_HD_T];
   for (int a = lane; a < nact; a += 64) d_actor_step(r, a, t);
-
-  if (lane == 0) {  // Scene dist2goal bookkeeping (scene.py:97-98,175-177)
-    hd[CBEV_HD_D2G_T1] = hd[CBEV_HD_D2G];
-    double dx = s[0] - hd[CBEV_HD_GOAL_X], dy = s[1] - hd[CBEV_HD_GOAL_Y];
-    hd[CBEV_HD_D2G] = sqrt(dx * dx + dy * dy);
-  }
 }
 
 // ============================================================== k_raster
@@ -419,38 +410,57 @@ __device__ __forceinline__ void d_crop_origin(const cbev_params& P, double x, do
 // rect_from_world_center (transforms.py:46-51): centre rounded half-even, x = c - w/2
 __device__ __forceinline__ int d_rect_lo(double w, int pad, int size) { return (int)rint((double)pad + w * 1.0) - size / 2; }
 
-// paint one group of rects (same colour) into the LDS crop; thread t handles pixel
-// (t & 15) of rect base + (t >> 4); rect side <= 4 for actors and targets
-__device__ __forceinline__ void lds_paint_px(uint8_t* lds, int stride, int shift, int C, int rx, int ry, int sz, int p,
+// LDS image of the crop window: crop row r starts at dword r * sd, holding the
+// padded-map bytes from xa = xmin & ~3 on (so crop column c is byte
+// r*4*sd + shift + c, shift = xmin & 3). sd is odd: crop rows land in different
+// LDS banks, which keeps the gathers along rotated rows conflict-free for the
+// axis-aligned cases and spread for the rest.
+__host__ __device__ __forceinline__ int raster_row_dwords(int C) { return (C + 6) / 4; }
+__host__ __device__ __forceinline__ int raster_stride_dwords(int C) { return raster_row_dwords(C) | 1; }
+
+// paint one pixel of a rect (side <= 4) into the LDS crop; thread t handles
+// pixel (t & 15) of rect base + (t >> 4)
+__device__ __forceinline__ void lds_paint_px(uint8_t* lds, int sb, int shift, int C, int rx, int ry, int sz, int p,
                                              uint8_t col) {
   if (p >= sz * sz) return;
   int px = rx + (p % sz), py = ry + (p / sz);
   if (px < 0 || py < 0 || px >= C || py >= C) return;
-  lds[py * stride + shift + px] = col;
+  lds[py * sb + shift + px] = col;
 }
 
-// Render one env's observation (whole workgroup). RESET: BaseMap.reset's
+// Render one env's observation (whole 256-thread workgroup). RESET: BaseMap.reset's
 // frame (theta = 0, no actors drawn, world.py:92-100). The frame is written to
 // `nout` destinations out + k*out_stride (the frame-stack ring on reset).
+//
+// Output mapping: each wave renders units of 256 consecutive output pixels;
+// gather j (0..3) has lane l sample pixel 64j + l (a 64-pixel run of one output
+// row, so consecutive lanes read along a rotated source row), and a ds_bpermute
+// transpose then gives lane l the 4 consecutive pixels 4l..4l+3 it stores as one
+// dword (256 contiguous bytes per wave store).
 template <bool RESET>
 __device__ __forceinline__ void raster_env(const KArgs& K, const DRec& r, uint8_t* __restrict__ out, int nout,
                                            int64_t out_stride, uint8_t* __restrict__ lds) {
   const cbev_params& P = K.P;
-  const int C = P.crop, S = P.size, pitch = P.map_pitch;
+  const int C = P.crop, S = P.size;
   const double x = r.hd[CBEV_HD_X], y = r.hd[CBEV_HD_Y], yaw = r.hd[CBEV_HD_YAW];
   int xmin, ymin;
   d_crop_origin(P, x, y, &xmin, &ymin);
-  const int shift = xmin & 15;
-  const int W16 = (C + 30) / 16;  // 16-B chunks per staged row: covers shift (<=15) + C
-  const int stride = W16 * 16;
+  const int xa = xmin & ~3, shift = xmin - xa;
+  const int W4 = raster_row_dwords(C), sd = raster_stride_dwords(C), sb = 4 * sd;
 
-  // ---- stage the crop window (rows of the padded map) into LDS
-  const uint8_t* src0 = K.map + (int64_t)ymin * pitch + (xmin - shift);
-  const int nchunks = C * W16;
-  for (int q = threadIdx.x; q < nchunks; q += 256) {
-    int row = q / W16, col = q - row * W16;
-    uint4 v = *(const uint4*)(src0 + (int64_t)row * pitch + col * 16);
-    *(uint4*)(lds + row * stride + col * 16) = v;
+  // ---- stage the crop window into LDS: dword loads from L2 (the map is
+  // cache-resident), lane-consecutive dword LDS stores (conflict-free)
+  {
+    uint32_t* l32 = (uint32_t*)lds;
+    const uint32_t* src = (const uint32_t*)(K.map + (int64_t)ymin * P.map_pitch + xa);
+    const int pitch4 = P.map_pitch >> 2;
+    const int total = C * W4;
+    const float inv = 1.0f / (float)W4;
+    for (int q = threadIdx.x; q < total; q += 256) {
+      const int row = (int)(((float)q + 0.5f) * inv);  // exact: q < 2^17, margin 0.5/W4
+      const int col = q - row * W4;
+      l32[row * sd + col] = src[(int64_t)row * pitch4 + col];
+    }
   }
   __syncthreads();
 
@@ -465,11 +475,11 @@ __device__ __forceinline__ void raster_env(const KArgs& K, const DRec& r, uint8_
           int sz = RAI(r, CBEV_AI_SIZE, a);
           int rx = d_rect_lo(RAD(r, CBEV_AD_X, a), P.pad, sz) - xmin;
           int ry = d_rect_lo(RAD(r, CBEV_AD_Y, a), P.pad, sz) - ymin;
-          lds_paint_px(lds, stride, shift, C, rx, ry, sz, threadIdx.x & 15,
+          lds_paint_px(lds, sb, shift, C, rx, ry, sz, threadIdx.x & 15,
                        pass == 0 ? CBEV_PX_VEHICLE : CBEV_PX_PEDESTRIAN);
         }
       }
-      __syncthreads();
+      if (a1 > a0) __syncthreads();
     }
     const int nt = r.hi[CBEV_HI_NROUTE];
     for (int base = 0; base < nt; base += 16) {
@@ -478,7 +488,7 @@ __device__ __forceinline__ void raster_env(const KArgs& K, const DRec& r, uint8_
         int sz = (i < nt - 1) ? 2 : 4;  // checkpoints 2x2, goal 4x4 (scenes/utils.py:114-122)
         int rx = d_rect_lo(r.cx[i], P.pad, sz) - xmin;
         int ry = d_rect_lo(r.cy[i], P.pad, sz) - ymin;
-        lds_paint_px(lds, stride, shift, C, rx, ry, sz, threadIdx.x & 15, CBEV_PX_ROUTE);
+        lds_paint_px(lds, sb, shift, C, rx, ry, sz, threadIdx.x & 15, CBEV_PX_ROUTE);
       }
     }
     __syncthreads();
@@ -489,14 +499,14 @@ __device__ __forceinline__ void raster_env(const KArgs& K, const DRec& r, uint8_
       uint8_t col = (uint8_t)r.ti[CBEV_TI_COLOR * r.T + k];
       for (int p = threadIdx.x; p < rw * rh; p += 256) {
         int px = rx + p % rw, py = ry + p / rw;
-        if (px >= 0 && py >= 0 && px < C && py < C) lds[py * stride + shift + px] = col;
+        if (px >= 0 && py >= 0 && px < C && py < C) lds[py * sb + shift + px] = col;
       }
       __syncthreads();
     }
   }
 
   // ---- rotate (pygame transform.rotate / rotate90) + compose + ego overlay
-  const uint8_t bg = lds[shift];  // crop top-left pixel after painting
+  const uint32_t bg = lds[shift];  // crop top-left pixel after painting
   const float angle = RESET ? 90.0f : (float)(d_degrees(yaw) + 90);
   const bool r90 = fmod((double)angle, (double)90.0f) == 0.0;
   int nx = C, ny = C, numturns = 0;
@@ -514,52 +524,65 @@ __device__ __forceinline__ void raster_env(const KArgs& K, const DRec& r, uint8_
     nx = (int)m1;
     ny = (int)m2;
     icy = ny / 2;
-    xd = (C - nx) * 32768;
+    xd = (C - nx) * 32768;  // (src->w - dst->w) << 15
     yd = (C - ny) * 32768;
     isin = (int)(sn * 65536);
     icos = (int)(cs * 65536);
     axf = (nx << 15) - (int)(cs * ((nx - 1) << 15));
     ayf = (ny << 15) - (int)(sn * ((nx - 1) << 15));
   }
-  const int xmaxv = (C << 16) - 1, ymaxv = (C << 16) - 1;
-  const int rx0 = P.anchor_x - nx / 2, ry0 = P.anchor_y - ny / 2;
+  const uint32_t xmaxv = (uint32_t)((C << 16) - 1), ymaxv = (uint32_t)((C << 16) - 1);
+  const int rx0 = P.anchor_x - nx / 2, ry0 = P.anchor_y - ny / 2;  // get_rect(center=anchor)
   const int hx0 = P.anchor_x - P.hero_w / 2, hy0 = P.anchor_y - P.hero_w / 2;
   const int hx1 = hx0 + P.hero_w, hy1 = hy0 + P.hero_w;
-  const int cpr = S / 16;  // 16-pixel chunks per output row
-  for (int q = threadIdx.x; q < S * cpr; q += 256) {
-    const int v = q / cpr, u0 = (q - v * cpr) * 16;
-    uint32_t w[4] = {0, 0, 0, 0};
-    const int yy = v - ry0;
-    const bool row_in = (yy >= 0 && yy < ny);
-    const bool hrow = (v >= hy0 && v < hy1);
-    int dxr = 0, dyr = 0;
-    if (!r90) {
-      dxr = (axf + (isin * (icy - yy))) + xd;
-      dyr = (ayf - (icos * (icy - yy))) + yd;
-    }
+  // the rotated image covers the whole output (anchor-centred default) -> no compose clipping
+  const bool full = rx0 <= 0 && ry0 <= 0 && rx0 + nx >= S && ry0 + ny >= S;
+  // rotate90: source byte = base(row) + xx * step
+  const int step = !r90 ? 0 : (numturns == 0 ? 1 : numturns == 1 ? sb : numturns == 2 ? -1 : -sb);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int nunits = (S * S) >> 8;
+  for (int unit = wave; unit < nunits; unit += 4) {
+    const int p0 = unit << 8;
+    uint32_t Pk = 0;
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      const int u = u0 + k;
-      const int xx = u - rx0;
+    for (int j = 0; j < 4; ++j) {
+      const int pj = p0 + 64 * j;  // wave-uniform: 64 | S, so one output row
+      const int v = pj / S, u0 = pj - v * S;
+      const int yy = v - ry0;
+      const int xx = u0 + lane - rx0;
       uint32_t px = CBEV_PX_BLACK;
-      if (row_in && xx >= 0 && xx < nx) {
+      if (full || (yy >= 0 && yy < ny && xx >= 0 && xx < nx)) {
         if (r90) {
-          int ri, ci;
-          if (numturns == 0) { ri = yy; ci = xx; }
-          else if (numturns == 1) { ri = xx; ci = C - 1 - yy; }
-          else if (numturns == 2) { ri = C - 1 - yy; ci = C - 1 - xx; }
-          else { ri = C - 1 - xx; ci = yy; }
-          px = lds[ri * stride + shift + ci];
+          const int base = numturns == 0   ? yy * sb + shift
+                           : numturns == 1 ? shift + C - 1 - yy
+                           : numturns == 2 ? (C - 1 - yy) * sb + shift + C - 1
+                                           : (C - 1) * sb + shift + yy;
+          px = lds[base + xx * step];
         } else {
-          int dx = dxr + xx * icos, dy = dyr + xx * isin;
-          px = (dx < 0 || dy < 0 || dx > xmaxv || dy > ymaxv) ? bg : lds[(dy >> 16) * stride + shift + (dx >> 16)];
+          const int dxr = (axf + (isin * (icy - yy))) + xd;
+          const int dyr = (ayf - (icos * (icy - yy))) + yd;
+          const int dx = dxr + xx * icos, dy = dyr + xx * isin;
+          px = ((uint32_t)dx > xmaxv || (uint32_t)dy > ymaxv) ? bg : (uint32_t)lds[(dy >> 16) * sb + shift + (dx >> 16)];
         }
       }
-      if (hrow && u >= hx0 && u < hx1) px = CBEV_PX_BLACK;
-      w[k >> 2] |= px << (8 * (k & 3));
+      Pk |= px << (8 * j);
     }
-    const uint4 val = make_uint4(w[0], w[1], w[2], w[3]);
-    for (int k = 0; k < nout; ++k) *(uint4*)(out + k * out_stride + v * S + u0) = val;
+    // transpose: lane l collects pixels 4l..4l+3 = byte (l >> 4) of lanes (4l + k) & 63
+    const int sel = 8 * (lane >> 4);
+    uint32_t D = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t Q = (uint32_t)__builtin_amdgcn_ds_bpermute(((4 * lane + k) & 63) << 2, (int)Pk);
+      D |= ((Q >> sel) & 255u) << (8 * k);
+    }
+    const int pd = p0 + 4 * lane;
+    const int vd = pd / S, ud = pd - vd * S;
+    if (vd >= hy0 && vd < hy1) {  // Hero.draw: black w x w rect at the anchor (hero.py:26-32)
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (ud + k >= hx0 && ud + k < hx1) D = (D & ~(255u << (8 * k))) | ((uint32_t)CBEV_PX_BLACK << (8 * k));
+    }
+    for (int o = 0; o < nout; ++o) *(uint32_t*)(out + o * out_stride + pd) = D;
   }
 }
 
@@ -618,11 +641,12 @@ __device__ __forceinline__ double d_lateral_error(double px, double py, const do
   return min_error;
 }
 
-__global__ __launch_bounds__(256) void k_collide(KArgs K, uint8_t* __restrict__ recs, int n, double* __restrict__ reward_out,
-                                                 uint8_t* __restrict__ term_out, uint8_t* __restrict__ trunc_out,
-                                                 int32_t* __restrict__ cause_out, float* __restrict__ info_out) {
-  const int lane = threadIdx.x & 63;
-  const int e = blockIdx.x * 4 + (threadIdx.x >> 6);
+// One thread per env: the per-env work here is a few short serial loops plus
+// a float64 scalar chain, so 64 envs share a wave.
+__global__ __launch_bounds__(64) void k_collide(KArgs K, uint8_t* __restrict__ recs, int n, double* __restrict__ reward_out,
+                                                uint8_t* __restrict__ term_out, uint8_t* __restrict__ trunc_out,
+                                                int32_t* __restrict__ cause_out, float* __restrict__ info_out) {
+  const int e = blockIdx.x * 64 + threadIdx.x;
   if (e >= n) return;
   DRec r = bind_rec(recs + (int64_t)e * K.L.record_bytes, K.L, K.C);
   const cbev_params& P = K.P;
@@ -644,7 +668,7 @@ __global__ __launch_bounds__(256) void k_collide(KArgs K, uint8_t* __restrict__ 
   const double hx_m = x * CB_MPP, hy_m = y * CB_MPP, hv_m = v * CB_MPP;
   const double hvx_m = hv_m * cos(yaw), hvy_m = hv_m * sin(yaw);
   const double hvx = v * cos(yaw), hvy = v * sin(yaw);
-  for (int a = lane; a < nact; a += 64) {
+  for (int a = 0; a < nact; ++a) {
     const int sz = RAI(r, CBEV_AI_SIZE, a);
     const double ax = RAD(r, CBEV_AD_X, a), ay = RAD(r, CBEV_AD_Y, a);
     const int arx = d_rect_lo(ax, P.pad, sz), ary = d_rect_lo(ay, P.pad, sz);
@@ -678,25 +702,21 @@ __global__ __launch_bounds__(256) void k_collide(KArgs K, uint8_t* __restrict__ 
     }
     if (hit) last_hit = a;
   }
-  for (int i = lane; i < nt; i += 64) {
+  for (int i = 0; i < nt; ++i) {
     if (!((r.vis[i >> 5] >> (i & 31)) & 1u)) continue;
     const int sz = (i < nt - 1) ? 2 : 4;
     const int trx = d_rect_lo(r.cx[i], P.pad, sz), try_ = d_rect_lo(r.cy[i], P.pad, sz);
     if (hrx < trx + sz && hry < try_ + sz && hrx + hw > trx && hry + hw > try_) {
-      atomicAnd(&r.vis[i >> 5], ~(1u << (i & 31)));  // every visible target hit is consumed
-      last_hit = nact + i;
+      r.vis[i >> 5] &= ~(1u << (i & 31));  // every visible target hit is consumed
+      last_hit = nact + i;  // the last hit in iteration order wins
     }
   }
-  last_hit = wave_max_i(last_hit);
-  nas = wave_sum_i(nas);
-  ttc_carl = wave_min(ttc_carl);
-  ttc_sh = wave_min(ttc_sh);
 
   // ---- CaRL route progress: arg-min over raw-route segments (carl_reward_fn.py:29-58)
   const int nraw = hi[CBEV_HI_NRAW];
   double bdist = 1e9;
-  int bseg = 0x7fffffff;
-  for (int i = lane; i < nraw - 1; i += 64) {
+  int bseg = 0;
+  for (int i = 0; i < nraw - 1; ++i) {
     const int abx_i = r.raw_x[i + 1] - r.raw_x[i], aby_i = r.raw_y[i + 1] - r.raw_y[i];
     const double ax = r.raw_x[i], ay = r.raw_y[i];
     const double apx = x - ax, apy = y - ay;
@@ -708,9 +728,7 @@ __global__ __launch_bounds__(256) void k_collide(KArgs K, uint8_t* __restrict__ 
       bseg = i;
     }
   }
-  wave_argmin(bdist, bseg);
 
-  if (lane != 0) return;
 
   int result = CBEV_COLL_NONE, coll_id = -1;
   if (last_hit >= 0) {
@@ -1064,7 +1082,7 @@ static KArgs kargs(const cbev_ctx* c) {
   return K;
 }
 
-static size_t raster_lds_bytes(const cbev_params& P) { return (size_t)P.crop * (size_t)((P.crop + 30) / 16) * 16; }
+static size_t raster_lds_bytes(const cbev_params& P) { return (size_t)P.crop * (size_t)raster_stride_dwords(P.crop) * 4; }
 
 extern "C" {
 
@@ -1098,7 +1116,7 @@ const char* cbev_field_names(int group) {
 int cbev_create(const cbev_params* params, const cbev_caps* caps, int device, cbev_ctx** out) {
   if (!params || !caps || !out) return set_err(CBEV_EINVAL, "null argument");
   const cbev_params& P = *params;
-  if (P.size <= 0 || P.size % 16 != 0) return set_err(CBEV_EINVAL, "size %d must be a positive multiple of 16", P.size);
+  if (P.size <= 0 || P.size % 64 != 0) return set_err(CBEV_EINVAL, "size %d must be a positive multiple of 64", P.size);
   if (P.crop < P.size || P.crop > 400) return set_err(CBEV_EINVAL, "crop %d out of range", P.crop);
   if (P.map_pitch % 16 != 0 || P.map_pitch < P.render_w) return set_err(CBEV_EINVAL, "bad map pitch %d", P.map_pitch);
   if (P.render_w != P.map_w + 2 * P.pad || P.render_h != P.map_h + 2 * P.pad) return set_err(CBEV_EINVAL, "bad render shape");
@@ -1197,11 +1215,13 @@ int cbev_step(cbev_ctx* c, void* records, int n, const void* actions, uint8_t* f
   hipEvent_t* ev = nullptr;
   if (c->prof_on && c->prof_n < CBEV_PROF_MAX) ev = c->prof_ev + 4 * c->prof_n++;
   if (ev) HIP_TRY(hipEventRecord(ev[0], s));
-  hipLaunchKernelGGL(k_dyn, dim3(wg4), dim3(256), 0, s, K, (uint8_t*)records, n, actions);
+  hipLaunchKernelGGL(k_hero, dim3((n + 63) / 64), dim3(64), 0, s, K, (uint8_t*)records, n, actions);
+  if (c->C.actor_cap > 0) hipLaunchKernelGGL(k_actors, dim3(wg4), dim3(256), 0, s, K, (uint8_t*)records, n);
   if (ev) HIP_TRY(hipEventRecord(ev[1], s));
   hipLaunchKernelGGL(k_raster, dim3(n), dim3(256), raster_lds_bytes(c->P), s, K, (uint8_t*)records, n, frames);
   if (ev) HIP_TRY(hipEventRecord(ev[2], s));
-  hipLaunchKernelGGL(k_collide, dim3(wg4), dim3(256), 0, s, K, (uint8_t*)records, n, reward, term, trunc, cause, info);
+  hipLaunchKernelGGL(k_collide, dim3((n + 63) / 64), dim3(64), 0, s, K, (uint8_t*)records, n, reward, term, trunc, cause,
+                     info);
   if (ev) HIP_TRY(hipEventRecord(ev[3], s));
   HIP_TRY(hipGetLastError());
   return CBEV_OK;

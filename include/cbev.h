@@ -89,7 +89,7 @@ int cbev_expand_obs(cbev_ctx* ctx, const uint8_t* ring, int n, int n_frames, int
  * of the three step kernels (used by bench.py for the roofline figure).
  * cbev_profile(ctx, 1) resets the counters and starts recording (up to 8192
  * steps); cbev_profile_read synchronises on the last event and returns the
- * summed milliseconds of [k_dyn, k_raster, k_collide] and the step count. */
+ * summed milliseconds of [k_hero + k_actors, k_raster, k_collide] and the step count. */
 int cbev_profile(cbev_ctx* ctx, int enable);
 int cbev_profile_read(cbev_ctx* ctx, double* ms3, int64_t* steps);
 
