@@ -9,11 +9,12 @@
 //              Reference: Scene._scene_step (scene.py:90-98), hero.py:88-187,
 //              actor.py:110-124, behavior/*.py, stanley_controller.py:51-123.
 //   k_raster   256-thread workgroup per env: stage the C x C crop of the padded
-//              class map into LDS (16-B loads), paint vehicles / pedestrians /
-//              visible targets / traffic lights in draw order, then the
-//              pygame rotate (16.16 fixed-point inverse map or exact rotate90)
-//              + compose at the ego anchor + ego overlay, written once to HBM
-//              as one palette id per pixel with 16-B stores.
+//              class map into LDS (LDS-DMA, lane-linear odd-stride image),
+//              paint vehicles / pedestrians / visible targets / traffic lights
+//              in draw order, then the pygame rotate (16.16 fixed-point inverse
+//              map, stepped per lane, or exact rotate90) + compose at the ego
+//              anchor + ego overlay, written once to HBM as one palette id per
+//              pixel (64-byte contiguous runs per wave store).
 //              Reference: BaseMap.draw_fov (world.py:137-157), fov.py:70-99,
 //              actor_manager.py:121-132, hero.py:26-32.
 //   k_collide  one thread per env: ego tile, rect collisions (last hit in
@@ -412,9 +413,10 @@ __device__ __forceinline__ int d_rect_lo(double w, int pad, int size) { return (
 
 // LDS image of the crop window: crop row r starts at dword r * sd, holding the
 // padded-map bytes from xa = xmin & ~3 on (so crop column c is byte
-// r*4*sd + shift + c, shift = xmin & 3). sd is odd: crop rows land in different
-// LDS banks, which keeps the gathers along rotated rows conflict-free for the
-// axis-aligned cases and spread for the rest.
+// r*4*sd + shift + c, shift = xmin & 3). sd is odd so that successive crop
+// rows start in different LDS banks: gathers along a rotated output row then
+// spread over the banks for every angle. The image is one contiguous run of
+// C*sd dwords, which lets LDS-DMA fill it lane-linearly.
 __host__ __device__ __forceinline__ int raster_row_dwords(int C) { return (C + 6) / 4; }
 __host__ __device__ __forceinline__ int raster_stride_dwords(int C) { return raster_row_dwords(C) | 1; }
 
@@ -428,38 +430,212 @@ __device__ __forceinline__ void lds_paint_px(uint8_t* lds, int sb, int shift, in
   lds[py * sb + shift + px] = col;
 }
 
+// Per-env rotation parameters (pygame transform.rotate, 16.16 fixed point;
+// rotate90 for exact multiples of 90 degrees) and the compose placement.
+struct RotSetup {
+  bool r90;
+  int nx, ny;                  // rotated surface size
+  int isin, icos;              // 16.16 sin/cos
+  int dx00, dy00;              // source 16.16 coordinates of rotated pixel (0, 0)
+  int a00, ustep, vstep;       // rotate90: LDS byte of rotated pixel (0,0) and its steps
+  int rx0, ry0;                // rotated surface top-left in the output (get_rect(center=anchor))
+};
+
+__device__ __forceinline__ RotSetup rot_setup(const cbev_params& P, float angle, int sb) {
+  RotSetup R;
+  const int C = P.crop;
+  R.r90 = fmod((double)angle, (double)90.0f) == 0.0;
+  R.nx = C;
+  R.ny = C;
+  R.isin = R.icos = R.dx00 = R.dy00 = 0;
+  R.a00 = 0;
+  R.ustep = 1;
+  R.vstep = sb;
+  if (R.r90) {
+    int numturns = ((int)angle / 90) % 4;
+    if (numturns < 0) numturns += 4;
+    // rotated pixel (xx, yy) reads LDS byte a00 + xx*ustep + yy*vstep (rotate90 per turn count)
+    switch (numturns) {
+      case 0: R.a00 = 0;                     R.ustep = 1;   R.vstep = sb;  break;
+      case 1: R.a00 = C - 1;                 R.ustep = sb;  R.vstep = -1;  break;
+      case 2: R.a00 = (C - 1) * sb + C - 1;  R.ustep = -1;  R.vstep = -sb; break;
+      default: R.a00 = (C - 1) * sb;         R.ustep = -sb; R.vstep = 1;   break;
+    }
+  } else {
+    double rad = angle * .01745329251994329;
+    double sn = sin(rad), cs = cos(rad);
+    double xw = C, yh = C;
+    double cxw = cs * xw, cyh = cs * yh, sxw = sn * xw, syh = sn * yh;
+    double m1 = fmax(fmax(fmax(fabs(cxw + syh), fabs(cxw - syh)), fabs(-cxw + syh)), fabs(-cxw - syh));
+    double m2 = fmax(fmax(fmax(fabs(sxw + cyh), fabs(sxw - cyh)), fabs(-sxw + cyh)), fabs(-sxw - cyh));
+    R.nx = (int)m1;
+    R.ny = (int)m2;
+    const int icy = R.ny / 2;
+    const int xd = (C - R.nx) * 32768;  // (src->w - dst->w) << 15
+    const int yd = (C - R.ny) * 32768;
+    R.isin = (int)(sn * 65536);
+    R.icos = (int)(cs * 65536);
+    const int axf = (R.nx << 15) - (int)(cs * ((R.nx - 1) << 15));
+    const int ayf = (R.ny << 15) - (int)(sn * ((R.nx - 1) << 15));
+    // rotozoom inner loop: dx = (ax + isin*(cy - y)) + xd + x*icos, dy = (ay - icos*(cy - y)) + yd + x*isin;
+    // every term stays far inside int32, so it is affine in (x, y) and can be stepped exactly
+    R.dx00 = (axf + R.isin * icy) + xd;
+    R.dy00 = (ayf - R.icos * icy) + yd;
+  }
+  R.rx0 = P.anchor_x - R.nx / 2;
+  R.ry0 = P.anchor_y - R.ny / 2;
+  return R;
+}
+
+// Output pass over one wave's chunks of 1024 output pixels: gather j (0..15) of
+// a chunk has lane l sample output pixel (row r0 + j / G, column 64 (j % G) + l),
+// so a gather walks 64 consecutive pixels of one output row (consecutive lanes
+// read neighbouring source pixels: few distinct LDS dwords, spread banks) and
+// its byte store is a contiguous 64-byte run. Source coordinates are stepped,
+// not recomputed: per gather two adds, a shift/multiply-add for the LDS byte
+// address, the LDS read and the store.
+//   CHECK = false: the rotated surface covers the whole output and every output
+//   pixel samples inside the crop (checked once per env at the four corners;
+//   the map is affine) -> no per-pixel tests.
+//   CHECK = true: compose clipping (black outside the rotated surface) and the
+//   rotozoom background test (bg outside the source), per pixel.
+template <int G, bool R90, bool CHECK>
+__device__ __forceinline__ void raster_out(const cbev_params& P, const RotSetup& R, const uint8_t* __restrict__ lds,
+                                           int shift, uint32_t bg, uint8_t* __restrict__ out, int nout,
+                                           int64_t out_stride, int lane, int wave) {
+  constexpr int RPC = 16 / G;  // output rows per chunk
+  const int S = P.size, C = P.crop;
+  const uint32_t vmax = (uint32_t)((C << 16) - 1);
+  const int hero_w = P.hero_w;
+  const int hx0 = P.anchor_x - hero_w / 2, hy0 = P.anchor_y - hero_w / 2;
+  // per-lane hero columns (Hero.draw: black w x w rect at the anchor, hero.py:26-32)
+  uint32_t hcol = 0, xok = 0;
+#pragma unroll
+  for (int cj = 0; cj < G; ++cj) {
+    const int u = 64 * cj + lane;
+    if (u >= hx0 && u < hx0 + hero_w) hcol |= 1u << cj;
+    const int xx = u - R.rx0;
+    if (xx >= 0 && xx < R.nx) xok |= 1u << cj;
+  }
+  const int r0 = wave * RPC;
+  const int xx0 = lane - R.rx0, yy0 = r0 - R.ry0;
+  // lane state at (output column lane, output row r0 of this wave's first chunk)
+  int sx = R.dx00 + xx0 * R.icos - yy0 * R.isin;  // 16.16 source x (general)
+  int sy = R.dy00 + xx0 * R.isin + yy0 * R.icos;  // 16.16 source y (general)
+  int sa = R.a00 + shift + xx0 * R.ustep + yy0 * R.vstep;  // LDS byte (rotate90)
+  // unchecked general path: the crop byte offset rides in the integer part of sx
+  // (sx stays positive there), so the LDS address is (sy >> 16) * sb + (sx >> 16)
+  const uint8_t* img = (R90 || !CHECK) ? lds : lds + shift;
+  if (!R90 && !CHECK) sx += shift << 16;
+  const uint32_t sb = (uint32_t)R.vstep;
+  const int chunk_rows = 4 * RPC;                 // the 4 waves interleave chunks
+  const int nchunks = S / RPC;
+  for (int ch = wave, r = r0; ch < nchunks; ch += 4, r += chunk_rows) {
+    uint8_t* o = out + (int64_t)r * S + lane;
+    const bool hero_rows = (unsigned)(r + RPC - 1 - hy0) < (unsigned)(RPC - 1 + hero_w);  // chunk meets the hero rows
+    uint32_t px[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int rj = j / G, cj = j % G;
+      uint32_t v;
+      if (R90) {
+        const int a = sa + rj * R.vstep + 64 * cj * R.ustep;
+        if (CHECK) {
+          const bool ok = ((xok >> cj) & 1u) && (unsigned)(r + rj - R.ry0) < (unsigned)R.ny;
+          v = ok ? (uint32_t)img[ok ? a : 0] : (uint32_t)CBEV_PX_BLACK;
+        } else {
+          v = img[a];
+        }
+      } else {
+        const int dx = sx + (64 * cj * R.icos - rj * R.isin);
+        const int dy = sy + (64 * cj * R.isin + rj * R.icos);
+        if (CHECK) {
+          const bool ok = ((xok >> cj) & 1u) && (unsigned)(r + rj - R.ry0) < (unsigned)R.ny;
+          const bool in = (uint32_t)dx <= vmax && (uint32_t)dy <= vmax;
+          const uint32_t s = img[(in && ok) ? __umul24((uint32_t)dy >> 16, sb) + ((uint32_t)dx >> 16) : 0u];
+          v = !ok ? (uint32_t)CBEV_PX_BLACK : (in ? s : bg);
+        } else {
+          v = img[__umul24((uint32_t)dy >> 16, sb) + ((uint32_t)dx >> 16)];
+        }
+      }
+      px[j] = v;
+    }
+    if (hero_rows) {
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const int rj = j / G, cj = j % G;
+        if ((unsigned)(r + rj - hy0) < (unsigned)hero_w && ((hcol >> cj) & 1u)) px[j] = CBEV_PX_BLACK;
+      }
+    }
+    for (int k = 0; k < nout; ++k) {
+#pragma unroll
+      for (int j = 0; j < 16; ++j) o[(int64_t)k * out_stride + (j / G) * S + 64 * (j % G)] = (uint8_t)px[j];
+    }
+    sx -= chunk_rows * R.isin;
+    sy += chunk_rows * R.icos;
+    sa += chunk_rows * R.vstep;
+  }
+}
+
+template <int G>
+__device__ __forceinline__ void raster_out_dispatch(const cbev_params& P, const RotSetup& R, const uint8_t* lds,
+                                                    int shift, uint32_t bg, uint8_t* out, int nout, int64_t out_stride,
+                                                    int lane, int wave) {
+  const int S = P.size;
+  // compose: does the rotated surface cover the whole output?
+  const bool full = R.rx0 <= 0 && R.ry0 <= 0 && R.rx0 + R.nx >= S && R.ry0 + R.ny >= S;
+  if (R.r90) {
+    if (full) raster_out<G, true, false>(P, R, lds, shift, bg, out, nout, out_stride, lane, wave);
+    else      raster_out<G, true, true>(P, R, lds, shift, bg, out, nout, out_stride, lane, wave);
+    return;
+  }
+  // every output pixel inside the source: check the four output corners
+  bool inb = full;
+  const uint32_t vmax = (uint32_t)((P.crop << 16) - 1);
+  for (int c = 0; c < 4 && inb; ++c) {
+    const int64_t xx = (int64_t)((c & 1) ? S - 1 : 0) - R.rx0, yy = (int64_t)((c & 2) ? S - 1 : 0) - R.ry0;
+    const int64_t dx = R.dx00 + xx * R.icos - yy * R.isin, dy = R.dy00 + xx * R.isin + yy * R.icos;
+    inb = dx >= 0 && dy >= 0 && dx <= (int64_t)vmax && dy <= (int64_t)vmax;
+  }
+  if (inb) raster_out<G, false, false>(P, R, lds, shift, bg, out, nout, out_stride, lane, wave);
+  else     raster_out<G, false, true>(P, R, lds, shift, bg, out, nout, out_stride, lane, wave);
+}
+
 // Render one env's observation (whole 256-thread workgroup). RESET: BaseMap.reset's
 // frame (theta = 0, no actors drawn, world.py:92-100). The frame is written to
 // `nout` destinations out + k*out_stride (the frame-stack ring on reset).
-//
-// Output mapping: each wave renders units of 256 consecutive output pixels;
-// gather j (0..3) has lane l sample pixel 64j + l (a 64-pixel run of one output
-// row, so consecutive lanes read along a rotated source row), and a ds_bpermute
-// transpose then gives lane l the 4 consecutive pixels 4l..4l+3 it stores as one
-// dword (256 contiguous bytes per wave store).
-template <bool RESET>
+template <bool RESET, int G>
 __device__ __forceinline__ void raster_env(const KArgs& K, const DRec& r, uint8_t* __restrict__ out, int nout,
                                            int64_t out_stride, uint8_t* __restrict__ lds) {
   const cbev_params& P = K.P;
-  const int C = P.crop, S = P.size;
+  const int C = P.crop;
   const double x = r.hd[CBEV_HD_X], y = r.hd[CBEV_HD_Y], yaw = r.hd[CBEV_HD_YAW];
   int xmin, ymin;
   d_crop_origin(P, x, y, &xmin, &ymin);
   const int xa = xmin & ~3, shift = xmin - xa;
-  const int W4 = raster_row_dwords(C), sd = raster_stride_dwords(C), sb = 4 * sd;
+  const int sd = raster_stride_dwords(C), sb = 4 * sd;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
 
-  // ---- stage the crop window into LDS: dword loads from L2 (the map is
-  // cache-resident), lane-consecutive dword LDS stores (conflict-free)
+  // ---- stage the crop window into LDS by LDS-DMA (global_load_lds_dword): the
+  // image is lane-linear, dword q = row * sd + col; each wave-instruction moves
+  // 64 consecutive dwords, the lane's source address steps with q.
   {
-    uint32_t* l32 = (uint32_t*)lds;
-    const uint32_t* src = (const uint32_t*)(K.map + (int64_t)ymin * P.map_pitch + xa);
-    const int pitch4 = P.map_pitch >> 2;
-    const int total = C * W4;
-    const float inv = 1.0f / (float)W4;
-    for (int q = threadIdx.x; q < total; q += 256) {
-      const int row = (int)(((float)q + 0.5f) * inv);  // exact: q < 2^17, margin 0.5/W4
-      const int col = q - row * W4;
-      l32[row * sd + col] = src[(int64_t)row * pitch4 + col];
+    const uint8_t* gbase = K.map + (int64_t)ymin * P.map_pitch + xa;
+    const int total = C * sd;
+    const int dr = 256 / sd, dc = 256 - dr * sd;
+    const int q0 = wave * 64 + lane;
+    int row = q0 / sd, col = q0 - row * sd;
+    for (int b = wave * 64; b < total; b += 256) {
+      if (b + lane < total)
+        __builtin_amdgcn_global_load_lds((const void*)(gbase + (int64_t)row * P.map_pitch + 4 * col),
+                                         (__attribute__((address_space(3))) void*)(lds + 4 * b), 4, 0, 0);
+      row += dr;
+      col += dc;
+      if (col >= sd) {
+        col -= sd;
+        ++row;
+      }
     }
   }
   __syncthreads();
@@ -506,93 +682,26 @@ __device__ __forceinline__ void raster_env(const KArgs& K, const DRec& r, uint8_
   }
 
   // ---- rotate (pygame transform.rotate / rotate90) + compose + ego overlay
-  const uint32_t bg = lds[shift];  // crop top-left pixel after painting
+  const uint8_t* img = lds + shift;
+  const uint32_t bg = img[0];  // crop top-left pixel after painting
   const float angle = RESET ? 90.0f : (float)(d_degrees(yaw) + 90);
-  const bool r90 = fmod((double)angle, (double)90.0f) == 0.0;
-  int nx = C, ny = C, numturns = 0;
-  int isin = 0, icos = 0, axf = 0, ayf = 0, xd = 0, yd = 0, icy = 0;
-  if (r90) {
-    numturns = ((int)angle / 90) % 4;
-    if (numturns < 0) numturns += 4;
-  } else {
-    double rad = angle * .01745329251994329;
-    double sn = sin(rad), cs = cos(rad);
-    double xw = C, yh = C;
-    double cxw = cs * xw, cyh = cs * yh, sxw = sn * xw, syh = sn * yh;
-    double m1 = fmax(fmax(fmax(fabs(cxw + syh), fabs(cxw - syh)), fabs(-cxw + syh)), fabs(-cxw - syh));
-    double m2 = fmax(fmax(fmax(fabs(sxw + cyh), fabs(sxw - cyh)), fabs(-sxw + cyh)), fabs(-sxw - cyh));
-    nx = (int)m1;
-    ny = (int)m2;
-    icy = ny / 2;
-    xd = (C - nx) * 32768;  // (src->w - dst->w) << 15
-    yd = (C - ny) * 32768;
-    isin = (int)(sn * 65536);
-    icos = (int)(cs * 65536);
-    axf = (nx << 15) - (int)(cs * ((nx - 1) << 15));
-    ayf = (ny << 15) - (int)(sn * ((nx - 1) << 15));
-  }
-  const uint32_t xmaxv = (uint32_t)((C << 16) - 1), ymaxv = (uint32_t)((C << 16) - 1);
-  const int rx0 = P.anchor_x - nx / 2, ry0 = P.anchor_y - ny / 2;  // get_rect(center=anchor)
-  const int hx0 = P.anchor_x - P.hero_w / 2, hy0 = P.anchor_y - P.hero_w / 2;
-  const int hx1 = hx0 + P.hero_w, hy1 = hy0 + P.hero_w;
-  // the rotated image covers the whole output (anchor-centred default) -> no compose clipping
-  const bool full = rx0 <= 0 && ry0 <= 0 && rx0 + nx >= S && ry0 + ny >= S;
-  // rotate90: source byte = base(row) + xx * step
-  const int step = !r90 ? 0 : (numturns == 0 ? 1 : numturns == 1 ? sb : numturns == 2 ? -1 : -sb);
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int nunits = (S * S) >> 8;
-  for (int unit = wave; unit < nunits; unit += 4) {
-    const int p0 = unit << 8;
-    uint32_t Pk = 0;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int pj = p0 + 64 * j;  // wave-uniform: 64 | S, so one output row
-      const int v = pj / S, u0 = pj - v * S;
-      const int yy = v - ry0;
-      const int xx = u0 + lane - rx0;
-      uint32_t px = CBEV_PX_BLACK;
-      if (full || (yy >= 0 && yy < ny && xx >= 0 && xx < nx)) {
-        if (r90) {
-          const int base = numturns == 0   ? yy * sb + shift
-                           : numturns == 1 ? shift + C - 1 - yy
-                           : numturns == 2 ? (C - 1 - yy) * sb + shift + C - 1
-                                           : (C - 1) * sb + shift + yy;
-          px = lds[base + xx * step];
-        } else {
-          const int dxr = (axf + (isin * (icy - yy))) + xd;
-          const int dyr = (ayf - (icos * (icy - yy))) + yd;
-          const int dx = dxr + xx * icos, dy = dyr + xx * isin;
-          px = ((uint32_t)dx > xmaxv || (uint32_t)dy > ymaxv) ? bg : (uint32_t)lds[(dy >> 16) * sb + shift + (dx >> 16)];
-        }
-      }
-      Pk |= px << (8 * j);
-    }
-    // transpose: lane l collects pixels 4l..4l+3 = byte (l >> 4) of lanes (4l + k) & 63
-    const int sel = 8 * (lane >> 4);
-    uint32_t D = 0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const uint32_t Q = (uint32_t)__builtin_amdgcn_ds_bpermute(((4 * lane + k) & 63) << 2, (int)Pk);
-      D |= ((Q >> sel) & 255u) << (8 * k);
-    }
-    const int pd = p0 + 4 * lane;
-    const int vd = pd / S, ud = pd - vd * S;
-    if (vd >= hy0 && vd < hy1) {  // Hero.draw: black w x w rect at the anchor (hero.py:26-32)
-#pragma unroll
-      for (int k = 0; k < 4; ++k)
-        if (ud + k >= hx0 && ud + k < hx1) D = (D & ~(255u << (8 * k))) | ((uint32_t)CBEV_PX_BLACK << (8 * k));
-    }
-    for (int o = 0; o < nout; ++o) *(uint32_t*)(out + o * out_stride + pd) = D;
+  const RotSetup R = rot_setup(P, angle, sb);
+  switch (P.size >> 6) {
+    case 1: raster_out_dispatch<1>(P, R, lds, shift, bg, out, nout, out_stride, lane, wave); break;
+    case 2: raster_out_dispatch<2>(P, R, lds, shift, bg, out, nout, out_stride, lane, wave); break;
+    default: raster_out_dispatch<4>(P, R, lds, shift, bg, out, nout, out_stride, lane, wave); break;
   }
 }
 
+// G = size / 64 (64-pixel gathers per output row)
+template <int G>
 __global__ __launch_bounds__(256) void k_raster(KArgs K, uint8_t* __restrict__ recs, int n,
                                                 uint8_t* __restrict__ frames) {
   extern __shared__ __align__(16) uint8_t lds[];
   const int e = blockIdx.x;
   if (e >= n) return;
   DRec r = bind_rec(recs + (int64_t)e * K.L.record_bytes, K.L, K.C);
-  raster_env<false>(K, r, frames + (int64_t)e * K.P.size * K.P.size, 1, 0, lds);
+  raster_env<false, G>(K, r, frames + (int64_t)e * K.P.size * K.P.size, 1, 0, lds);
 }
 
 // Partial reset (SyncVectorEnv.reset with reset_mask -> CarlaBEV.reset):
@@ -600,6 +709,7 @@ __global__ __launch_bounds__(256) void k_raster(KArgs K, uint8_t* __restrict__ r
 // every slot of the frame-stack ring (FrameStackObservation padding "reset").
 // The frame is rendered from the bank record itself, so no other workgroup's
 // stores need to be visible.
+template <int G>
 __global__ __launch_bounds__(256) void k_reset(KArgs K, uint8_t* __restrict__ recs, int n,
                                                const uint8_t* __restrict__ bank, int n_bank,
                                                const uint8_t* __restrict__ mask, const int32_t* __restrict__ bank_idx,
@@ -621,7 +731,7 @@ __global__ __launch_bounds__(256) void k_reset(KArgs K, uint8_t* __restrict__ re
   }
   DRec r = bind_rec((uint8_t*)src, K.L, K.C);  // read-only use below
   const int64_t SS = (int64_t)K.P.size * K.P.size;
-  raster_env<true>(K, r, ring + (int64_t)e * SS, n_frames, (int64_t)n * SS, lds);
+  raster_env<true, G>(K, r, ring + (int64_t)e * SS, n_frames, (int64_t)n * SS, lds);
 }
 
 // ============================================================== k_collide
@@ -1082,6 +1192,12 @@ static KArgs kargs(const cbev_ctx* c) {
   return K;
 }
 
+static const void* raster_kernel(int size) {
+  return size == 64 ? (const void*)k_raster<1> : size == 128 ? (const void*)k_raster<2> : (const void*)k_raster<4>;
+}
+static const void* reset_kernel(int size) {
+  return size == 64 ? (const void*)k_reset<1> : size == 128 ? (const void*)k_reset<2> : (const void*)k_reset<4>;
+}
 static size_t raster_lds_bytes(const cbev_params& P) { return (size_t)P.crop * (size_t)raster_stride_dwords(P.crop) * 4; }
 
 extern "C" {
@@ -1116,7 +1232,7 @@ const char* cbev_field_names(int group) {
 int cbev_create(const cbev_params* params, const cbev_caps* caps, int device, cbev_ctx** out) {
   if (!params || !caps || !out) return set_err(CBEV_EINVAL, "null argument");
   const cbev_params& P = *params;
-  if (P.size <= 0 || P.size % 64 != 0) return set_err(CBEV_EINVAL, "size %d must be a positive multiple of 64", P.size);
+  if (P.size != 64 && P.size != 128 && P.size != 256) return set_err(CBEV_EINVAL, "size %d must be 64, 128 or 256", P.size);
   if (P.crop < P.size || P.crop > 400) return set_err(CBEV_EINVAL, "crop %d out of range", P.crop);
   if (P.map_pitch % 16 != 0 || P.map_pitch < P.render_w) return set_err(CBEV_EINVAL, "bad map pitch %d", P.map_pitch);
   if (P.render_w != P.map_w + 2 * P.pad || P.render_h != P.map_h + 2 * P.pad) return set_err(CBEV_EINVAL, "bad render shape");
@@ -1136,9 +1252,9 @@ int cbev_create(const cbev_params* params, const cbev_caps* caps, int device, cb
   hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(c_sg), &T, sizeof T);
   if (e == hipSuccess) e = hipMalloc(&c->lut_dev, 64 * sizeof(uint32_t));
   if (e == hipSuccess)
-    e = hipFuncSetAttribute((const void*)k_raster, hipFuncAttributeMaxDynamicSharedMemorySize, (int)raster_lds_bytes(P));
+    e = hipFuncSetAttribute(raster_kernel(P.size), hipFuncAttributeMaxDynamicSharedMemorySize, (int)raster_lds_bytes(P));
   if (e == hipSuccess)
-    e = hipFuncSetAttribute((const void*)k_reset, hipFuncAttributeMaxDynamicSharedMemorySize, (int)raster_lds_bytes(P));
+    e = hipFuncSetAttribute(reset_kernel(P.size), hipFuncAttributeMaxDynamicSharedMemorySize, (int)raster_lds_bytes(P));
   if (e != hipSuccess) {
     free(c);
     return set_err(CBEV_EHIP, "cbev_create: %s", hipGetErrorString(e));
@@ -1218,7 +1334,14 @@ int cbev_step(cbev_ctx* c, void* records, int n, const void* actions, uint8_t* f
   hipLaunchKernelGGL(k_hero, dim3((n + 63) / 64), dim3(64), 0, s, K, (uint8_t*)records, n, actions);
   if (c->C.actor_cap > 0) hipLaunchKernelGGL(k_actors, dim3(wg4), dim3(256), 0, s, K, (uint8_t*)records, n);
   if (ev) HIP_TRY(hipEventRecord(ev[1], s));
-  hipLaunchKernelGGL(k_raster, dim3(n), dim3(256), raster_lds_bytes(c->P), s, K, (uint8_t*)records, n, frames);
+  {
+    const size_t lb = raster_lds_bytes(c->P);
+    switch (c->P.size) {
+      case 64: hipLaunchKernelGGL(k_raster<1>, dim3(n), dim3(256), lb, s, K, (uint8_t*)records, n, frames); break;
+      case 128: hipLaunchKernelGGL(k_raster<2>, dim3(n), dim3(256), lb, s, K, (uint8_t*)records, n, frames); break;
+      default: hipLaunchKernelGGL(k_raster<4>, dim3(n), dim3(256), lb, s, K, (uint8_t*)records, n, frames); break;
+    }
+  }
   if (ev) HIP_TRY(hipEventRecord(ev[2], s));
   hipLaunchKernelGGL(k_collide, dim3((n + 63) / 64), dim3(64), 0, s, K, (uint8_t*)records, n, reward, term, trunc, cause,
                      info);
@@ -1235,8 +1358,17 @@ int cbev_reset(cbev_ctx* c, void* records, int n, const void* bank, int n_bank, 
   if (n_frames < 1) return set_err(CBEV_EINVAL, "n_frames < 1");
   if (n <= 0) return CBEV_OK;
   KArgs K = kargs(c);
-  hipLaunchKernelGGL(k_reset, dim3(n), dim3(256), raster_lds_bytes(c->P), (hipStream_t)stream, K, (uint8_t*)records, n,
-                     (const uint8_t*)bank, n_bank, mask, bank_idx, bank_offset, frames, n_frames);
+  const size_t lb = raster_lds_bytes(c->P);
+  hipStream_t s = (hipStream_t)stream;
+#define CBEV_LAUNCH_RESET(G_)                                                                                          \
+  hipLaunchKernelGGL(k_reset<G_>, dim3(n), dim3(256), lb, s, K, (uint8_t*)records, n, (const uint8_t*)bank, n_bank, mask, \
+                     bank_idx, bank_offset, frames, n_frames)
+  switch (c->P.size) {
+    case 64: CBEV_LAUNCH_RESET(1); break;
+    case 128: CBEV_LAUNCH_RESET(2); break;
+    default: CBEV_LAUNCH_RESET(4); break;
+  }
+#undef CBEV_LAUNCH_RESET
   HIP_TRY(hipGetLastError());
   return CBEV_OK;
 }
