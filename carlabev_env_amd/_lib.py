@@ -10,7 +10,8 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libcbev.so")
+# CBEV_LIB overrides the path (performance-experiment builds only)
+LIB_PATH = os.environ.get("CBEV_LIB") or os.path.join(HERE, "libcbev.so")
 
 _P = ctypes.c_void_p
 _I = ctypes.c_int

@@ -289,6 +289,141 @@ __device__ void d_actor_step(DRec& r, int a, double t) {
   RAD(r, CBEV_AD_TIME, a) += CB_DT;
 }
 
+// ============================================================== k_raster
+__device__ __forceinline__ void d_crop_origin(const cbev_params& P, double x, double y, int* xm, int* ym) {
+  const double C = (double)P.crop;
+  double offx = trunc(((double)P.pad + x) + (-C / 2));  // Follow.scroll int() (camera.py:39-42)
+  double offy = trunc(((double)P.pad + y) + (-C / 2));
+  int cxc = (int)rint(offx + C / 2.0);  // round() half-even (fov.py:70-79)
+  int cyc = (int)rint(offy + C / 2.0);
+  int xmin = cxc - P.crop / 2, ymin = cyc - P.crop / 2;
+  int maxx = P.render_w - P.crop, maxy = P.render_h - P.crop;
+  maxx = maxx < 0 ? 0 : maxx;
+  maxy = maxy < 0 ? 0 : maxy;
+  *xm = xmin < 0 ? 0 : (xmin > maxx ? maxx : xmin);
+  *ym = ymin < 0 ? 0 : (ymin > maxy ? maxy : ymin);
+}
+
+// rect_from_world_center (transforms.py:46-51): centre rounded half-even, x = c - w/2
+__device__ __forceinline__ int d_rect_lo(double w, int pad, int size) { return (int)rint((double)pad + w * 1.0) - size / 2; }
+
+// Phase mask for raster performance experiments (tools/raster_phases.sh):
+// 1 stage, 2 paint, 4 gather, 8 store. Products always build with all four.
+#ifndef CBEV_RASTER_PHASES
+#define CBEV_RASTER_PHASES 15
+#endif
+
+// LDS image of the crop window: crop row r starts at dword r * sd, holding the
+// padded-map bytes from xa = xmin & ~15 on (so crop column c is byte
+// r*4*sd + shift + c, shift = xmin & 15), copied as 16-byte chunks. sd is odd
+// so that successive crop rows start in different LDS banks: gathers along a
+// rotated output row then spread over the banks for every angle.
+__host__ __device__ __forceinline__ int raster_row_chunks(int C) { return (C + 30) / 16; }
+__host__ __device__ __forceinline__ int raster_stride_dwords(int C) { return (4 * raster_row_chunks(C)) | 1; }
+__host__ __device__ __forceinline__ int raster_image_bytes(int C) { return C * raster_stride_dwords(C) * 4; }
+
+// Paint a square rect of side sz (<= 4 * nb) into the LDS crop: 16 lanes per
+// rect, lane p covers pixel (p & 3, p >> 2) of each 4x4 block of the rect.
+__device__ __forceinline__ void lds_paint_rect(uint8_t* lds, int sb, int shift, int C, int rx, int ry, int sz, int nb,
+                                               int p, uint8_t col) {
+  const int ox = p & 3, oy = p >> 2;
+  for (int by = 0; by < nb; ++by)
+    for (int bx = 0; bx < nb; ++bx) {
+      const int qx = 4 * bx + ox, qy = 4 * by + oy;
+      const int px = rx + qx, py = ry + qy;
+      if (qx < sz && qy < sz && px >= 0 && py >= 0 && px < C && py < C) lds[py * sb + shift + px] = col;
+    }
+}
+
+// Per-env rotation parameters (pygame transform.rotate, 16.16 fixed point;
+// rotate90 for exact multiples of 90 degrees) and the compose placement.
+struct RotSetup {
+  int r90;
+  int nx, ny;                  // rotated surface size
+  int isin, icos;              // 16.16 sin/cos
+  int dx00, dy00;              // source 16.16 coordinates of rotated pixel (0, 0)
+  int a00, ustep, vstep;       // rotate90: LDS byte of rotated pixel (0,0) and its steps
+  int rx0, ry0;                // rotated surface top-left in the output (get_rect(center=anchor))
+};
+
+static_assert(sizeof(RotSetup) == 4 * CBEV_RS_WORDS, "RotSetup must match the record's RS_* ints");
+
+__device__ __forceinline__ RotSetup rot_setup(const cbev_params& P, float angle, int sb) {
+  RotSetup R;
+  const int C = P.crop;
+  R.r90 = fmod((double)angle, (double)90.0f) == 0.0;
+  R.nx = C;
+  R.ny = C;
+  R.isin = R.icos = R.dx00 = R.dy00 = 0;
+  R.a00 = 0;
+  R.ustep = 1;
+  R.vstep = sb;
+  if (R.r90) {
+    int numturns = ((int)angle / 90) % 4;
+    if (numturns < 0) numturns += 4;
+    // rotated pixel (xx, yy) reads LDS byte a00 + xx*ustep + yy*vstep (rotate90 per turn count)
+    switch (numturns) {
+      case 0: R.a00 = 0;                     R.ustep = 1;   R.vstep = sb;  break;
+      case 1: R.a00 = C - 1;                 R.ustep = sb;  R.vstep = -1;  break;
+      case 2: R.a00 = (C - 1) * sb + C - 1;  R.ustep = -1;  R.vstep = -sb; break;
+      default: R.a00 = (C - 1) * sb;         R.ustep = -sb; R.vstep = 1;   break;
+    }
+  } else {
+    double rad = angle * .01745329251994329;
+    double sn = sin(rad), cs = cos(rad);
+    double xw = C, yh = C;
+    double cxw = cs * xw, cyh = cs * yh, sxw = sn * xw, syh = sn * yh;
+    double m1 = fmax(fmax(fmax(fabs(cxw + syh), fabs(cxw - syh)), fabs(-cxw + syh)), fabs(-cxw - syh));
+    double m2 = fmax(fmax(fmax(fabs(sxw + cyh), fabs(sxw - cyh)), fabs(-sxw + cyh)), fabs(-sxw - cyh));
+    R.nx = (int)m1;
+    R.ny = (int)m2;
+    const int icy = R.ny / 2;
+    const int xd = (C - R.nx) * 32768;  // (src->w - dst->w) << 15
+    const int yd = (C - R.ny) * 32768;
+    R.isin = (int)(sn * 65536);
+    R.icos = (int)(cs * 65536);
+    const int axf = (R.nx << 15) - (int)(cs * ((R.nx - 1) << 15));
+    const int ayf = (R.ny << 15) - (int)(sn * ((R.nx - 1) << 15));
+    // rotozoom inner loop: dx = (ax + isin*(cy - y)) + xd + x*icos, dy = (ay - icos*(cy - y)) + yd + x*isin;
+    // every term stays far inside int32, so it is affine in (x, y) and can be stepped exactly
+    R.dx00 = (axf + R.isin * icy) + xd;
+    R.dy00 = (ayf - R.icos * icy) + yd;
+  }
+  R.rx0 = P.anchor_x - R.nx / 2;
+  R.ry0 = P.anchor_y - R.ny / 2;
+  return R;
+}
+
+// XCD-aware env placement. The dispatcher deals workgroups round-robin over
+// the 8 XCDs (workgroup w -> XCD w % 8), and each XCD has its own L2. The
+// thread-per-env kernels (k_hero, k_collide) put env block b = e / 64 on XCD
+// b % 8; the per-env-workgroup kernels (k_raster, k_reset) and k_actors map
+// their workgroups so that env e is handled on that same XCD, keeping each
+// record in one L2 across the step's launches. Exact for n % 512 == 0, the
+// identity on the tail.
+__device__ __forceinline__ int xcd_env_of_wg(int w, int n) {
+  if (w >= (n & ~511)) return w;
+  return ((w >> 3) & 63) + 64 * (w & 7) + 512 * (w >> 9);
+}
+// k_actors: 4 envs per workgroup (one wave each), 16 workgroups per env block
+__device__ __forceinline__ int xcd_env4_of_wg(int w, int wave, int n) {
+  if (4 * w >= (n & ~511)) return 4 * w + wave;
+  return 64 * ((w & 7) + 8 * (w >> 7)) + 4 * ((w >> 3) & 15) + wave;
+}
+
+// The render set-up lives in the record's RS_* ints (written by k_hero, read by k_raster).
+__device__ __forceinline__ void d_store_render_setup(const cbev_params& P, int32_t* hi, double x, double y,
+                                                     float angle) {
+  const RotSetup R = rot_setup(P, angle, 4 * raster_stride_dwords(P.crop));
+  int xm, ym;
+  d_crop_origin(P, x, y, &xm, &ym);
+  hi[CBEV_HI_RS_XMIN] = xm;
+  hi[CBEV_HI_RS_YMIN] = ym;
+  const int32_t* w = (const int32_t*)&R;
+#pragma unroll
+  for (int k = 0; k < CBEV_RS_WORDS; ++k) hi[CBEV_HI_RS_R90 + k] = w[k];
+}
+
 // ============================================================== k_hero / k_actors
 // Ego update: one thread per env, so all 64 lanes of a wave carry the float64
 // scalar chain of 64 envs (BaseAgent.physics_step, hero.py:88-138).
@@ -377,6 +512,9 @@ __global__ __launch_bounds__(64) void k_hero(KArgs K, uint8_t* __restrict__ recs
   hd[CBEV_HD_D2G_T1] = hd[CBEV_HD_D2G];
   const double gx = s[0] - hd[CBEV_HD_GOAL_X], gy = s[1] - hd[CBEV_HD_GOAL_Y];
   hd[CBEV_HD_D2G] = sqrt(gx * gx + gy * gy);
+  // render set-up of this step's observation (crop origin + rotation), once per
+  // env here instead of in every raster wave
+  d_store_render_setup(K.P, r.hi, s[0], s[1], (float)(d_degrees(s[2]) + 90));
 }
 
 // Scripted actors (ActorManager.step_all, actor_manager.py:111-119): one
@@ -384,107 +522,13 @@ __global__ __launch_bounds__(64) void k_hero(KArgs K, uint8_t* __restrict__ recs
 // k_hero, so the scene clock hd[T] is already advanced.
 __global__ __launch_bounds__(256) void k_actors(KArgs K, uint8_t* __restrict__ recs, int n) {
   const int lane = threadIdx.x & 63;
-  const int e = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int e = xcd_env4_of_wg(blockIdx.x, threadIdx.x >> 6, n);
   if (e >= n) return;
   DRec r = bind_rec(recs + (int64_t)e * K.L.record_bytes, K.L, K.C);
   const int nact = r.hi[CBEV_HI_NACT];
   if (nact == 0) return;
   const double t = r.hd[CBEV_HD_T];
   for (int a = lane; a < nact; a += 64) d_actor_step(r, a, t);
-}
-
-// ============================================================== k_raster
-__device__ __forceinline__ void d_crop_origin(const cbev_params& P, double x, double y, int* xm, int* ym) {
-  const double C = (double)P.crop;
-  double offx = trunc(((double)P.pad + x) + (-C / 2));  // Follow.scroll int() (camera.py:39-42)
-  double offy = trunc(((double)P.pad + y) + (-C / 2));
-  int cxc = (int)rint(offx + C / 2.0);  // round() half-even (fov.py:70-79)
-  int cyc = (int)rint(offy + C / 2.0);
-  int xmin = cxc - P.crop / 2, ymin = cyc - P.crop / 2;
-  int maxx = P.render_w - P.crop, maxy = P.render_h - P.crop;
-  maxx = maxx < 0 ? 0 : maxx;
-  maxy = maxy < 0 ? 0 : maxy;
-  *xm = xmin < 0 ? 0 : (xmin > maxx ? maxx : xmin);
-  *ym = ymin < 0 ? 0 : (ymin > maxy ? maxy : ymin);
-}
-
-// rect_from_world_center (transforms.py:46-51): centre rounded half-even, x = c - w/2
-__device__ __forceinline__ int d_rect_lo(double w, int pad, int size) { return (int)rint((double)pad + w * 1.0) - size / 2; }
-
-// LDS image of the crop window: crop row r starts at dword r * sd, holding the
-// padded-map bytes from xa = xmin & ~3 on (so crop column c is byte
-// r*4*sd + shift + c, shift = xmin & 3). sd is odd so that successive crop
-// rows start in different LDS banks: gathers along a rotated output row then
-// spread over the banks for every angle. The image is one contiguous run of
-// C*sd dwords, which lets LDS-DMA fill it lane-linearly.
-__host__ __device__ __forceinline__ int raster_row_dwords(int C) { return (C + 6) / 4; }
-__host__ __device__ __forceinline__ int raster_stride_dwords(int C) { return raster_row_dwords(C) | 1; }
-
-// paint one pixel of a rect (side <= 4) into the LDS crop; thread t handles
-// pixel (t & 15) of rect base + (t >> 4)
-__device__ __forceinline__ void lds_paint_px(uint8_t* lds, int sb, int shift, int C, int rx, int ry, int sz, int p,
-                                             uint8_t col) {
-  if (p >= sz * sz) return;
-  int px = rx + (p % sz), py = ry + (p / sz);
-  if (px < 0 || py < 0 || px >= C || py >= C) return;
-  lds[py * sb + shift + px] = col;
-}
-
-// Per-env rotation parameters (pygame transform.rotate, 16.16 fixed point;
-// rotate90 for exact multiples of 90 degrees) and the compose placement.
-struct RotSetup {
-  bool r90;
-  int nx, ny;                  // rotated surface size
-  int isin, icos;              // 16.16 sin/cos
-  int dx00, dy00;              // source 16.16 coordinates of rotated pixel (0, 0)
-  int a00, ustep, vstep;       // rotate90: LDS byte of rotated pixel (0,0) and its steps
-  int rx0, ry0;                // rotated surface top-left in the output (get_rect(center=anchor))
-};
-
-__device__ __forceinline__ RotSetup rot_setup(const cbev_params& P, float angle, int sb) {
-  RotSetup R;
-  const int C = P.crop;
-  R.r90 = fmod((double)angle, (double)90.0f) == 0.0;
-  R.nx = C;
-  R.ny = C;
-  R.isin = R.icos = R.dx00 = R.dy00 = 0;
-  R.a00 = 0;
-  R.ustep = 1;
-  R.vstep = sb;
-  if (R.r90) {
-    int numturns = ((int)angle / 90) % 4;
-    if (numturns < 0) numturns += 4;
-    // rotated pixel (xx, yy) reads LDS byte a00 + xx*ustep + yy*vstep (rotate90 per turn count)
-    switch (numturns) {
-      case 0: R.a00 = 0;                     R.ustep = 1;   R.vstep = sb;  break;
-      case 1: R.a00 = C - 1;                 R.ustep = sb;  R.vstep = -1;  break;
-      case 2: R.a00 = (C - 1) * sb + C - 1;  R.ustep = -1;  R.vstep = -sb; break;
-      default: R.a00 = (C - 1) * sb;         R.ustep = -sb; R.vstep = 1;   break;
-    }
-  } else {
-    double rad = angle * .01745329251994329;
-    double sn = sin(rad), cs = cos(rad);
-    double xw = C, yh = C;
-    double cxw = cs * xw, cyh = cs * yh, sxw = sn * xw, syh = sn * yh;
-    double m1 = fmax(fmax(fmax(fabs(cxw + syh), fabs(cxw - syh)), fabs(-cxw + syh)), fabs(-cxw - syh));
-    double m2 = fmax(fmax(fmax(fabs(sxw + cyh), fabs(sxw - cyh)), fabs(-sxw + cyh)), fabs(-sxw - cyh));
-    R.nx = (int)m1;
-    R.ny = (int)m2;
-    const int icy = R.ny / 2;
-    const int xd = (C - R.nx) * 32768;  // (src->w - dst->w) << 15
-    const int yd = (C - R.ny) * 32768;
-    R.isin = (int)(sn * 65536);
-    R.icos = (int)(cs * 65536);
-    const int axf = (R.nx << 15) - (int)(cs * ((R.nx - 1) << 15));
-    const int ayf = (R.ny << 15) - (int)(sn * ((R.nx - 1) << 15));
-    // rotozoom inner loop: dx = (ax + isin*(cy - y)) + xd + x*icos, dy = (ay - icos*(cy - y)) + yd + x*isin;
-    // every term stays far inside int32, so it is affine in (x, y) and can be stepped exactly
-    R.dx00 = (axf + R.isin * icy) + xd;
-    R.dy00 = (ayf - R.icos * icy) + yd;
-  }
-  R.rx0 = P.anchor_x - R.nx / 2;
-  R.ry0 = P.anchor_y - R.ny / 2;
-  return R;
 }
 
 // Output pass over one wave's chunks of 1024 output pixels: gather j (0..15) of
@@ -558,7 +602,7 @@ __device__ __forceinline__ void raster_out(const cbev_params& P, const RotSetup&
           v = img[__umul24((uint32_t)dy >> 16, sb) + ((uint32_t)dx >> 16)];
         }
       }
-      px[j] = v;
+      px[j] = (CBEV_RASTER_PHASES & 4) ? v : (uint32_t)(lane + j);
     }
     if (hero_rows) {
 #pragma unroll
@@ -567,9 +611,17 @@ __device__ __forceinline__ void raster_out(const cbev_params& P, const RotSetup&
         if ((unsigned)(r + rj - hy0) < (unsigned)hero_w && ((hcol >> cj) & 1u)) px[j] = CBEV_PX_BLACK;
       }
     }
-    for (int k = 0; k < nout; ++k) {
+    if (CBEV_RASTER_PHASES & 8) {
+      for (int k = 0; k < nout; ++k) {
 #pragma unroll
-      for (int j = 0; j < 16; ++j) o[(int64_t)k * out_stride + (j / G) * S + 64 * (j % G)] = (uint8_t)px[j];
+        for (int j = 0; j < 16; ++j)  // streamed out: keep the L2 for the map and the records
+          __builtin_nontemporal_store((uint8_t)px[j], o + (int64_t)k * out_stride + (j / G) * S + 64 * (j % G));
+      }
+    } else {
+      uint32_t acc = 0;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) acc += px[j];
+      if (acc == 0x7fffffffu) o[0] = 1;  // keeps the gathers live
     }
     sx -= chunk_rows * R.isin;
     sy += chunk_rows * R.icos;
@@ -609,88 +661,105 @@ __device__ __forceinline__ void raster_env(const KArgs& K, const DRec& r, uint8_
                                            int64_t out_stride, uint8_t* __restrict__ lds) {
   const cbev_params& P = K.P;
   const int C = P.crop;
-  const double x = r.hd[CBEV_HD_X], y = r.hd[CBEV_HD_Y], yaw = r.hd[CBEV_HD_YAW];
-  int xmin, ymin;
-  d_crop_origin(P, x, y, &xmin, &ymin);
-  const int xa = xmin & ~3, shift = xmin - xa;
   const int sd = raster_stride_dwords(C), sb = 4 * sd;
+  int xmin, ymin;
+  RotSetup R;
+  if (RESET) {  // BaseMap.reset: theta 0 -> rotate90 by one turn, crop at the bank record's pose
+    d_crop_origin(P, r.hd[CBEV_HD_X], r.hd[CBEV_HD_Y], &xmin, &ymin);
+    R = rot_setup(P, 90.0f, sb);
+  } else {  // written by k_hero for this step
+    xmin = r.hi[CBEV_HI_RS_XMIN];
+    ymin = r.hi[CBEV_HI_RS_YMIN];
+    int32_t* w = (int32_t*)&R;
+#pragma unroll
+    for (int k = 0; k < CBEV_RS_WORDS; ++k) w[k] = r.hi[CBEV_HI_RS_R90 + k];
+  }
+  const int xa = xmin & ~15, shift = xmin - xa;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
 
-  // ---- stage the crop window into LDS by LDS-DMA (global_load_lds_dword): the
-  // image is lane-linear, dword q = row * sd + col; each wave-instruction moves
-  // 64 consecutive dwords, the lane's source address steps with q.
-  {
+  // ---- stage the crop window into LDS: 16-byte global loads (lane-linear over
+  // the window's row chunks, all of a batch in flight), then dword LDS stores
+  if (CBEV_RASTER_PHASES & 1) {
+    constexpr int U = 10;  // chunks in flight per thread (one batch covers size 128)
+    const int nch = raster_row_chunks(C), total = C * nch;
     const uint8_t* gbase = K.map + (int64_t)ymin * P.map_pitch + xa;
-    const int total = C * sd;
-    const int dr = 256 / sd, dc = 256 - dr * sd;
-    const int q0 = wave * 64 + lane;
-    int row = q0 / sd, col = q0 - row * sd;
-    for (int b = wave * 64; b < total; b += 256) {
-      if (b + lane < total)
-        __builtin_amdgcn_global_load_lds((const void*)(gbase + (int64_t)row * P.map_pitch + 4 * col),
-                                         (__attribute__((address_space(3))) void*)(lds + 4 * b), 4, 0, 0);
-      row += dr;
-      col += dc;
-      if (col >= sd) {
-        col -= sd;
-        ++row;
+    const int dr = 256 / nch, dj = 256 - dr * nch;
+    int row = threadIdx.x / nch, j = threadIdx.x - row * nch;
+    uint32_t* l32 = (uint32_t*)lds;
+    for (int q0 = 0; q0 < total; q0 += 256 * U) {
+      uint4 v[U];
+      int r = row, c = j;
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (q0 + 256 * u + (int)threadIdx.x < total) v[u] = *(const uint4*)(gbase + (int64_t)r * P.map_pitch + 16 * c);
+        r += dr;
+        c += dj;
+        if (c >= nch) { c -= nch; ++r; }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (q0 + 256 * u + (int)threadIdx.x < total) {
+          uint32_t* d = l32 + row * sd + 4 * j;
+          d[0] = v[u].x;
+          d[1] = v[u].y;
+          d[2] = v[u].z;
+          d[3] = v[u].w;
+        }
+        row += dr;
+        j += dj;
+        if (j >= nch) { j -= nch; ++row; }
       }
     }
   }
   __syncthreads();
 
   // ---- paint actors / visible targets / traffic lights in draw order
-  if (!RESET) {
+  if (!RESET && (CBEV_RASTER_PHASES & 2)) {
     const int nact = r.hi[CBEV_HI_NACT], nveh = r.hi[CBEV_HI_NVEH];
+    const int nb = (P.hero_w + 3) >> 2;  // 4x4 blocks per rect side: vehicles are hero_w wide (vehicle.py:24)
     for (int pass = 0; pass < 2; ++pass) {  // vehicles, then pedestrians
       const int a0 = pass == 0 ? 0 : nveh, a1 = pass == 0 ? nveh : nact;
-      for (int base = a0; base < a1; base += 16) {
-        int a = base + (threadIdx.x >> 4);
+      for (int base = a0 + 4 * wave; base < a1; base += 16) {
+        const int a = base + (lane >> 4);
         if (a < a1) {
-          int sz = RAI(r, CBEV_AI_SIZE, a);
-          int rx = d_rect_lo(RAD(r, CBEV_AD_X, a), P.pad, sz) - xmin;
-          int ry = d_rect_lo(RAD(r, CBEV_AD_Y, a), P.pad, sz) - ymin;
-          lds_paint_px(lds, sb, shift, C, rx, ry, sz, threadIdx.x & 15,
-                       pass == 0 ? CBEV_PX_VEHICLE : CBEV_PX_PEDESTRIAN);
+          const int sz = RAI(r, CBEV_AI_SIZE, a);
+          const int rx = d_rect_lo(RAD(r, CBEV_AD_X, a), P.pad, sz) - xmin;
+          const int ry = d_rect_lo(RAD(r, CBEV_AD_Y, a), P.pad, sz) - ymin;
+          lds_paint_rect(lds, sb, shift, C, rx, ry, sz, nb, lane & 15,
+                         pass == 0 ? CBEV_PX_VEHICLE : CBEV_PX_PEDESTRIAN);
         }
       }
       if (a1 > a0) __syncthreads();
     }
     const int nt = r.hi[CBEV_HI_NROUTE];
-    for (int base = 0; base < nt; base += 16) {
-      int i = base + (threadIdx.x >> 4);
+    for (int base = 4 * wave; base < nt; base += 16) {
+      const int i = base + (lane >> 4);
       if (i < nt && ((r.vis[i >> 5] >> (i & 31)) & 1u)) {
-        int sz = (i < nt - 1) ? 2 : 4;  // checkpoints 2x2, goal 4x4 (scenes/utils.py:114-122)
-        int rx = d_rect_lo(r.cx[i], P.pad, sz) - xmin;
-        int ry = d_rect_lo(r.cy[i], P.pad, sz) - ymin;
-        lds_paint_px(lds, sb, shift, C, rx, ry, sz, threadIdx.x & 15, CBEV_PX_ROUTE);
+        const int sz = (i < nt - 1) ? 2 : 4;  // checkpoints 2x2, goal 4x4 (scenes/utils.py:114-122)
+        const int rx = d_rect_lo(r.cx[i], P.pad, sz) - xmin;
+        const int ry = d_rect_lo(r.cy[i], P.pad, sz) - ymin;
+        lds_paint_rect(lds, sb, shift, C, rx, ry, sz, 1, lane & 15, CBEV_PX_ROUTE);
       }
     }
     __syncthreads();
     const int ntl = r.hi[CBEV_HI_NTL];
     for (int k = 0; k < ntl; ++k) {  // traffic lights one at a time (colours may differ)
-      int rx = r.ti[CBEV_TI_RX * r.T + k] - xmin, ry = r.ti[CBEV_TI_RY * r.T + k] - ymin;
-      int rw = r.ti[CBEV_TI_RW * r.T + k], rh = r.ti[CBEV_TI_RH * r.T + k];
-      uint8_t col = (uint8_t)r.ti[CBEV_TI_COLOR * r.T + k];
-      for (int p = threadIdx.x; p < rw * rh; p += 256) {
-        int px = rx + p % rw, py = ry + p / rw;
-        if (px >= 0 && py >= 0 && px < C && py < C) lds[py * sb + shift + px] = col;
-      }
+      const int rx = r.ti[CBEV_TI_RX * r.T + k] - xmin, ry = r.ti[CBEV_TI_RY * r.T + k] - ymin;
+      const int rw = r.ti[CBEV_TI_RW * r.T + k], rh = r.ti[CBEV_TI_RH * r.T + k];
+      const uint8_t col = (uint8_t)r.ti[CBEV_TI_COLOR * r.T + k];
+      for (int qy = threadIdx.x >> 4; qy < rh; qy += 16)
+        for (int qx = threadIdx.x & 15; qx < rw; qx += 16) {
+          const int px = rx + qx, py = ry + qy;
+          if (px >= 0 && py >= 0 && px < C && py < C) lds[py * sb + shift + px] = col;
+        }
       __syncthreads();
     }
   }
 
   // ---- rotate (pygame transform.rotate / rotate90) + compose + ego overlay
-  const uint8_t* img = lds + shift;
-  const uint32_t bg = img[0];  // crop top-left pixel after painting
-  const float angle = RESET ? 90.0f : (float)(d_degrees(yaw) + 90);
-  const RotSetup R = rot_setup(P, angle, sb);
-  switch (P.size >> 6) {
-    case 1: raster_out_dispatch<1>(P, R, lds, shift, bg, out, nout, out_stride, lane, wave); break;
-    case 2: raster_out_dispatch<2>(P, R, lds, shift, bg, out, nout, out_stride, lane, wave); break;
-    default: raster_out_dispatch<4>(P, R, lds, shift, bg, out, nout, out_stride, lane, wave); break;
-  }
+  const uint32_t bg = lds[shift];  // crop top-left pixel after painting
+  raster_out_dispatch<G>(P, R, lds, shift, bg, out, nout, out_stride, lane, wave);
 }
 
 // G = size / 64 (64-pixel gathers per output row)
@@ -698,7 +767,7 @@ template <int G>
 __global__ __launch_bounds__(256) void k_raster(KArgs K, uint8_t* __restrict__ recs, int n,
                                                 uint8_t* __restrict__ frames) {
   extern __shared__ __align__(16) uint8_t lds[];
-  const int e = blockIdx.x;
+  const int e = xcd_env_of_wg(blockIdx.x, n);
   if (e >= n) return;
   DRec r = bind_rec(recs + (int64_t)e * K.L.record_bytes, K.L, K.C);
   raster_env<false, G>(K, r, frames + (int64_t)e * K.P.size * K.P.size, 1, 0, lds);
@@ -715,7 +784,7 @@ __global__ __launch_bounds__(256) void k_reset(KArgs K, uint8_t* __restrict__ re
                                                const uint8_t* __restrict__ mask, const int32_t* __restrict__ bank_idx,
                                                int bank_offset, uint8_t* __restrict__ ring, int n_frames) {
   extern __shared__ __align__(16) uint8_t lds[];
-  const int e = blockIdx.x;
+  const int e = xcd_env_of_wg(blockIdx.x, n);
   if (e >= n) return;
   if (mask != nullptr && mask[e] == 0) return;  // uniform per workgroup
   const int64_t rb = K.L.record_bytes;
@@ -1198,7 +1267,7 @@ static const void* raster_kernel(int size) {
 static const void* reset_kernel(int size) {
   return size == 64 ? (const void*)k_reset<1> : size == 128 ? (const void*)k_reset<2> : (const void*)k_reset<4>;
 }
-static size_t raster_lds_bytes(const cbev_params& P) { return (size_t)P.crop * (size_t)raster_stride_dwords(P.crop) * 4; }
+static size_t raster_lds_bytes(const cbev_params& P) { return (size_t)raster_image_bytes(P.crop); }
 
 extern "C" {
 

@@ -61,7 +61,11 @@
   F_(TILE)           /* SemanticClass of hero tile (world.py:159-165) */       \
   F_(COLLIDED)       /* 0 none, 1 vehicle, 2 pedestrian, 3 target */          \
   F_(ACTOR_ID)       /* -1 None, -2 "goal", else int id */                     \
-  F_(EP_LEN) F_(STEP) F_(SCENE_ID) F_(NACTSTATE) F_(PAD0)
+  F_(EP_LEN) F_(STEP) F_(SCENE_ID) F_(NACTSTATE) F_(PAD0)                         \
+  /* render set-up of the current observation (device scratch, k_hero -> k_raster): */ \
+  F_(RS_XMIN) F_(RS_YMIN) /* crop origin in the padded map (fov.py:70-79) */        \
+  F_(RS_R90) F_(RS_NX) F_(RS_NY) F_(RS_ISIN) F_(RS_ICOS) F_(RS_DX00) F_(RS_DY00)      \
+  F_(RS_A00) F_(RS_USTEP) F_(RS_VSTEP) F_(RS_RX0) F_(RS_RY0)
 
 /* ---- actor scalars, float64, field-major [field][actor_cap] ----------- */
 #define CBEV_AD_FIELDS(F_)                                                     \
@@ -85,6 +89,9 @@
   F_(BRAKING) F_(HAS_GOAL)
 
 /* ---- traffic-light ints, field-major [field][tl_cap] ------------------ */
+/* RotSetup words following RS_R90 (transform.rotate parameters, see cbev.hip) */
+#define CBEV_RS_WORDS 12
+
 #define CBEV_TI_FIELDS(F_) F_(RX) F_(RY) F_(RW) F_(RH) F_(COLOR)
 
 #define CBEV_ENUM_HD(n) CBEV_HD_##n,
