@@ -194,7 +194,9 @@ def pack_scene(view: LY.RecordView, spec: SceneSpec, size: int, scene_id: int = 
         raise ValueError(f"{len(actors)} actors exceed actor_cap={A}")
     actor_rng = _generator(spec.actor_rng_state, spec.actor_jitter_seed)
     for a, act in enumerate(actors):
-        init_actor_slot(view, a, act, actor_rng, map_size=size)
+        # actors are always built with map_size=128 (scene_generator.py:71-75,334), so
+        # they stay 4x4 / 2x2 at size 256
+        init_actor_slot(view, a, act, actor_rng)
     hi[LY.HI["NACT"]] = len(actors)
     hi[LY.HI["NVEH"]] = sum(1 for a in actors if a.kind == "vehicle")
     T = view.ti.shape[1]
