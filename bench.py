@@ -157,14 +157,14 @@ def main():
     total_steps = args.warmup + args.steps
     acts = torch.from_numpy(make_actions(P, n, total_steps, cfgd["act_seed"], rank * n)).to(device)
     gather = cfgd.get("gather", False) and world > 1
-    gbuf = [torch.empty_like(env.frames()) for _ in range(world)] if gather and rank == 0 else None
+    from carlabev_env_amd.sharding import gather_frames
 
     env.auto_obs = False
 
     def one_step(t, wire):
         env.step_async_only(acts[t])
-        if gather:
-            dist.gather(env.frames(), gbuf, dst=0)
+        if gather:  # config 4: uint8 class-id frames + reward/term of every rank to rank 0 (RCCL)
+            gather_frames(env.frames(), env.reward, env.term, dst=0)
         env.reset_from_bank(mask=env.term)  # canonical loop: reset(reset_mask=terminated)
         if wire:
             env._obs()
