@@ -411,6 +411,58 @@ __device__ __forceinline__ int xcd_env4_of_wg(int w, int wave, int n) {
   return 64 * ((w & 7) + 8 * (w >> 7)) + 4 * ((w >> 3) & 15) + wave;
 }
 
+// ---- in-kernel phase stamps (timing builds only, -DCBEV_TIMING): thread 0 of
+// each workgroup records s_memtime at phase boundaries; read by cbev_debug_times.
+#ifdef CBEV_TIMING
+__device__ unsigned long long g_stamps[2][4096][4];
+#define CBEV_STAMP(kern, slot) \
+  if (threadIdx.x == 0 && blockIdx.x < 4096) g_stamps[kern][blockIdx.x][slot] = __builtin_amdgcn_s_memtime()
+#else
+#define CBEV_STAMP(kern, slot)
+#endif
+
+// ---- record staging for the thread-per-env kernels. A workgroup owns `ne`
+// envs (a divisor of 64, so a 64-env block stays on one XCD) and copies the
+// first `sbytes` of each record into LDS with LDS-DMA (16-byte lane-linear
+// pieces, all in flight at once), so the float64 scalar chains and the route
+// loops read LDS instead of waiting on HBM; the fields the kernel changes are
+// copied back at the end.
+__device__ __forceinline__ int staged_env0(int w, int ne, int n) {
+  const int n512 = n & ~511;
+  if (w * ne >= n512) return w * ne;
+  const int sub = 64 / ne, j = w >> 3;
+  return 64 * ((w & 7) + 8 * (j / sub)) + ne * (j % sub);
+}
+
+__device__ __forceinline__ void stage_in(uint8_t* lds, const uint8_t* __restrict__ recs, int e0, int ne, int64_t rb,
+                                         int sbytes) {
+  const int nch = sbytes >> 4, total = ne * nch;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int dk = 256 / nch, dc = 256 - dk * nch;
+  int k = threadIdx.x / nch, c = threadIdx.x - k * nch;
+  for (int b = wave * 64; b < total; b += 256) {
+    if (b + lane < total)
+      __builtin_amdgcn_global_load_lds((const void*)(recs + (int64_t)(e0 + k) * rb + 16 * c),
+                                       (__attribute__((address_space(3))) void*)(lds + 16 * b), 16, 0, 0);
+    k += dk;
+    c += dc;
+    if (c >= nch) {
+      c -= nch;
+      ++k;
+    }
+  }
+}
+
+__device__ __forceinline__ void stage_out(const uint8_t* lds, uint8_t* __restrict__ recs, int e0, int ne, int64_t rb,
+                                          int sbytes, int off, int bytes) {
+  const int nr = bytes >> 4;
+  for (int q = threadIdx.x; q < ne * nr; q += 256) {
+    const int k = q / nr, c = q - k * nr;
+    *(uint4*)(recs + (int64_t)(e0 + k) * rb + off + 16 * c) = *(const uint4*)(lds + k * sbytes + off + 16 * c);
+  }
+}
+
 // The render set-up lives in the record's RS_* ints (written by k_hero, read by k_raster).
 __device__ __forceinline__ void d_store_render_setup(const cbev_params& P, int32_t* hi, double x, double y,
                                                      float angle) {
@@ -427,11 +479,7 @@ __device__ __forceinline__ void d_store_render_setup(const cbev_params& P, int32
 // ============================================================== k_hero / k_actors
 // Ego update: one thread per env, so all 64 lanes of a wave carry the float64
 // scalar chain of 64 envs (BaseAgent.physics_step, hero.py:88-138).
-__global__ __launch_bounds__(64) void k_hero(KArgs K, uint8_t* __restrict__ recs, int n,
-                                             const void* __restrict__ actions) {
-  const int e = blockIdx.x * 64 + threadIdx.x;
-  if (e >= n) return;
-  DRec r = bind_rec(recs + (int64_t)e * K.L.record_bytes, K.L, K.C);
+__device__ __forceinline__ void hero_env(const KArgs& K, DRec r, int e, const void* __restrict__ actions) {
   double* hd = r.hd;
   int32_t* hi = r.hi;
 
@@ -515,6 +563,25 @@ __global__ __launch_bounds__(64) void k_hero(KArgs K, uint8_t* __restrict__ recs
   // render set-up of this step's observation (crop origin + rotation), once per
   // env here instead of in every raster wave
   d_store_render_setup(K.P, r.hi, s[0], s[1], (float)(d_degrees(s[2]) + 90));
+}
+
+__global__ __launch_bounds__(256) void k_hero(KArgs K, uint8_t* __restrict__ recs, int n,
+                                              const void* __restrict__ actions, int ne, int sbytes) {
+  extern __shared__ __align__(16) uint8_t lds[];
+  const int e0 = staged_env0(blockIdx.x, ne, n);
+  const int ne_eff = min(ne, n - e0);
+  if (ne_eff <= 0) return;
+  const int64_t rb = K.L.record_bytes;
+  CBEV_STAMP(0, 0);
+  stage_in(lds, recs, e0, ne_eff, rb, sbytes);
+  __syncthreads();
+  CBEV_STAMP(0, 1);
+  if ((int)threadIdx.x < ne_eff)
+    hero_env(K, bind_rec(lds + threadIdx.x * sbytes, K.L, K.C), e0 + threadIdx.x, actions);
+  CBEV_STAMP(0, 2);
+  __syncthreads();
+  stage_out(lds, recs, e0, ne_eff, rb, sbytes, 0, (int)K.L.cx);  // HD + HI
+  CBEV_STAMP(0, 3);
 }
 
 // Scripted actors (ActorManager.step_all, actor_manager.py:111-119): one
@@ -804,6 +871,20 @@ __global__ __launch_bounds__(256) void k_reset(KArgs K, uint8_t* __restrict__ re
 }
 
 // ============================================================== k_collide
+// squared distance from (x, y) to raw-route segment i (carl_reward_fn.py:36-48)
+__device__ __forceinline__ double d_seg_dist2(const DRec& r, int i, double x, double y) {
+  const int abx_i = r.raw_x[i + 1] - r.raw_x[i], aby_i = r.raw_y[i + 1] - r.raw_y[i];
+  const double ax = r.raw_x[i], ay = r.raw_y[i];
+  const double apx = x - ax, apy = y - ay;
+  const double tt = d_clip((apx * abx_i + apy * aby_i) / ((double)(abx_i * abx_i + aby_i * aby_i) + 1e-9), 0, 1);
+  const double ex = x - (ax + tt * abx_i), ey = y - (ay + tt * aby_i);
+  return ex * ex + ey * ey;
+}
+
+// Loop mask for performance experiments: 1 target loop, 2 route-progress loop.
+#ifndef CBEV_COLLIDE_PHASES
+#define CBEV_COLLIDE_PHASES 3
+#endif
 __device__ __forceinline__ double d_lateral_error(double px, double py, const double* wx, const double* wy, int n) {
   double min_error = INFINITY;
   for (int i = 0; i < n - 1; ++i) {
@@ -822,12 +903,9 @@ __device__ __forceinline__ double d_lateral_error(double px, double py, const do
 
 // One thread per env: the per-env work here is a few short serial loops plus
 // a float64 scalar chain, so 64 envs share a wave.
-__global__ __launch_bounds__(64) void k_collide(KArgs K, uint8_t* __restrict__ recs, int n, double* __restrict__ reward_out,
-                                                uint8_t* __restrict__ term_out, uint8_t* __restrict__ trunc_out,
-                                                int32_t* __restrict__ cause_out, float* __restrict__ info_out) {
-  const int e = blockIdx.x * 64 + threadIdx.x;
-  if (e >= n) return;
-  DRec r = bind_rec(recs + (int64_t)e * K.L.record_bytes, K.L, K.C);
+__device__ __forceinline__ void collide_env(const KArgs& K, DRec r, int e, double* __restrict__ reward_out,
+                                            uint8_t* __restrict__ term_out, uint8_t* __restrict__ trunc_out,
+                                            int32_t* __restrict__ cause_out, float* __restrict__ info_out) {
   const cbev_params& P = K.P;
   double* hd = r.hd;
   int32_t* hi = r.hi;
@@ -881,7 +959,7 @@ __global__ __launch_bounds__(64) void k_collide(KArgs K, uint8_t* __restrict__ r
     }
     if (hit) last_hit = a;
   }
-  for (int i = 0; i < nt; ++i) {
+  for (int i = 0; (CBEV_COLLIDE_PHASES & 1) && i < nt; ++i) {
     if (!((r.vis[i >> 5] >> (i & 31)) & 1u)) continue;
     const int sz = (i < nt - 1) ? 2 : 4;
     const int trx = d_rect_lo(r.cx[i], P.pad, sz), try_ = d_rect_lo(r.cy[i], P.pad, sz);
@@ -895,19 +973,13 @@ __global__ __launch_bounds__(64) void k_collide(KArgs K, uint8_t* __restrict__ r
   const int nraw = hi[CBEV_HI_NRAW];
   double bdist = 1e9;
   int bseg = 0;
-  for (int i = 0; i < nraw - 1; ++i) {
-    const int abx_i = r.raw_x[i + 1] - r.raw_x[i], aby_i = r.raw_y[i + 1] - r.raw_y[i];
-    const double ax = r.raw_x[i], ay = r.raw_y[i];
-    const double apx = x - ax, apy = y - ay;
-    const double tt = d_clip((apx * abx_i + apy * aby_i) / ((double)(abx_i * abx_i + aby_i * aby_i) + 1e-9), 0, 1);
-    const double ex = x - (ax + tt * abx_i), ey = y - (ay + tt * aby_i);
-    const double dist = sqrt(ex * ex + ey * ey);
+  for (int i = 0; (CBEV_COLLIDE_PHASES & 2) && i < nraw - 1; ++i) {
+    const double dist = sqrt(d_seg_dist2(r, i, x, y));
     if (dist < bdist) {
       bdist = dist;
       bseg = i;
     }
   }
-
 
   int result = CBEV_COLL_NONE, coll_id = -1;
   if (last_hit >= 0) {
@@ -1104,6 +1176,29 @@ __global__ __launch_bounds__(64) void k_collide(KArgs K, uint8_t* __restrict__ r
   }
 }
 
+__global__ __launch_bounds__(256) void k_collide(KArgs K, uint8_t* __restrict__ recs, int n,
+                                                 double* __restrict__ reward_out, uint8_t* __restrict__ term_out,
+                                                 uint8_t* __restrict__ trunc_out, int32_t* __restrict__ cause_out,
+                                                 float* __restrict__ info_out, int ne, int sbytes) {
+  const int64_t rb = K.L.record_bytes;
+  extern __shared__ __align__(16) uint8_t lds[];
+  const int e0 = staged_env0(blockIdx.x, ne, n);
+  const int ne_eff = min(ne, n - e0);
+  if (ne_eff <= 0) return;
+  CBEV_STAMP(1, 0);
+  stage_in(lds, recs, e0, ne_eff, rb, sbytes);
+  __syncthreads();
+  CBEV_STAMP(1, 1);
+  if ((int)threadIdx.x < ne_eff)
+    collide_env(K, bind_rec(lds + threadIdx.x * sbytes, K.L, K.C), e0 + threadIdx.x, reward_out, term_out, trunc_out,
+                cause_out, info_out);
+  CBEV_STAMP(1, 2);
+  __syncthreads();
+  stage_out(lds, recs, e0, ne_eff, rb, sbytes, 0, (int)K.L.cx);                                // HD + HI
+  stage_out(lds, recs, e0, ne_eff, rb, sbytes, (int)K.L.vis, (4 * K.L.vis_words + 15) & ~15);  // target visibility
+  CBEV_STAMP(1, 3);
+}
+
 // ============================================================== reset / ring / expansion
 // semantic one-hot + frame stack + flatten: out[e][f*C + c][p] (rgb_to_semantic.py:65-142,256-272)
 __global__ __launch_bounds__(256) void k_expand_semantic(const uint8_t* __restrict__ ring, int n, int F, int head, int C,
@@ -1178,7 +1273,18 @@ struct cbev_ctx {
   int prof_on;
   int64_t prof_n;
   hipEvent_t* prof_ev;  // 4 per recorded step
+  int hero_ne, hero_sb;  // staged thread-per-env kernels: envs per workgroup, staged bytes per record
+  int coll_ne, coll_sb;
 };
+
+// envs per workgroup for a staged kernel: the largest divisor of 64 whose
+// records fit the LDS budget
+static int staged_ne(int sbytes) {
+  const int budget = 128 * 1024;
+  int ne = 64;
+  while (ne > 1 && ne * sbytes > budget) ne >>= 1;
+  return ne;
+}
 
 static thread_local std::string g_err;
 
@@ -1316,10 +1422,22 @@ int cbev_create(const cbev_params* params, const cbev_caps* caps, int device, cb
   c->C = *caps;
   c->L = cbev_make_layout(*caps);
   c->device = device;
+  c->hero_sb = (int)c->L.raw_x;  // HD, HI, ego route cx / cy / cyaw
+  c->coll_sb = (int)c->L.acx;    // ... + raw route, visibility, actor AD / AI groups
+  c->hero_ne = staged_ne(c->hero_sb);
+  c->coll_ne = staged_ne(c->coll_sb);
+  if (c->coll_ne * c->coll_sb > 160 * 1024) {
+    free(c);
+    return set_err(CBEV_EINVAL, "record prefix of %d bytes does not fit LDS", c->coll_sb);
+  }
   SgTables T;
   build_sg_tables(&T);
   hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(c_sg), &T, sizeof T);
   if (e == hipSuccess) e = hipMalloc(&c->lut_dev, 64 * sizeof(uint32_t));
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute((const void*)k_hero, hipFuncAttributeMaxDynamicSharedMemorySize, c->hero_ne * c->hero_sb);
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute((const void*)k_collide, hipFuncAttributeMaxDynamicSharedMemorySize, c->coll_ne * c->coll_sb);
   if (e == hipSuccess)
     e = hipFuncSetAttribute(raster_kernel(P.size), hipFuncAttributeMaxDynamicSharedMemorySize, (int)raster_lds_bytes(P));
   if (e == hipSuccess)
@@ -1350,6 +1468,7 @@ int cbev_profile_read(cbev_ctx* c, double* ms3, int64_t* steps) {
   if (steps) *steps = c->prof_n;
   if (!c->prof_ev || c->prof_n == 0) return CBEV_OK;
   HIP_TRY(hipEventSynchronize(c->prof_ev[4 * (c->prof_n - 1) + 3]));
+  // events: 0 before k_hero, 1 after k_actors, 2 after k_raster, 3 after k_collide
   for (int64_t i = 0; i < c->prof_n; ++i) {
     for (int k = 0; k < 3; ++k) {
       float ms = 0.f;
@@ -1400,7 +1519,8 @@ int cbev_step(cbev_ctx* c, void* records, int n, const void* actions, uint8_t* f
   hipEvent_t* ev = nullptr;
   if (c->prof_on && c->prof_n < CBEV_PROF_MAX) ev = c->prof_ev + 4 * c->prof_n++;
   if (ev) HIP_TRY(hipEventRecord(ev[0], s));
-  hipLaunchKernelGGL(k_hero, dim3((n + 63) / 64), dim3(64), 0, s, K, (uint8_t*)records, n, actions);
+  hipLaunchKernelGGL(k_hero, dim3((n + c->hero_ne - 1) / c->hero_ne), dim3(256), (size_t)c->hero_ne * c->hero_sb, s, K,
+                     (uint8_t*)records, n, actions, c->hero_ne, c->hero_sb);
   if (c->C.actor_cap > 0) hipLaunchKernelGGL(k_actors, dim3(wg4), dim3(256), 0, s, K, (uint8_t*)records, n);
   if (ev) HIP_TRY(hipEventRecord(ev[1], s));
   {
@@ -1412,8 +1532,8 @@ int cbev_step(cbev_ctx* c, void* records, int n, const void* actions, uint8_t* f
     }
   }
   if (ev) HIP_TRY(hipEventRecord(ev[2], s));
-  hipLaunchKernelGGL(k_collide, dim3((n + 63) / 64), dim3(64), 0, s, K, (uint8_t*)records, n, reward, term, trunc, cause,
-                     info);
+  hipLaunchKernelGGL(k_collide, dim3((n + c->coll_ne - 1) / c->coll_ne), dim3(256), (size_t)c->coll_ne * c->coll_sb, s,
+                     K, (uint8_t*)records, n, reward, term, trunc, cause, info, c->coll_ne, c->coll_sb);
   if (ev) HIP_TRY(hipEventRecord(ev[3], s));
   HIP_TRY(hipGetLastError());
   return CBEV_OK;
@@ -1465,4 +1585,10 @@ int cbev_expand_obs(cbev_ctx* c, const uint8_t* ring, int n, int n_frames, int h
   return CBEV_OK;
 }
 
+#ifdef CBEV_TIMING
+// timing builds only: copy the phase stamps [2][4096][4] (u64 s_memtime ticks)
+int cbev_debug_times(unsigned long long* out_host) {
+  return hipMemcpyFromSymbol(out_host, HIP_SYMBOL(g_stamps), sizeof(g_stamps)) == hipSuccess ? 0 : -1;
+}
+#endif
 }  // extern "C"

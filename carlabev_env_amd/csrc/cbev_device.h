@@ -158,13 +158,29 @@ __device__ __forceinline__ int d_target_index_serial(double x, double y, double 
                                                      const double* cy, int n, double* err) {
   double fx = x + CB_WHEELBASE * cos(yaw);
   double fy = y + CB_WHEELBASE * sin(yaw);
+  // argmin of hypot (first on ties) in two passes: the squared distance
+  // dx*dx + dy*dy is within a few ulp of hypot^2, so every index whose hypot
+  // can reach the minimum has a squared distance within (1 + 1e-14) of the
+  // smallest one; hypot is evaluated only for those candidates (almost always
+  // exactly one), in index order, with the reference's strict '<'.
+  double m2 = INFINITY;
+  for (int i = 0; i < n; ++i) {
+    const double dx = fx - cx[i], dy = fy - cy[i];
+    const double d2 = dx * dx + dy * dy;
+    m2 = d2 < m2 ? d2 : m2;
+  }
+  const double lim = m2 * (1.0 + 1e-14);
   int best = 0;
   double bd = 0.0;
+  bool first = true;
   for (int i = 0; i < n; ++i) {
-    double d = hypot(fx - cx[i], fy - cy[i]);
-    if (i == 0 || d < bd) {
+    const double dx = fx - cx[i], dy = fy - cy[i];
+    if (!(dx * dx + dy * dy <= lim)) continue;
+    const double d = hypot(dx, dy);
+    if (first || d < bd) {
       bd = d;
       best = i;
+      first = false;
     }
   }
   if (err) {

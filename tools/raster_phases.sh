@@ -9,7 +9,7 @@ CFG=${CFG:-2}
 for ph in ${PHASES:-15 14 11 7 1 13 9}; do
   so=$OUT/libcbev_p$ph.so
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -shared -std=c++17 -ffp-contract=off -fno-fast-math -Iinclude \
-    -DCBEV_RASTER_PHASES=$ph -o $so carlabev_env_amd/csrc/cbev.hip || exit 1
+    -DCBEV_RASTER_PHASES=$ph ${EXTRA_DEFS:-} -o $so carlabev_env_amd/csrc/cbev.hip || exit 1
   CBEV_LIB=$so timeout -k 10 300 python bench.py --config $CFG --steps 100 --warmup 10 --no-cpu-baseline --no-wire \
     > $OUT/p$ph.json 2> $OUT/p$ph.err
   rc=$?
