@@ -31,6 +31,7 @@
 #include <string.h>
 
 #include <string>
+#include <vector>
 
 #include "../../include/cbev.h"
 #include "cbev_device.h"
@@ -308,18 +309,31 @@ __device__ __forceinline__ void d_crop_origin(const cbev_params& P, double x, do
 __device__ __forceinline__ int d_rect_lo(double w, int pad, int size) { return (int)rint((double)pad + w * 1.0) - size / 2; }
 
 // Phase mask for raster performance experiments (tools/raster_phases.sh):
-// 1 stage, 2 paint, 4 gather, 8 store. Products always build with all four.
+// 1 stage, 2 paint, 4 gather, 8 store, 16 read the render set-up, 32 output
+// pass. Products always build with all of them.
 #ifndef CBEV_RASTER_PHASES
-#define CBEV_RASTER_PHASES 15
+#define CBEV_RASTER_PHASES 63
 #endif
 
-// LDS image of the crop window: crop row r starts at dword r * sd, holding the
-// padded-map bytes from xa = xmin & ~15 on (so crop column c is byte
-// r*4*sd + shift + c, shift = xmin & 15), copied as 16-byte chunks. sd is odd
-// so that successive crop rows start in different LDS banks: gathers along a
-// rotated output row then spread over the banks for every angle.
-__host__ __device__ __forceinline__ int raster_row_chunks(int C) { return (C + 30) / 16; }
+// LDS image of the crop window, nibble-packed like the map: crop row r starts
+// at dword r * sd and holds the packed map bytes from xa = (xmin >> 1) & ~15 on,
+// so crop pixel (c, r) is nibble shift + c of the row (shift = xmin - 2 xa, 0..31),
+// i.e. "nibble address" r * 8 sd + shift + c: byte >> 1 of it, high nibble when odd.
+// Rows are copied as 16-byte chunks; sd is odd so that successive crop rows start
+// in different LDS banks and gathers along a rotated row spread over the banks at
+// every angle. 182 x 29 dwords = 21 KB at S=128: 7 workgroups per CU.
+__host__ __device__ __forceinline__ int raster_row_chunks(int C) { return (C + 63) / 32; }
 __host__ __device__ __forceinline__ int raster_stride_dwords(int C) { return (4 * raster_row_chunks(C)) | 1; }
+// nibble-level helpers on the LDS image
+__device__ __forceinline__ uint32_t lds_nib(const uint8_t* lds, uint32_t na) {
+  return (lds[na >> 1] >> ((na & 1u) << 2)) & 15u;
+}
+__device__ __forceinline__ void lds_set_nib(uint8_t* lds, uint32_t na, uint32_t col) {
+  uint32_t* w = (uint32_t*)lds + (na >> 3);
+  const uint32_t sh = (na & 7u) << 2;
+  atomicAnd(w, ~(15u << sh));
+  atomicOr(w, col << sh);
+}
 __host__ __device__ __forceinline__ int raster_image_bytes(int C) { return C * raster_stride_dwords(C) * 4; }
 
 // Paint a square rect of side sz (<= 4 * nb) into the LDS crop: 16 lanes per
@@ -331,7 +345,7 @@ __device__ __forceinline__ void lds_paint_rect(uint8_t* lds, int sb, int shift, 
     for (int bx = 0; bx < nb; ++bx) {
       const int qx = 4 * bx + ox, qy = 4 * by + oy;
       const int px = rx + qx, py = ry + qy;
-      if (qx < sz && qy < sz && px >= 0 && py >= 0 && px < C && py < C) lds[py * sb + shift + px] = col;
+      if (qx < sz && qy < sz && px >= 0 && py >= 0 && px < C && py < C) lds_set_nib(lds, py * 2 * sb + shift + px, col);
     }
 }
 
@@ -342,7 +356,7 @@ struct RotSetup {
   int nx, ny;                  // rotated surface size
   int isin, icos;              // 16.16 sin/cos
   int dx00, dy00;              // source 16.16 coordinates of rotated pixel (0, 0)
-  int a00, ustep, vstep;       // rotate90: LDS byte of rotated pixel (0,0) and its steps
+  int a00, ustep, vstep;       // rotate90: LDS nibble address of rotated pixel (0,0) and its steps
   int rx0, ry0;                // rotated surface top-left in the output (get_rect(center=anchor))
 };
 
@@ -361,7 +375,7 @@ __device__ __forceinline__ RotSetup rot_setup(const cbev_params& P, float angle,
   if (R.r90) {
     int numturns = ((int)angle / 90) % 4;
     if (numturns < 0) numturns += 4;
-    // rotated pixel (xx, yy) reads LDS byte a00 + xx*ustep + yy*vstep (rotate90 per turn count)
+    // rotated pixel (xx, yy) reads LDS nibble a00 + xx*ustep + yy*vstep (rotate90 per turn count)
     switch (numturns) {
       case 0: R.a00 = 0;                     R.ustep = 1;   R.vstep = sb;  break;
       case 1: R.a00 = C - 1;                 R.ustep = sb;  R.vstep = -1;  break;
@@ -414,9 +428,17 @@ __device__ __forceinline__ int xcd_env4_of_wg(int w, int wave, int n) {
 // ---- in-kernel phase stamps (timing builds only, -DCBEV_TIMING): thread 0 of
 // each workgroup records s_memtime at phase boundaries; read by cbev_debug_times.
 #ifdef CBEV_TIMING
-__device__ unsigned long long g_stamps[2][4096][4];
-#define CBEV_STAMP(kern, slot) \
-  if (threadIdx.x == 0 && blockIdx.x < 4096) g_stamps[kern][blockIdx.x][slot] = __builtin_amdgcn_s_memtime()
+__device__ unsigned long long g_stamps[3][4096][4];
+__device__ unsigned long long g_rtstamps[3][4096][4];  // s_memrealtime (constant 100 MHz)
+__device__ unsigned g_xcc[3][4096];                    // XCC (XCD) the workgroup ran on
+#define CBEV_STAMP(kern, slot)                                                  \
+  if (threadIdx.x == 0 && blockIdx.x < 4096) {                                  \
+    g_stamps[kern][blockIdx.x][slot] = __builtin_amdgcn_s_memtime();            \
+    g_rtstamps[kern][blockIdx.x][slot] = __builtin_amdgcn_s_memrealtime();      \
+    unsigned xcc_;                                                              \
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc_));         \
+    g_xcc[kern][blockIdx.x] = xcc_;                                             \
+  }
 #else
 #define CBEV_STAMP(kern, slot)
 #endif
@@ -466,7 +488,7 @@ __device__ __forceinline__ void stage_out(const uint8_t* lds, uint8_t* __restric
 // The render set-up lives in the record's RS_* ints (written by k_hero, read by k_raster).
 __device__ __forceinline__ void d_store_render_setup(const cbev_params& P, int32_t* hi, double x, double y,
                                                      float angle) {
-  const RotSetup R = rot_setup(P, angle, 4 * raster_stride_dwords(P.crop));
+  const RotSetup R = rot_setup(P, angle, 8 * raster_stride_dwords(P.crop));  // nibble row stride
   int xm, ym;
   d_crop_origin(P, x, y, &xm, &ym);
   hi[CBEV_HI_RS_XMIN] = xm;
@@ -633,12 +655,12 @@ __device__ __forceinline__ void raster_out(const cbev_params& P, const RotSetup&
   // lane state at (output column lane, output row r0 of this wave's first chunk)
   int sx = R.dx00 + xx0 * R.icos - yy0 * R.isin;  // 16.16 source x (general)
   int sy = R.dy00 + xx0 * R.isin + yy0 * R.icos;  // 16.16 source y (general)
-  int sa = R.a00 + shift + xx0 * R.ustep + yy0 * R.vstep;  // LDS byte (rotate90)
-  // unchecked general path: the crop byte offset rides in the integer part of sx
-  // (sx stays positive there), so the LDS address is (sy >> 16) * sb + (sx >> 16)
-  const uint8_t* img = (R90 || !CHECK) ? lds : lds + shift;
-  if (!R90 && !CHECK) sx += shift << 16;
-  const uint32_t sb = (uint32_t)R.vstep;
+  int sa = R.a00 + shift + xx0 * R.ustep + yy0 * R.vstep;  // LDS nibble address (rotate90)
+  // the crop's nibble offset rides in the integer part of sx, so the LDS byte is
+  // (sy >> 16) * sb + (sx >> 17) and the nibble (sx >> 16) & 1
+  sx += shift << 16;
+  const uint8_t* img = lds;
+  const uint32_t sb = 4u * (uint32_t)raster_stride_dwords(C);  // LDS bytes per crop row
   const int chunk_rows = 4 * RPC;                 // the 4 waves interleave chunks
   const int nchunks = S / RPC;
   for (int ch = wave, r = r0; ch < nchunks; ch += 4, r += chunk_rows) {
@@ -653,20 +675,23 @@ __device__ __forceinline__ void raster_out(const cbev_params& P, const RotSetup&
         const int a = sa + rj * R.vstep + 64 * cj * R.ustep;
         if (CHECK) {
           const bool ok = ((xok >> cj) & 1u) && (unsigned)(r + rj - R.ry0) < (unsigned)R.ny;
-          v = ok ? (uint32_t)img[ok ? a : 0] : (uint32_t)CBEV_PX_BLACK;
+          v = ok ? lds_nib(img, ok ? a : 0) : (uint32_t)CBEV_PX_BLACK;
         } else {
-          v = img[a];
+          v = lds_nib(img, a);
         }
       } else {
         const int dx = sx + (64 * cj * R.icos - rj * R.isin);
         const int dy = sy + (64 * cj * R.isin + rj * R.icos);
-        if (CHECK) {
+        const uint32_t byte = __umul24((uint32_t)dy >> 16, sb) + ((uint32_t)dx >> 17);
+        const uint32_t nsh = ((uint32_t)dx >> 14) & 4u;
+        if (CHECK) {  // bounds on the unshifted source coordinate
+          const int ux = dx - (shift << 16);
           const bool ok = ((xok >> cj) & 1u) && (unsigned)(r + rj - R.ry0) < (unsigned)R.ny;
-          const bool in = (uint32_t)dx <= vmax && (uint32_t)dy <= vmax;
-          const uint32_t s = img[(in && ok) ? __umul24((uint32_t)dy >> 16, sb) + ((uint32_t)dx >> 16) : 0u];
+          const bool in = (uint32_t)ux <= vmax && (uint32_t)dy <= vmax;
+          const uint32_t s = (img[(in && ok) ? byte : 0u] >> nsh) & 15u;
           v = !ok ? (uint32_t)CBEV_PX_BLACK : (in ? s : bg);
         } else {
-          v = img[__umul24((uint32_t)dy >> 16, sb) + ((uint32_t)dx >> 16)];
+          v = (img[byte] >> nsh) & 15u;
         }
       }
       px[j] = (CBEV_RASTER_PHASES & 4) ? v : (uint32_t)(lane + j);
@@ -723,66 +748,14 @@ __device__ __forceinline__ void raster_out_dispatch(const cbev_params& P, const 
 // Render one env's observation (whole 256-thread workgroup). RESET: BaseMap.reset's
 // frame (theta = 0, no actors drawn, world.py:92-100). The frame is written to
 // `nout` destinations out + k*out_stride (the frame-stack ring on reset).
-template <bool RESET, int G>
-__device__ __forceinline__ void raster_env(const KArgs& K, const DRec& r, uint8_t* __restrict__ out, int nout,
-                                           int64_t out_stride, uint8_t* __restrict__ lds) {
+// Paint actors / visible targets / traffic lights into the LDS crop in the
+// reference's draw order (scene.py:93-95, actor_manager.py:121-132).
+__device__ __forceinline__ void raster_paint(const KArgs& K, const DRec& r, int xmin, int ymin, int shift, int lane,
+                                             int wave, uint8_t* __restrict__ lds) {
   const cbev_params& P = K.P;
   const int C = P.crop;
-  const int sd = raster_stride_dwords(C), sb = 4 * sd;
-  int xmin, ymin;
-  RotSetup R;
-  if (RESET) {  // BaseMap.reset: theta 0 -> rotate90 by one turn, crop at the bank record's pose
-    d_crop_origin(P, r.hd[CBEV_HD_X], r.hd[CBEV_HD_Y], &xmin, &ymin);
-    R = rot_setup(P, 90.0f, sb);
-  } else {  // written by k_hero for this step
-    xmin = r.hi[CBEV_HI_RS_XMIN];
-    ymin = r.hi[CBEV_HI_RS_YMIN];
-    int32_t* w = (int32_t*)&R;
-#pragma unroll
-    for (int k = 0; k < CBEV_RS_WORDS; ++k) w[k] = r.hi[CBEV_HI_RS_R90 + k];
-  }
-  const int xa = xmin & ~15, shift = xmin - xa;
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-
-  // ---- stage the crop window into LDS: 16-byte global loads (lane-linear over
-  // the window's row chunks, all of a batch in flight), then dword LDS stores
-  if (CBEV_RASTER_PHASES & 1) {
-    constexpr int U = 10;  // chunks in flight per thread (one batch covers size 128)
-    const int nch = raster_row_chunks(C), total = C * nch;
-    const uint8_t* gbase = K.map + (int64_t)ymin * P.map_pitch + xa;
-    const int dr = 256 / nch, dj = 256 - dr * nch;
-    int row = threadIdx.x / nch, j = threadIdx.x - row * nch;
-    uint32_t* l32 = (uint32_t*)lds;
-    for (int q0 = 0; q0 < total; q0 += 256 * U) {
-      uint4 v[U];
-      int r = row, c = j;
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        if (q0 + 256 * u + (int)threadIdx.x < total) v[u] = *(const uint4*)(gbase + (int64_t)r * P.map_pitch + 16 * c);
-        r += dr;
-        c += dj;
-        if (c >= nch) { c -= nch; ++r; }
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        if (q0 + 256 * u + (int)threadIdx.x < total) {
-          uint32_t* d = l32 + row * sd + 4 * j;
-          d[0] = v[u].x;
-          d[1] = v[u].y;
-          d[2] = v[u].z;
-          d[3] = v[u].w;
-        }
-        row += dr;
-        j += dj;
-        if (j >= nch) { j -= nch; ++row; }
-      }
-    }
-  }
-  __syncthreads();
-
-  // ---- paint actors / visible targets / traffic lights in draw order
-  if (!RESET && (CBEV_RASTER_PHASES & 2)) {
+  const int sb = 4 * raster_stride_dwords(C);
+  if (CBEV_RASTER_PHASES & 2) {
     const int nact = r.hi[CBEV_HI_NACT], nveh = r.hi[CBEV_HI_NVEH];
     const int nb = (P.hero_w + 3) >> 2;  // 4x4 blocks per rect side: vehicles are hero_w wide (vehicle.py:24)
     for (int pass = 0; pass < 2; ++pass) {  // vehicles, then pedestrians
@@ -818,15 +791,84 @@ __device__ __forceinline__ void raster_env(const KArgs& K, const DRec& r, uint8_
       for (int qy = threadIdx.x >> 4; qy < rh; qy += 16)
         for (int qx = threadIdx.x & 15; qx < rw; qx += 16) {
           const int px = rx + qx, py = ry + qy;
-          if (px >= 0 && py >= 0 && px < C && py < C) lds[py * sb + shift + px] = col;
+          if (px >= 0 && py >= 0 && px < C && py < C) lds_set_nib(lds, py * 2 * sb + shift + px, col);
         }
       __syncthreads();
     }
   }
 
+}
+
+template <bool RESET, int G>
+__device__ __forceinline__ void raster_env(const KArgs& K, const DRec& r, uint8_t* __restrict__ out, int nout,
+                                           int64_t out_stride, uint8_t* __restrict__ lds) {
+  const cbev_params& P = K.P;
+  const int C = P.crop;
+  const int sd = raster_stride_dwords(C), sb = 4 * sd;
+  int xmin, ymin;
+  RotSetup R;
+  if (RESET) {  // BaseMap.reset: theta 0 -> rotate90 by one turn, crop at the bank record's pose
+    d_crop_origin(P, r.hd[CBEV_HD_X], r.hd[CBEV_HD_Y], &xmin, &ymin);
+    R = rot_setup(P, 90.0f, 2 * sb);  // nibble row stride
+  } else if (CBEV_RASTER_PHASES & 16) {  // written by k_hero for this step
+    xmin = r.hi[CBEV_HI_RS_XMIN];
+    ymin = r.hi[CBEV_HI_RS_YMIN];
+    int32_t* w = (int32_t*)&R;
+#pragma unroll
+    for (int k = 0; k < CBEV_RS_WORDS; ++k) w[k] = r.hi[CBEV_HI_RS_R90 + k];
+  } else {  // (phase experiments only) a fixed pose, no record read
+    xmin = ymin = 1000;
+    R = rot_setup(P, 90.0f, 2 * sb);
+  }
+  const int xa = (xmin >> 1) & ~15, shift = xmin - 2 * xa;  // packed byte column, nibble offset
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+
+  // ---- stage the crop window into LDS: 16-byte global loads (lane-linear over
+  // the window's row chunks, all of a batch in flight), then dword LDS stores
+  if (CBEV_RASTER_PHASES & 1) {
+    constexpr int U = 5;  // chunks in flight per thread (one batch covers size 128)
+    const int nch = raster_row_chunks(C), total = C * nch;
+    const uint8_t* gbase = K.map + (int64_t)ymin * K.npitch + xa;
+    const int dr = 256 / nch, dj = 256 - dr * nch;
+    int row = threadIdx.x / nch, j = threadIdx.x - row * nch;
+    uint32_t* l32 = (uint32_t*)lds;
+    for (int q0 = 0; q0 < total; q0 += 256 * U) {
+      uint4 v[U];
+      int r = row, c = j;
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (q0 + 256 * u + (int)threadIdx.x < total) v[u] = *(const uint4*)(gbase + (int64_t)r * K.npitch + 16 * c);
+        r += dr;
+        c += dj;
+        if (c >= nch) { c -= nch; ++r; }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (q0 + 256 * u + (int)threadIdx.x < total) {
+          uint32_t* d = l32 + row * sd + 4 * j;
+          d[0] = v[u].x;
+          d[1] = v[u].y;
+          d[2] = v[u].z;
+          d[3] = v[u].w;
+        }
+        row += dr;
+        j += dj;
+        if (j >= nch) { j -= nch; ++row; }
+      }
+    }
+  }
+  __syncthreads();
+
+  if (!RESET) {
+    CBEV_STAMP(2, 1);
+    raster_paint(K, r, xmin, ymin, shift, lane, wave, lds);
+    CBEV_STAMP(2, 2);
+  }
+
   // ---- rotate (pygame transform.rotate / rotate90) + compose + ego overlay
-  const uint32_t bg = lds[shift];  // crop top-left pixel after painting
-  raster_out_dispatch<G>(P, R, lds, shift, bg, out, nout, out_stride, lane, wave);
+  const uint32_t bg = lds_nib(lds, shift);  // crop top-left pixel after painting
+  if (CBEV_RASTER_PHASES & 32) raster_out_dispatch<G>(P, R, lds, shift, bg, out, nout, out_stride, lane, wave);
 }
 
 // G = size / 64 (64-pixel gathers per output row)
@@ -836,8 +878,10 @@ __global__ __launch_bounds__(256) void k_raster(KArgs K, uint8_t* __restrict__ r
   extern __shared__ __align__(16) uint8_t lds[];
   const int e = xcd_env_of_wg(blockIdx.x, n);
   if (e >= n) return;
+  CBEV_STAMP(2, 0);
   DRec r = bind_rec(recs + (int64_t)e * K.L.record_bytes, K.L, K.C);
   raster_env<false, G>(K, r, frames + (int64_t)e * K.P.size * K.P.size, 1, 0, lds);
+  CBEV_STAMP(2, 3);
 }
 
 // Partial reset (SyncVectorEnv.reset with reset_mask -> CarlaBEV.reset):
@@ -913,7 +957,7 @@ __device__ __forceinline__ void collide_env(const KArgs& K, DRec r, int e, doubl
 
   // ---- ego tile (world.py:159-165)
   int tx = (int)d_clip(rint(x), 0, P.map_w - 1), ty = (int)d_clip(rint(y), 0, P.map_h - 1);
-  const int tile = K.map[(int64_t)(ty + P.pad) * P.map_pitch + tx + P.pad];
+  const int tile = d_map_texel(K, tx + P.pad, ty + P.pad);
 
   // ---- collisions (scene.py:110-140): hero rect vs vehicles, pedestrians, visible targets
   const int hw = P.hero_w;
@@ -1273,6 +1317,7 @@ struct cbev_ctx {
   int prof_on;
   int64_t prof_n;
   hipEvent_t* prof_ev;  // 4 per recorded step
+  int npitch;            // nibble-packed map pitch (bytes)
   int hero_ne, hero_sb;  // staged thread-per-env kernels: envs per workgroup, staged bytes per record
   int coll_ne, coll_sb;
 };
@@ -1364,6 +1409,7 @@ static KArgs kargs(const cbev_ctx* c) {
   K.C = c->C;
   K.L = c->L;
   K.map = c->map_dev;
+  K.npitch = c->npitch;
   return K;
 }
 
@@ -1495,15 +1541,25 @@ int cbev_set_map(cbev_ctx* c, const uint8_t* map_host, int64_t bytes) {
   if (!c || !map_host) return set_err(CBEV_EINVAL, "null argument");
   const int64_t need = (int64_t)c->P.map_pitch * c->P.render_h;
   if (bytes != need) return set_err(CBEV_EINVAL, "map bytes %lld != pitch*render_h %lld", (long long)bytes, (long long)need);
+  const int W = c->P.render_w, H = c->P.render_h, pitch = c->P.map_pitch;
+  for (int64_t i = 0; i < need; ++i)
+    if (map_host[i] > 15) return set_err(CBEV_EINVAL, "class id %d > 15 at byte %lld", map_host[i], (long long)i);
+  // nibble-pack on the host: 2 texels per byte, rows padded to 64 bytes
+  const int np = ((W + 1) / 2 + 63) & ~63;
+  std::vector<uint8_t> packed((size_t)np * H, 0);
+  for (int y = 0; y < H; ++y)
+    for (int x = 0; x < W; ++x) packed[(size_t)y * np + (x >> 1)] |= (uint8_t)(map_host[(size_t)y * pitch + x] << ((x & 1) * 4));
   HIP_TRY(hipSetDevice(c->device));
   if (c->map_dev) HIP_TRY(hipFree(c->map_dev));
   c->map_dev = nullptr;
-  // slack after the last row: the 16-B staging loads of the last crop row may run
-  // up to 30 bytes past render_w
-  HIP_TRY(hipMalloc(&c->map_dev, need + 4096));
-  HIP_TRY(hipMemset(c->map_dev, 0, need + 4096));
-  HIP_TRY(hipMemcpy(c->map_dev, map_host, need, hipMemcpyHostToDevice));
-  c->map_bytes = need;
+  // slack after the last row: the 16-B staging loads of the last crop row run
+  // up to ~32 bytes past the row's last texel
+  const int64_t nbytes = (int64_t)np * H;
+  HIP_TRY(hipMalloc(&c->map_dev, nbytes + 4096));
+  HIP_TRY(hipMemset(c->map_dev, 0, nbytes + 4096));
+  HIP_TRY(hipMemcpy(c->map_dev, packed.data(), nbytes, hipMemcpyHostToDevice));
+  c->map_bytes = nbytes;
+  c->npitch = np;
   return CBEV_OK;
 }
 
@@ -1586,9 +1642,14 @@ int cbev_expand_obs(cbev_ctx* c, const uint8_t* ring, int n, int n_frames, int h
 }
 
 #ifdef CBEV_TIMING
-// timing builds only: copy the phase stamps [2][4096][4] (u64 s_memtime ticks)
+// timing builds only: copy the phase stamps [3][4096][4] (u64 s_memtime ticks)
 int cbev_debug_times(unsigned long long* out_host) {
-  return hipMemcpyFromSymbol(out_host, HIP_SYMBOL(g_stamps), sizeof(g_stamps)) == hipSuccess ? 0 : -1;
+  if (hipMemcpyFromSymbol(out_host, HIP_SYMBOL(g_stamps), sizeof(g_stamps)) != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(out_host + 3 * 4096 * 4, HIP_SYMBOL(g_rtstamps), sizeof(g_rtstamps)) != hipSuccess) return -1;
+  unsigned x[3 * 4096];
+  if (hipMemcpyFromSymbol(x, HIP_SYMBOL(g_xcc), sizeof(x)) != hipSuccess) return -1;
+  for (int i = 0; i < 3 * 4096; ++i) out_host[6 * 4096 * 4 + i] = x[i];
+  return 0;
 }
 #endif
 }  // extern "C"

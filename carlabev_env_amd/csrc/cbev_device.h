@@ -22,8 +22,15 @@ struct KArgs {
   cbev_params P;
   cbev_caps C;
   cbev_layout L;
-  const uint8_t* map;  // padded class map, render_h rows x map_pitch bytes
+  const uint8_t* map;  // padded class map, nibble-packed: render_h rows x npitch bytes,
+                       // texel x of a row in byte x >> 1, high nibble when x is odd
+  int npitch;
 };
+
+// class id of padded-map texel (x, y)
+__device__ __forceinline__ int d_map_texel(const KArgs& K, int x, int y) {
+  return (K.map[(int64_t)y * K.npitch + (x >> 1)] >> ((x & 1) << 2)) & 15;
+}
 
 // Savitzky-Golay hat-matrix rows for window w = 3,5,..,11 (index w/2),
 // polyorder min(3, w-1): interior centre weights and the rows that evaluate

@@ -41,13 +41,27 @@ L.cbev_debug_times.argtypes = [ctypes.c_void_p]
 for t in range(a.steps):
     env.step_async_only(acts[t])
 torch.cuda.synchronize()
-buf = np.zeros((2, 4096, 4), np.uint64)
+buf = np.zeros(2 * 3 * 4096 * 4 + 3 * 4096, np.uint64)
 assert L.cbev_debug_times(buf.ctypes.data_as(ctypes.c_void_p)) == 0
-for k, name in enumerate(("k_hero", "k_collide")):
-    st = buf[k].astype(np.int64)
+xcc = buf[2 * 3 * 4096 * 4:].reshape(3, 4096).astype(np.int64)
+buf = buf[:2 * 3 * 4096 * 4].reshape(2, 3, 4096, 4)
+for k, name in enumerate(("k_hero", "k_collide", "k_raster")):
+    st = buf[0, k].astype(np.int64)
+    rt = buf[1, k].astype(np.int64)
     used = st[:, 0] > 0
-    st = st[used]
+    st, rt = st[used], rt[used]
+    print(f"{name}: realtime (100 MHz) launch span {(rt[:, 3].max() - rt[:, 0].min()) / 100:.2f} us, "
+          f"WG mean {(rt[:, 3] - rt[:, 0]).mean() / 100:.2f} us, first start->last start "
+          f"{(rt[:, 0].max() - rt[:, 0].min()) / 100:.2f} us; clock {((st[:, 3] - st[:, 0]).sum() / max((rt[:, 3] - rt[:, 0]).sum(), 1)) / 100:.2f} GHz")
     d = np.diff(st, axis=1)
-    print(f"{name}: {used.sum()} WGs; cycles mean stage_in {d[:, 0].mean():.0f}  compute {d[:, 1].mean():.0f} "
-          f"(max {d[:, 1].max():.0f})  write_back {d[:, 2].mean():.0f}; WG total mean {(st[:, 3] - st[:, 0]).mean():.0f}; "
-          f"launch span {st[:, 3].max() - st[:, 0].min()} cycles; start spread {st[:, 0].max() - st[:, 0].min()}")
+    print(f"{name}: {used.sum()} WGs; cycles mean phase1 {d[:, 0].mean():.0f}  phase2 {d[:, 1].mean():.0f} "
+          f"(max {d[:, 1].max():.0f})  phase3 {d[:, 2].mean():.0f}; WG total mean {(st[:, 3] - st[:, 0]).mean():.0f}; "
+          )
+    idx = np.flatnonzero(used)
+    xs = xcc[k][used] & 0xF
+    print(f"   XCC id: workgroups with xcc == w % 8: {(xs == (idx % 8)).mean() * 100:.1f}%; first 16: {list(xs[:16])}")
+    for x in range(8):  # s_memtime is per XCD: spans within one XCD (workgroup w runs on XCD w % 8)
+        m = (idx % 8) == x
+        if m.any():
+            sx = st[m]
+            print(f"   xcd {x}: WGs {m.sum()} span {sx[:, 3].max() - sx[:, 0].min()} start-spread {sx[:, 0].max() - sx[:, 0].min()}")
