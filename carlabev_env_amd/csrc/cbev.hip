@@ -501,7 +501,8 @@ __device__ __forceinline__ void d_store_render_setup(const cbev_params& P, int32
 // ============================================================== k_hero / k_actors
 // Ego update: one thread per env, so all 64 lanes of a wave carry the float64
 // scalar chain of 64 envs (BaseAgent.physics_step, hero.py:88-138).
-__device__ __forceinline__ void hero_env(const KArgs& K, DRec r, int e, const void* __restrict__ actions) {
+__device__ __forceinline__ void hero_env(const KArgs& K, DRec r, int e, const void* __restrict__ actions,
+                                         const double* __restrict__ route_dist) {
   double* hd = r.hd;
   int32_t* hi = r.hi;
 
@@ -527,8 +528,20 @@ __device__ __forceinline__ void hero_env(const KArgs& K, DRec r, int e, const vo
   double s[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) s[k] = hd[CBEV_HD_X + k];
-  // stanley_control's target search; its steering output is unused by the hero
-  const int bi = d_target_index_serial(s[0], s[1], s[2], r.cx, r.cy, hi[CBEV_HI_NROUTE], nullptr);
+  // stanley_control's target search (first arg-min of the precomputed hypots);
+  // its steering output is unused by the hero
+  int bi = 0;
+  {
+    const int nr = hi[CBEV_HI_NROUTE];
+    double bd = 0.0;
+    for (int i = 0; i < nr; ++i) {
+      const double d = route_dist[i];
+      if (i == 0 || d < bd) {
+        bd = d;
+        bi = i;
+      }
+    }
+  }
   hi[CBEV_HI_TIDX] = hi[CBEV_HI_TIDX] >= bi ? hi[CBEV_HI_TIDX] : bi;
   const double v = s[3];
   const int scale = K.P.scale;
@@ -594,12 +607,29 @@ __global__ __launch_bounds__(256) void k_hero(KArgs K, uint8_t* __restrict__ rec
   const int ne_eff = min(ne, n - e0);
   if (ne_eff <= 0) return;
   const int64_t rb = K.L.record_bytes;
+  const int R = K.C.route_cap, tid = threadIdx.x;
+  double* fxy = (double*)(lds + ne * sbytes);  // [ne][2] front-axle position
+  double* dist = fxy + 2 * ne;                 // [ne][R] hypot(front axle - route point)
   CBEV_STAMP(0, 0);
   stage_in(lds, recs, e0, ne_eff, rb, sbytes);
   __syncthreads();
   CBEV_STAMP(0, 1);
-  if ((int)threadIdx.x < ne_eff)
-    hero_env(K, bind_rec(lds + threadIdx.x * sbytes, K.L, K.C), e0 + threadIdx.x, actions);
+  if (tid < ne_eff) {  // Controller.calc_target_index's front axle (stanley_controller.py:51-62), pre-update state
+    const double* hd = (const double*)(lds + tid * sbytes + K.L.hd);
+    fxy[2 * tid] = hd[CBEV_HD_X] + CB_WHEELBASE * cos(hd[CBEV_HD_YAW]);
+    fxy[2 * tid + 1] = hd[CBEV_HD_Y] + CB_WHEELBASE * sin(hd[CBEV_HD_YAW]);
+  }
+  __syncthreads();
+  for (int q = tid; q < ne_eff * R; q += 256) {  // the hypot of every route point, over all threads
+    const int k = q / R, i = q - k * R;
+    const uint8_t* base = lds + k * sbytes;
+    if (i < ((const int32_t*)(base + K.L.hi))[CBEV_HI_NROUTE])
+      dist[k * R + i] = hypot(fxy[2 * k] - ((const double*)(base + K.L.cx))[i],
+                              fxy[2 * k + 1] - ((const double*)(base + K.L.cy))[i]);
+  }
+  __syncthreads();
+  if (tid < ne_eff)
+    hero_env(K, bind_rec(lds + tid * sbytes, K.L, K.C), e0 + tid, actions, dist + tid * R);
   CBEV_STAMP(0, 2);
   __syncthreads();
   stage_out(lds, recs, e0, ne_eff, rb, sbytes, 0, (int)K.L.cx);  // HD + HI
@@ -945,11 +975,38 @@ __device__ __forceinline__ double d_lateral_error(double px, double py, const do
   return min_error;
 }
 
-// One thread per env: the per-env work here is a few short serial loops plus
-// a float64 scalar chain, so 64 envs share a wave.
-__device__ __forceinline__ void collide_env(const KArgs& K, DRec r, int e, double* __restrict__ reward_out,
-                                            uint8_t* __restrict__ term_out, uint8_t* __restrict__ trunc_out,
-                                            int32_t* __restrict__ cause_out, float* __restrict__ info_out) {
+// Per-env scratch of k_collide's cooperative pre-pass (LDS, after the staged
+// records): the element loops (raw-route segments, targets, actors) run over all
+// 256 threads of the workgroup as (env, element) pairs; the per-env thread then
+// only reduces in the reference's order.
+struct CollScratchLayout {
+  int segd, ttcc, ttcs, ints, hitw, bytes;  // byte offsets within one env's scratch
+};
+__host__ __device__ __forceinline__ CollScratchLayout coll_scratch_layout(const cbev_caps& C, int vis_words) {
+  CollScratchLayout o;
+  o.segd = 0;                                   // double[R]: sqrt(e2) per raw segment
+  o.ttcc = o.segd + 8 * C.route_cap;            // double[A]: compute_ttc_raw per actor (INF if none)
+  o.ttcs = o.ttcc + 8 * C.actor_cap;            // double[A]: compute_ttc per actor
+  o.ints = o.ttcs + 8 * C.actor_cap;            // int[8]: tgt_last, act_last, nas, hrx, hry, pad...
+  o.hitw = o.ints + 32;                         // uint32[vis_words]: visible targets hit
+  o.bytes = (o.hitw + 4 * vis_words + 15) & ~15;
+  return o;
+}
+enum { CS_TGT_LAST = 0, CS_ACT_LAST = 1, CS_NAS = 2 };
+struct CollPre {  // one env's pre-pass results, as seen by collide_env
+  const double* segd;
+  const double* ttcc;
+  const double* ttcs;
+  const int* ints;
+  const uint32_t* hitw;
+};
+
+// One thread per env for the float64 scalar chain; the element loops come
+// precomputed in `pre`.
+__device__ __forceinline__ void collide_env(const KArgs& K, DRec r, int e, const CollPre& pre,
+                                            double* __restrict__ reward_out, uint8_t* __restrict__ term_out,
+                                            uint8_t* __restrict__ trunc_out, int32_t* __restrict__ cause_out,
+                                            float* __restrict__ info_out) {
   const cbev_params& P = K.P;
   double* hd = r.hd;
   int32_t* hi = r.hi;
@@ -959,66 +1016,27 @@ __device__ __forceinline__ void collide_env(const KArgs& K, DRec r, int e, doubl
   int tx = (int)d_clip(rint(x), 0, P.map_w - 1), ty = (int)d_clip(rint(y), 0, P.map_h - 1);
   const int tile = d_map_texel(K, tx + P.pad, ty + P.pad);
 
-  // ---- collisions (scene.py:110-140): hero rect vs vehicles, pedestrians, visible targets
-  const int hw = P.hero_w;
-  const int hrx = d_rect_lo(x, P.pad, hw), hry = d_rect_lo(y, P.pad, hw);
+  // ---- collisions (scene.py:110-140): hero rect vs vehicles, pedestrians, visible
+  // targets; the last hit in iteration order (vehicles, pedestrians, then targets)
+  // wins; every visible target hit is consumed (rect tests in k_collide's pre-pass)
   const int nact = hi[CBEV_HI_NACT];
   const int nt = hi[CBEV_HI_NROUTE];
-  int last_hit = -1, nas = 0;
+  const int tgt_last = pre.ints[CS_TGT_LAST], act_last = pre.ints[CS_ACT_LAST];
+  const int last_hit = tgt_last >= 0 ? nact + tgt_last : act_last;
+  const int nas = pre.ints[CS_NAS];
+  for (int w = 0; w < K.L.vis_words; ++w) r.vis[w] &= ~pre.hitw[w];
   double ttc_carl = INFINITY, ttc_sh = INFINITY;
-  const double hx_m = x * CB_MPP, hy_m = y * CB_MPP, hv_m = v * CB_MPP;
-  const double hvx_m = hv_m * cos(yaw), hvy_m = hv_m * sin(yaw);
-  const double hvx = v * cos(yaw), hvy = v * sin(yaw);
   for (int a = 0; a < nact; ++a) {
-    const int sz = RAI(r, CBEV_AI_SIZE, a);
-    const double ax = RAD(r, CBEV_AD_X, a), ay = RAD(r, CBEV_AD_Y, a);
-    const int arx = d_rect_lo(ax, P.pad, sz), ary = d_rect_lo(ay, P.pad, sz);
-    const bool hit = hw > 0 && sz > 0 && hrx < arx + sz && hry < ary + sz && hrx + hw > arx && hry + hw > ary;
-    const int ddx = (hrx + hw / 2) - (arx + sz / 2), ddy = (hry + hw / 2) - (ary + sz / 2);
-    const double dist = hypot((double)ddx, (double)ddy);
-    if (fabs(dist) < P.collide_min_dist) {  // actors_state entry
-      ++nas;
-      const double av = RAD(r, CBEV_AD_V, a), ayaw = RAD(r, CBEV_AD_YAW, a);
-      const double avx = av * cos(ayaw), avy = av * sin(ayaw);
-      {  // compute_ttc_raw (reward_signals.py:46-94)
-        double rx_ = ax * CB_MPP - hx_m, ry_ = ay * CB_MPP - hy_m;
-        double rvx = avx * CB_MPP - hvx_m, rvy = avy * CB_MPP - hvy_m;
-        double nrm = sqrt(rx_ * rx_ + ry_ * ry_);
-        double rel = (rvx * rx_ + rvy * ry_) / (nrm + 1e-6);
-        if (!(rel >= 0)) {
-          double ttc = fabs(nrm / rel);
-          ttc_carl = ttc < ttc_carl ? ttc : ttc_carl;
-        }
-      }
-      {  // compute_ttc (reward_signals.py:15-42)
-        double rx_ = ax - x, ry_ = ay - y;
-        double rvx = avx - hvx, rvy = avy - hvy;
-        double nrm = sqrt(rx_ * rx_ + ry_ * ry_);
-        double rel = (rvx * rx_ + rvy * ry_) / (nrm + 1e-6);
-        if (!(rel >= 0)) {
-          double ttc = fabs(nrm / rel);
-          ttc_sh = ttc < ttc_sh ? ttc : ttc_sh;
-        }
-      }
-    }
-    if (hit) last_hit = a;
-  }
-  for (int i = 0; (CBEV_COLLIDE_PHASES & 1) && i < nt; ++i) {
-    if (!((r.vis[i >> 5] >> (i & 31)) & 1u)) continue;
-    const int sz = (i < nt - 1) ? 2 : 4;
-    const int trx = d_rect_lo(r.cx[i], P.pad, sz), try_ = d_rect_lo(r.cy[i], P.pad, sz);
-    if (hrx < trx + sz && hry < try_ + sz && hrx + hw > trx && hry + hw > try_) {
-      r.vis[i >> 5] &= ~(1u << (i & 31));  // every visible target hit is consumed
-      last_hit = nact + i;  // the last hit in iteration order wins
-    }
+    ttc_carl = pre.ttcc[a] < ttc_carl ? pre.ttcc[a] : ttc_carl;
+    ttc_sh = pre.ttcs[a] < ttc_sh ? pre.ttcs[a] : ttc_sh;
   }
 
-  // ---- CaRL route progress: arg-min over raw-route segments (carl_reward_fn.py:29-58)
+  // ---- CaRL route progress: first strict arg-min over raw-route segments (carl_reward_fn.py:29-58)
   const int nraw = hi[CBEV_HI_NRAW];
   double bdist = 1e9;
   int bseg = 0;
   for (int i = 0; (CBEV_COLLIDE_PHASES & 2) && i < nraw - 1; ++i) {
-    const double dist = sqrt(d_seg_dist2(r, i, x, y));
+    const double dist = pre.segd[i];
     if (dist < bdist) {
       bdist = dist;
       bseg = i;
@@ -1229,13 +1247,104 @@ __global__ __launch_bounds__(256) void k_collide(KArgs K, uint8_t* __restrict__ 
   const int e0 = staged_env0(blockIdx.x, ne, n);
   const int ne_eff = min(ne, n - e0);
   if (ne_eff <= 0) return;
+  const cbev_params& P = K.P;
+  const CollScratchLayout SL = coll_scratch_layout(K.C, K.L.vis_words);
+  uint8_t* scr = lds + ne * sbytes;
+  const int tid = threadIdx.x;
   CBEV_STAMP(1, 0);
   stage_in(lds, recs, e0, ne_eff, rb, sbytes);
   __syncthreads();
   CBEV_STAMP(1, 1);
-  if ((int)threadIdx.x < ne_eff)
-    collide_env(K, bind_rec(lds + threadIdx.x * sbytes, K.L, K.C), e0 + threadIdx.x, reward_out, term_out, trunc_out,
-                cause_out, info_out);
+  const int hw = P.hero_w;
+  // per-env prologue: hero rect, counters
+  if (tid < ne_eff) {
+    const double* hd = (const double*)(lds + tid * sbytes + K.L.hd);
+    int* I = (int*)(scr + tid * SL.bytes + SL.ints);
+    I[CS_TGT_LAST] = -1;
+    I[CS_ACT_LAST] = -1;
+    I[CS_NAS] = 0;
+    I[3] = d_rect_lo(hd[CBEV_HD_X], P.pad, hw);
+    I[4] = d_rect_lo(hd[CBEV_HD_Y], P.pad, hw);
+    uint32_t* hitw = (uint32_t*)(scr + tid * SL.bytes + SL.hitw);
+    for (int w = 0; w < K.L.vis_words; ++w) hitw[w] = 0;
+  }
+  __syncthreads();
+  // ---- cooperative pre-pass over (env, element) pairs
+  {
+    const int R = K.C.route_cap, A = K.C.actor_cap;
+    // raw-route segments (carl_reward_fn.py:36-48)
+    for (int q = tid; q < ne_eff * (R - 1); q += 256) {
+      const int k = q / (R - 1), i = q - k * (R - 1);
+      DRec r = bind_rec(lds + k * sbytes, K.L, K.C);
+      if (i < r.hi[CBEV_HI_NRAW] - 1)
+        ((double*)(scr + k * SL.bytes + SL.segd))[i] = sqrt(d_seg_dist2(r, i, r.hd[CBEV_HD_X], r.hd[CBEV_HD_Y]));
+    }
+    // visible targets vs the hero rect (target.py:37-44)
+    for (int q = tid; q < ne_eff * R; q += 256) {
+      const int k = q / R, i = q - k * R;
+      DRec r = bind_rec(lds + k * sbytes, K.L, K.C);
+      const int nt = r.hi[CBEV_HI_NROUTE];
+      if (i >= nt || !((r.vis[i >> 5] >> (i & 31)) & 1u)) continue;
+      int* I = (int*)(scr + k * SL.bytes + SL.ints);
+      const int hrx = I[3], hry = I[4];
+      const int sz = (i < nt - 1) ? 2 : 4;
+      const int trx = d_rect_lo(r.cx[i], P.pad, sz), try_ = d_rect_lo(r.cy[i], P.pad, sz);
+      if (hrx < trx + sz && hry < try_ + sz && hrx + hw > trx && hry + hw > try_) {
+        atomicOr((uint32_t*)(scr + k * SL.bytes + SL.hitw) + (i >> 5), 1u << (i & 31));
+        atomicMax(&I[CS_TGT_LAST], i);
+      }
+    }
+    // vehicles / pedestrians: rect hit, actors_state entry and both TTCs (scene.py:110-140,
+    // reward_signals.py:15-94)
+    for (int q = tid; q < ne_eff * A; q += 256) {
+      const int k = q / A, a = q - k * A;
+      DRec r = bind_rec(lds + k * sbytes, K.L, K.C);
+      if (a >= r.hi[CBEV_HI_NACT]) continue;
+      int* I = (int*)(scr + k * SL.bytes + SL.ints);
+      const int hrx = I[3], hry = I[4];
+      const double x = r.hd[CBEV_HD_X], y = r.hd[CBEV_HD_Y], yaw = r.hd[CBEV_HD_YAW], v = r.hd[CBEV_HD_V];
+      const int sz = RAI(r, CBEV_AI_SIZE, a);
+      const double ax = RAD(r, CBEV_AD_X, a), ay = RAD(r, CBEV_AD_Y, a);
+      const int arx = d_rect_lo(ax, P.pad, sz), ary = d_rect_lo(ay, P.pad, sz);
+      if (hw > 0 && sz > 0 && hrx < arx + sz && hry < ary + sz && hrx + hw > arx && hry + hw > ary)
+        atomicMax(&I[CS_ACT_LAST], a);
+      const int ddx = (hrx + hw / 2) - (arx + sz / 2), ddy = (hry + hw / 2) - (ary + sz / 2);
+      const double dist = hypot((double)ddx, (double)ddy);
+      double tc = INFINITY, ts = INFINITY;
+      if (fabs(dist) < P.collide_min_dist) {  // actors_state entry
+        atomicAdd(&I[CS_NAS], 1);
+        const double hx_m = x * CB_MPP, hy_m = y * CB_MPP, hv_m = v * CB_MPP;
+        const double hvx_m = hv_m * cos(yaw), hvy_m = hv_m * sin(yaw);
+        const double hvx = v * cos(yaw), hvy = v * sin(yaw);
+        const double av = RAD(r, CBEV_AD_V, a), ayaw = RAD(r, CBEV_AD_YAW, a);
+        const double avx = av * cos(ayaw), avy = av * sin(ayaw);
+        {  // compute_ttc_raw (reward_signals.py:46-94)
+          double rx_ = ax * CB_MPP - hx_m, ry_ = ay * CB_MPP - hy_m;
+          double rvx = avx * CB_MPP - hvx_m, rvy = avy * CB_MPP - hvy_m;
+          double nrm = sqrt(rx_ * rx_ + ry_ * ry_);
+          double rel = (rvx * rx_ + rvy * ry_) / (nrm + 1e-6);
+          if (!(rel >= 0)) tc = fabs(nrm / rel);
+        }
+        {  // compute_ttc (reward_signals.py:15-42)
+          double rx_ = ax - x, ry_ = ay - y;
+          double rvx = avx - hvx, rvy = avy - hvy;
+          double nrm = sqrt(rx_ * rx_ + ry_ * ry_);
+          double rel = (rvx * rx_ + rvy * ry_) / (nrm + 1e-6);
+          if (!(rel >= 0)) ts = fabs(nrm / rel);
+        }
+      }
+      ((double*)(scr + k * SL.bytes + SL.ttcc))[a] = tc;
+      ((double*)(scr + k * SL.bytes + SL.ttcs))[a] = ts;
+    }
+  }
+  __syncthreads();
+  if (tid < ne_eff) {
+    const uint8_t* sk = scr + tid * SL.bytes;
+    const CollPre pre{(const double*)(sk + SL.segd), (const double*)(sk + SL.ttcc), (const double*)(sk + SL.ttcs),
+                      (const int*)(sk + SL.ints), (const uint32_t*)(sk + SL.hitw)};
+    collide_env(K, bind_rec(lds + tid * sbytes, K.L, K.C), e0 + tid, pre, reward_out, term_out, trunc_out, cause_out,
+                info_out);
+  }
   CBEV_STAMP(1, 2);
   __syncthreads();
   stage_out(lds, recs, e0, ne_eff, rb, sbytes, 0, (int)K.L.cx);                                // HD + HI
@@ -1319,7 +1428,7 @@ struct cbev_ctx {
   hipEvent_t* prof_ev;  // 4 per recorded step
   int npitch;            // nibble-packed map pitch (bytes)
   int hero_ne, hero_sb;  // staged thread-per-env kernels: envs per workgroup, staged bytes per record
-  int coll_ne, coll_sb;
+  int coll_ne, coll_sb, coll_scr;
 };
 
 // envs per workgroup for a staged kernel: the largest divisor of 64 whose
@@ -1470,9 +1579,10 @@ int cbev_create(const cbev_params* params, const cbev_caps* caps, int device, cb
   c->device = device;
   c->hero_sb = (int)c->L.raw_x;  // HD, HI, ego route cx / cy / cyaw
   c->coll_sb = (int)c->L.acx;    // ... + raw route, visibility, actor AD / AI groups
-  c->hero_ne = staged_ne(c->hero_sb);
-  c->coll_ne = staged_ne(c->coll_sb);
-  if (c->coll_ne * c->coll_sb > 160 * 1024) {
+  c->hero_ne = staged_ne(c->hero_sb + 8 * c->C.route_cap + 16);
+  c->coll_scr = coll_scratch_layout(c->C, c->L.vis_words).bytes;
+  c->coll_ne = staged_ne(c->coll_sb + c->coll_scr);
+  if (c->coll_ne * (c->coll_sb + c->coll_scr) > 160 * 1024) {
     free(c);
     return set_err(CBEV_EINVAL, "record prefix of %d bytes does not fit LDS", c->coll_sb);
   }
@@ -1481,9 +1591,11 @@ int cbev_create(const cbev_params* params, const cbev_caps* caps, int device, cb
   hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(c_sg), &T, sizeof T);
   if (e == hipSuccess) e = hipMalloc(&c->lut_dev, 64 * sizeof(uint32_t));
   if (e == hipSuccess)
-    e = hipFuncSetAttribute((const void*)k_hero, hipFuncAttributeMaxDynamicSharedMemorySize, c->hero_ne * c->hero_sb);
+    e = hipFuncSetAttribute((const void*)k_hero, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            c->hero_ne * (c->hero_sb + 8 * c->C.route_cap + 16));
   if (e == hipSuccess)
-    e = hipFuncSetAttribute((const void*)k_collide, hipFuncAttributeMaxDynamicSharedMemorySize, c->coll_ne * c->coll_sb);
+    e = hipFuncSetAttribute((const void*)k_collide, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            c->coll_ne * (c->coll_sb + c->coll_scr));
   if (e == hipSuccess)
     e = hipFuncSetAttribute(raster_kernel(P.size), hipFuncAttributeMaxDynamicSharedMemorySize, (int)raster_lds_bytes(P));
   if (e == hipSuccess)
@@ -1575,7 +1687,8 @@ int cbev_step(cbev_ctx* c, void* records, int n, const void* actions, uint8_t* f
   hipEvent_t* ev = nullptr;
   if (c->prof_on && c->prof_n < CBEV_PROF_MAX) ev = c->prof_ev + 4 * c->prof_n++;
   if (ev) HIP_TRY(hipEventRecord(ev[0], s));
-  hipLaunchKernelGGL(k_hero, dim3((n + c->hero_ne - 1) / c->hero_ne), dim3(256), (size_t)c->hero_ne * c->hero_sb, s, K,
+  hipLaunchKernelGGL(k_hero, dim3((n + c->hero_ne - 1) / c->hero_ne), dim3(256),
+                     (size_t)c->hero_ne * (c->hero_sb + 8 * c->C.route_cap + 16), s, K,
                      (uint8_t*)records, n, actions, c->hero_ne, c->hero_sb);
   if (c->C.actor_cap > 0) hipLaunchKernelGGL(k_actors, dim3(wg4), dim3(256), 0, s, K, (uint8_t*)records, n);
   if (ev) HIP_TRY(hipEventRecord(ev[1], s));
@@ -1588,7 +1701,8 @@ int cbev_step(cbev_ctx* c, void* records, int n, const void* actions, uint8_t* f
     }
   }
   if (ev) HIP_TRY(hipEventRecord(ev[2], s));
-  hipLaunchKernelGGL(k_collide, dim3((n + c->coll_ne - 1) / c->coll_ne), dim3(256), (size_t)c->coll_ne * c->coll_sb, s,
+  hipLaunchKernelGGL(k_collide, dim3((n + c->coll_ne - 1) / c->coll_ne), dim3(256),
+                     (size_t)c->coll_ne * (c->coll_sb + c->coll_scr), s,
                      K, (uint8_t*)records, n, reward, term, trunc, cause, info, c->coll_ne, c->coll_sb);
   if (ev) HIP_TRY(hipEventRecord(ev[3], s));
   HIP_TRY(hipGetLastError());
