@@ -428,9 +428,9 @@ __device__ __forceinline__ int xcd_env4_of_wg(int w, int wave, int n) {
 // ---- in-kernel phase stamps (timing builds only, -DCBEV_TIMING): thread 0 of
 // each workgroup records s_memtime at phase boundaries; read by cbev_debug_times.
 #ifdef CBEV_TIMING
-__device__ unsigned long long g_stamps[3][4096][4];
-__device__ unsigned long long g_rtstamps[3][4096][4];  // s_memrealtime (constant 100 MHz)
-__device__ unsigned g_xcc[3][4096];                    // XCC (XCD) the workgroup ran on
+__device__ unsigned long long g_stamps[6][4096][4];
+__device__ unsigned long long g_rtstamps[6][4096][4];  // s_memrealtime (constant 100 MHz)
+__device__ unsigned g_xcc[6][4096];                    // XCC (XCD) the workgroup ran on
 #define CBEV_STAMP(kern, slot)                                                  \
   if (threadIdx.x == 0 && blockIdx.x < 4096) {                                  \
     g_stamps[kern][blockIdx.x][slot] = __builtin_amdgcn_s_memtime();            \
@@ -501,29 +501,49 @@ __device__ __forceinline__ void d_store_render_setup(const cbev_params& P, int32
 // ============================================================== k_hero / k_actors
 // Ego update: one thread per env, so all 64 lanes of a wave carry the float64
 // scalar chain of 64 envs (BaseAgent.physics_step, hero.py:88-138).
-__device__ __forceinline__ void hero_env(const KArgs& K, DRec r, int e, const void* __restrict__ actions,
-                                         const double* __restrict__ route_dist) {
-  double* hd = r.hd;
-  int32_t* hi = r.hi;
-
-  // decode_action (envs/spaces.py:43-47); continuous: ContinuousAgent clips in float32
-  float g, sa, b;
+// decode_action (envs/spaces.py:43-47); continuous: ContinuousAgent clips in float32
+__device__ __forceinline__ void d_decode_action(const KArgs& K, const void* __restrict__ actions, int e, float* g,
+                                                float* sa, float* b) {
   if (K.P.action_kind == 0) {
     int idx = ((const int32_t*)actions)[e];
     idx = idx < 0 ? 0 : (idx >= K.P.n_discrete ? K.P.n_discrete - 1 : idx);
-    g = K.P.action_table[idx][0];
-    sa = K.P.action_table[idx][1];
-    b = K.P.action_table[idx][2];
+    *g = K.P.action_table[idx][0];
+    *sa = K.P.action_table[idx][1];
+    *b = K.P.action_table[idx][2];
   } else {
     const float* a3 = (const float*)actions + 3 * (int64_t)e;
-    g = a3[0];
-    sa = a3[1];
-    b = a3[2];
-    g = (g != g) ? g : (g < 0.0f ? 0.0f : (g > 1.0f ? 1.0f : g));
-    sa = (sa != sa) ? sa : (sa < -1.0f ? -1.0f : (sa > 1.0f ? 1.0f : sa));
-    b = (b != b) ? b : (b < 0.0f ? 0.0f : (b > 1.0f ? 1.0f : b));
+    float x = a3[0], y = a3[1], z = a3[2];
+    *g = (x != x) ? x : (x < 0.0f ? 0.0f : (x > 1.0f ? 1.0f : x));
+    *sa = (y != y) ? y : (y < -1.0f ? -1.0f : (y > 1.0f ? 1.0f : y));
+    *b = (z != z) ? z : (z < 0.0f ? 0.0f : (z > 1.0f ? 1.0f : z));
   }
+}
+
+// BaseAgent.steering (hero.py:147-155): speed-dependent max steer
+__device__ __forceinline__ double d_hero_delta(double v, float sa) {
+  if (fabs(v) < 0.1) return 0.0;
+  double steer_deg = 18.0 / (1.0 + 0.35 * fabs(v));
+  steer_deg = d_clip(steer_deg, 8.0, 18.0);
+  return d_radians((double)sa * steer_deg);
+}
+
+// Per-env values k_hero computes ahead of the scalar chain, on separate waves:
+// cos / sin of the pre-update yaw (front axle and State.update) and
+// tan(clip(delta)) of State.update.
+struct HeroPre {
+  double cyaw, syaw, tdelta;
+};
+
+// Ego update, part A (one thread per env): target search reduction, throttle /
+// brake, State.update, damping (BaseAgent.physics_step, hero.py:88-138).
+__device__ __forceinline__ void hero_env_a(const KArgs& K, DRec r, int e, const void* __restrict__ actions,
+                                           const double* __restrict__ route_dist, const HeroPre& hp) {
+  double* hd = r.hd;
+  int32_t* hi = r.hi;
+  float g, sa, b;
+  d_decode_action(K, actions, e, &g, &sa, &b);
   hd[CBEV_HD_T] += CB_DT;  // Scene._t += dt (scene.py:91)
+  CBEV_STAMP(3, 0);
 
   double s[8];
 #pragma unroll
@@ -547,14 +567,7 @@ __device__ __forceinline__ void hero_env(const KArgs& K, DRec r, int e, const vo
   const int scale = K.P.scale;
   // BaseAgent.accelerate / steering / brake (hero.py:140-162)
   const double acc_val = (g > 0.0f) ? (double)((g * 1.0f) * (float)scale) : 0.0;
-  double delta;
-  if (fabs(v) < 0.1) {
-    delta = 0.0;
-  } else {
-    double steer_deg = 18.0 / (1.0 + 0.35 * fabs(v));
-    steer_deg = d_clip(steer_deg, 8.0, 18.0);
-    delta = d_radians((double)sa * steer_deg);
-  }
+  const double delta = d_hero_delta(v, sa);
   const double sf = d_clip(fabs(v) / 5.0, 0.3, 1.0);
   // NEP 50: float32(brake * 0.6) * scale in float32, then * float64 speed factor
   const double brake_val = (b > 0.0f) ? (double)((b * 0.6f) * (float)scale) * sf : 0.0 * 0.6 * scale * sf;
@@ -562,7 +575,17 @@ __device__ __forceinline__ void hero_env(const KArgs& K, DRec r, int e, const vo
   const double alpha = 0.2;
   const double acc = (1 - alpha) * hd[CBEV_HD_ACC] + alpha * target_acc;
   hd[CBEV_HD_ACC] = acc;
-  d_state_update(s, acc, delta, hd[CBEV_HD_TSPEED]);
+  // State.update (state.py:29-51) with the precomputed cos / sin / tan
+  s[4] = s[0];
+  s[5] = s[1];
+  s[6] = s[2];
+  s[7] = s[3];
+  s[0] += s[3] * hp.cyaw * CB_DT;
+  s[1] += s[3] * hp.syaw * CB_DT;
+  s[2] += s[3] / CB_WHEELBASE * hp.tdelta * CB_DT;
+  s[3] += acc * CB_DT;
+  s[2] = d_angle_mod(s[2]);
+  s[3] = d_clip(s[3], -1.0 * hd[CBEV_HD_TSPEED], hd[CBEV_HD_TSPEED]);
   s[3] *= 0.9999;
   if (fabs(s[3]) < 0.05) s[3] = 0.0;
   s[3] *= 0.985;
@@ -572,10 +595,19 @@ __device__ __forceinline__ void hero_env(const KArgs& K, DRec r, int e, const vo
   hd[CBEV_HD_U_STEER] = (double)sa;
   hd[CBEV_HD_U_BRAKE] = (double)b;
   hd[CBEV_HD_U_DELTA] = delta;
-  // compute_comfort_kinematics (comfort.py:17-61)
+  CBEV_STAMP(3, 1);
+}
+
+// Ego update, part B1: compute_comfort_kinematics (comfort.py:17-61) and the
+// Scene dist2goal bookkeeping (scene.py:97-98,175-177)
+__device__ __forceinline__ void hero_env_comfort(DRec r) {
+  double* hd = r.hd;
+  int32_t* hi = r.hi;
+  const double x = hd[CBEV_HD_X], y = hd[CBEV_HD_Y], yaw = hd[CBEV_HD_YAW], v = hd[CBEV_HD_V];
+  const double yaw1 = hd[CBEV_HD_YAW1], v1 = hd[CBEV_HD_V1];
   const int has_prev = hi[CBEV_HI_HAS_PREV_COMFORT];
-  const double speed_mps = s[3] * CB_MPP, prev_speed_mps = s[7] * CB_MPP;
-  const double dyaw = s[2] - s[6];
+  const double speed_mps = v * CB_MPP, prev_speed_mps = v1 * CB_MPP;
+  const double dyaw = yaw - yaw1;
   const double yr_rad = atan2(sin(dyaw), cos(dyaw)) / CB_DT;
   const double yr_deg = d_degrees(yr_rad);
   const double al = (speed_mps - prev_speed_mps) / CB_DT;
@@ -591,13 +623,18 @@ __device__ __forceinline__ void hero_env(const KArgs& K, DRec r, int e, const vo
   hd[CBEV_HD_PREV_ALAT] = alat;
   hd[CBEV_HD_PREV_YR] = yr_deg;
   hi[CBEV_HI_HAS_PREV_COMFORT] = 1;
-  // Scene dist2goal bookkeeping (scene.py:97-98,175-177)
   hd[CBEV_HD_D2G_T1] = hd[CBEV_HD_D2G];
-  const double gx = s[0] - hd[CBEV_HD_GOAL_X], gy = s[1] - hd[CBEV_HD_GOAL_Y];
+  const double gx = x - hd[CBEV_HD_GOAL_X], gy = y - hd[CBEV_HD_GOAL_Y];
   hd[CBEV_HD_D2G] = sqrt(gx * gx + gy * gy);
-  // render set-up of this step's observation (crop origin + rotation), once per
-  // env here instead of in every raster wave
-  d_store_render_setup(K.P, r.hi, s[0], s[1], (float)(d_degrees(s[2]) + 90));
+  CBEV_STAMP(3, 2);
+}
+
+// Ego update, part B2: render set-up of this step's observation (crop origin +
+// rotation), once per env here instead of in every raster wave
+__device__ __forceinline__ void hero_env_render_setup(const KArgs& K, DRec r) {
+  const double* hd = r.hd;
+  d_store_render_setup(K.P, r.hi, hd[CBEV_HD_X], hd[CBEV_HD_Y], (float)(d_degrees(hd[CBEV_HD_YAW]) + 90));
+  CBEV_STAMP(3, 3);
 }
 
 __global__ __launch_bounds__(256) void k_hero(KArgs K, uint8_t* __restrict__ recs, int n,
@@ -608,28 +645,73 @@ __global__ __launch_bounds__(256) void k_hero(KArgs K, uint8_t* __restrict__ rec
   if (ne_eff <= 0) return;
   const int64_t rb = K.L.record_bytes;
   const int R = K.C.route_cap, tid = threadIdx.x;
-  double* fxy = (double*)(lds + ne * sbytes);  // [ne][2] front-axle position
-  double* dist = fxy + 2 * ne;                 // [ne][R] hypot(front axle - route point)
+  const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  double* dist = (double*)(lds + ne * sbytes);  // [ne][R] hypot(front axle - route point), +inf off-candidate
+  HeroPre* pre = (HeroPre*)(dist + ne * R);      // [ne]
   CBEV_STAMP(0, 0);
   stage_in(lds, recs, e0, ne_eff, rb, sbytes);
   __syncthreads();
   CBEV_STAMP(0, 1);
-  if (tid < ne_eff) {  // Controller.calc_target_index's front axle (stanley_controller.py:51-62), pre-update state
-    const double* hd = (const double*)(lds + tid * sbytes + K.L.hd);
-    fxy[2 * tid] = hd[CBEV_HD_X] + CB_WHEELBASE * cos(hd[CBEV_HD_YAW]);
-    fxy[2 * tid + 1] = hd[CBEV_HD_Y] + CB_WHEELBASE * sin(hd[CBEV_HD_YAW]);
+  // P1, one lane per env on two waves at once: cos / sin of the yaw (wave 0) and
+  // tan(clip(delta)) (wave 1)
+  if (lane < ne_eff) {
+    const double* hd = (const double*)(lds + lane * sbytes + K.L.hd);
+    if (wave == 0) {
+      pre[lane].cyaw = cos(hd[CBEV_HD_YAW]);
+      pre[lane].syaw = sin(hd[CBEV_HD_YAW]);
+    } else if (wave == 1) {
+      float g, sa, b;
+      d_decode_action(K, actions, e0 + lane, &g, &sa, &b);
+      const double max_steer = 30.0 * (CB_PI / 180.0);
+      pre[lane].tdelta = tan(d_clip(d_hero_delta(hd[CBEV_HD_V], sa), -max_steer, max_steer));
+    }
   }
   __syncthreads();
-  for (int q = tid; q < ne_eff * R; q += 256) {  // the hypot of every route point, over all threads
-    const int k = q / R, i = q - k * R;
-    const uint8_t* base = lds + k * sbytes;
-    if (i < ((const int32_t*)(base + K.L.hi))[CBEV_HI_NROUTE])
-      dist[k * R + i] = hypot(fxy[2 * k] - ((const double*)(base + K.L.cx))[i],
-                              fxy[2 * k + 1] - ((const double*)(base + K.L.cy))[i]);
+  // P2: Controller.calc_target_index (stanley_controller.py:51-62) on the
+  // pre-update state, over (env, route point) pairs, env k = tid / tpe. The
+  // squared distance is within a few ulp of hypot^2, so only points within
+  // (1 + 1e-14) of the smallest squared distance can hold the hypot minimum;
+  // hypot is evaluated for those (+inf elsewhere) and k's thread then takes the
+  // first minimum, as numpy's argmin does.
+  {
+    const int tpe = 256 / ne, k = tid / tpe, sub = tid - k * tpe;
+    if (k < ne_eff) {
+      const uint8_t* base = lds + k * sbytes;
+      const double* hd = (const double*)(base + K.L.hd);
+      const double* cx = (const double*)(base + K.L.cx);
+      const double* cy = (const double*)(base + K.L.cy);
+      const int nr = ((const int32_t*)(base + K.L.hi))[CBEV_HI_NROUTE];
+      const double fx = hd[CBEV_HD_X] + CB_WHEELBASE * pre[k].cyaw;
+      const double fy = hd[CBEV_HD_Y] + CB_WHEELBASE * pre[k].syaw;
+      double m2 = INFINITY;
+#pragma unroll 4
+      for (int i = sub; i < nr; i += tpe) {
+        const double dx = fx - cx[i], dy = fy - cy[i];
+        const double d2 = dx * dx + dy * dy;
+        m2 = d2 < m2 ? d2 : m2;
+      }
+      for (int o = tpe >> 1; o > 0; o >>= 1) {
+        const double t = __shfl_xor(m2, o, tpe);
+        m2 = t < m2 ? t : m2;
+      }
+      const double lim = m2 * (1.0 + 1e-14);
+      for (int i = sub; i < nr; i += tpe) {
+        const double dx = fx - cx[i], dy = fy - cy[i];
+        double d = INFINITY;
+        if (dx * dx + dy * dy <= lim) d = hypot(dx, dy);
+        dist[k * R + i] = d;
+      }
+    }
   }
   __syncthreads();
-  if (tid < ne_eff)
-    hero_env(K, bind_rec(lds + tid * sbytes, K.L, K.C), e0 + tid, actions, dist + tid * R);
+  // A: the scalar chain, one thread per env
+  if (tid < ne_eff) hero_env_a(K, bind_rec(lds + tid * sbytes, K.L, K.C), e0 + tid, actions, dist + tid * R, pre[tid]);
+  __syncthreads();
+  // B: comfort + dist2goal (wave 1) beside the render set-up (wave 2)
+  if (lane < ne_eff) {
+    if (wave == 1) hero_env_comfort(bind_rec(lds + lane * sbytes, K.L, K.C));
+    else if (wave == 2) hero_env_render_setup(K, bind_rec(lds + lane * sbytes, K.L, K.C));
+  }
   CBEV_STAMP(0, 2);
   __syncthreads();
   stage_out(lds, recs, e0, ne_eff, rb, sbytes, 0, (int)K.L.cx);  // HD + HI
@@ -1019,6 +1101,7 @@ __device__ __forceinline__ void collide_env(const KArgs& K, DRec r, int e, const
   // ---- collisions (scene.py:110-140): hero rect vs vehicles, pedestrians, visible
   // targets; the last hit in iteration order (vehicles, pedestrians, then targets)
   // wins; every visible target hit is consumed (rect tests in k_collide's pre-pass)
+  CBEV_STAMP(4, 0);
   const int nact = hi[CBEV_HI_NACT];
   const int nt = hi[CBEV_HI_NROUTE];
   const int tgt_last = pre.ints[CS_TGT_LAST], act_last = pre.ints[CS_ACT_LAST];
@@ -1059,6 +1142,7 @@ __device__ __forceinline__ void collide_env(const KArgs& K, DRec r, int e, const
   hi[CBEV_HI_COLLIDED] = result;
   hi[CBEV_HI_ACTOR_ID] = coll_id;
   hi[CBEV_HI_NACTSTATE] = nas;
+  CBEV_STAMP(4, 1);
 
   // scene_info / controller_info (scene.py:206-225, stanley_controller.py:125-163)
   const int tidx = hi[CBEV_HI_TIDX];
@@ -1203,6 +1287,7 @@ __device__ __forceinline__ void collide_env(const KArgs& K, DRec r, int e, const
     }
   }
   hd[CBEV_HD_REWARD] = reward;
+  CBEV_STAMP(4, 2);
   // Stats.step accumulators (stats.py:30-56)
   hd[CBEV_HD_EP_RETURN] += reward;
   hd[CBEV_HD_EP_SPEED] += v;
@@ -1236,6 +1321,7 @@ __device__ __forceinline__ void collide_env(const KArgs& K, DRec r, int e, const
     o[14] = (float)result;
     o[15] = (float)nas;
   }
+  CBEV_STAMP(4, 3);
 }
 
 __global__ __launch_bounds__(256) void k_collide(KArgs K, uint8_t* __restrict__ recs, int n,
@@ -1270,30 +1356,37 @@ __global__ __launch_bounds__(256) void k_collide(KArgs K, uint8_t* __restrict__ 
   }
   __syncthreads();
   // ---- cooperative pre-pass over (env, element) pairs
+  CBEV_STAMP(5, 0);
   {
-    const int R = K.C.route_cap, A = K.C.actor_cap;
-    // raw-route segments (carl_reward_fn.py:36-48)
-    for (int q = tid; q < ne_eff * (R - 1); q += 256) {
-      const int k = q / (R - 1), i = q - k * (R - 1);
+    const int A = K.C.actor_cap;
+    // (env k, element i) pairs: env k = tid / tpe, elements sub, sub + tpe, ...
+    const int tpe = 256 / ne, k = tid / tpe, sub = tid - k * tpe;
+    if (k < ne_eff) {
       DRec r = bind_rec(lds + k * sbytes, K.L, K.C);
-      if (i < r.hi[CBEV_HI_NRAW] - 1)
-        ((double*)(scr + k * SL.bytes + SL.segd))[i] = sqrt(d_seg_dist2(r, i, r.hd[CBEV_HD_X], r.hd[CBEV_HD_Y]));
-    }
-    // visible targets vs the hero rect (target.py:37-44)
-    for (int q = tid; q < ne_eff * R; q += 256) {
-      const int k = q / R, i = q - k * R;
-      DRec r = bind_rec(lds + k * sbytes, K.L, K.C);
-      const int nt = r.hi[CBEV_HI_NROUTE];
-      if (i >= nt || !((r.vis[i >> 5] >> (i & 31)) & 1u)) continue;
-      int* I = (int*)(scr + k * SL.bytes + SL.ints);
+      uint8_t* sk = scr + k * SL.bytes;
+      const double x = r.hd[CBEV_HD_X], y = r.hd[CBEV_HD_Y];
+      // raw-route segments (carl_reward_fn.py:36-48)
+      const int nseg = r.hi[CBEV_HI_NRAW] - 1;
+      double* segd = (double*)(sk + SL.segd);
+#pragma unroll 4
+      for (int i = sub; i < nseg; i += tpe) segd[i] = sqrt(d_seg_dist2(r, i, x, y));
+      CBEV_STAMP(5, 1);
+      // visible targets vs the hero rect (target.py:37-44)
+      int* I = (int*)(sk + SL.ints);
       const int hrx = I[3], hry = I[4];
-      const int sz = (i < nt - 1) ? 2 : 4;
-      const int trx = d_rect_lo(r.cx[i], P.pad, sz), try_ = d_rect_lo(r.cy[i], P.pad, sz);
-      if (hrx < trx + sz && hry < try_ + sz && hrx + hw > trx && hry + hw > try_) {
-        atomicOr((uint32_t*)(scr + k * SL.bytes + SL.hitw) + (i >> 5), 1u << (i & 31));
-        atomicMax(&I[CS_TGT_LAST], i);
+      const int nt = r.hi[CBEV_HI_NROUTE];
+#pragma unroll 4
+      for (int i = sub; i < nt; i += tpe) {
+        if (!((r.vis[i >> 5] >> (i & 31)) & 1u)) continue;
+        const int sz = (i < nt - 1) ? 2 : 4;
+        const int trx = d_rect_lo(r.cx[i], P.pad, sz), try_ = d_rect_lo(r.cy[i], P.pad, sz);
+        if (hrx < trx + sz && hry < try_ + sz && hrx + hw > trx && hry + hw > try_) {
+          atomicOr((uint32_t*)(sk + SL.hitw) + (i >> 5), 1u << (i & 31));
+          atomicMax(&I[CS_TGT_LAST], i);
+        }
       }
     }
+    CBEV_STAMP(5, 2);
     // vehicles / pedestrians: rect hit, actors_state entry and both TTCs (scene.py:110-140,
     // reward_signals.py:15-94)
     for (int q = tid; q < ne_eff * A; q += 256) {
@@ -1338,6 +1431,7 @@ __global__ __launch_bounds__(256) void k_collide(KArgs K, uint8_t* __restrict__ 
     }
   }
   __syncthreads();
+  CBEV_STAMP(5, 3);
   if (tid < ne_eff) {
     const uint8_t* sk = scr + tid * SL.bytes;
     const CollPre pre{(const double*)(sk + SL.segd), (const double*)(sk + SL.ttcc), (const double*)(sk + SL.ttcs),
@@ -1579,10 +1673,10 @@ int cbev_create(const cbev_params* params, const cbev_caps* caps, int device, cb
   c->device = device;
   c->hero_sb = (int)c->L.raw_x;  // HD, HI, ego route cx / cy / cyaw
   c->coll_sb = (int)c->L.acx;    // ... + raw route, visibility, actor AD / AI groups
-  c->hero_ne = staged_ne(c->hero_sb + 8 * c->C.route_cap + 16);
+  c->hero_ne = staged_ne(c->hero_sb + 8 * c->C.route_cap + 32);
   c->coll_scr = coll_scratch_layout(c->C, c->L.vis_words).bytes;
   c->coll_ne = staged_ne(c->coll_sb + c->coll_scr);
-  if (c->coll_ne * (c->coll_sb + c->coll_scr) > 160 * 1024) {
+  if (c->coll_ne * (c->coll_sb + c->coll_scr) > 160 * 1024 || c->hero_ne < 4 || c->coll_ne < 4) {
     free(c);
     return set_err(CBEV_EINVAL, "record prefix of %d bytes does not fit LDS", c->coll_sb);
   }
@@ -1592,7 +1686,7 @@ int cbev_create(const cbev_params* params, const cbev_caps* caps, int device, cb
   if (e == hipSuccess) e = hipMalloc(&c->lut_dev, 64 * sizeof(uint32_t));
   if (e == hipSuccess)
     e = hipFuncSetAttribute((const void*)k_hero, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            c->hero_ne * (c->hero_sb + 8 * c->C.route_cap + 16));
+                            c->hero_ne * (c->hero_sb + 8 * c->C.route_cap + 32));
   if (e == hipSuccess)
     e = hipFuncSetAttribute((const void*)k_collide, hipFuncAttributeMaxDynamicSharedMemorySize,
                             c->coll_ne * (c->coll_sb + c->coll_scr));
@@ -1688,7 +1782,7 @@ int cbev_step(cbev_ctx* c, void* records, int n, const void* actions, uint8_t* f
   if (c->prof_on && c->prof_n < CBEV_PROF_MAX) ev = c->prof_ev + 4 * c->prof_n++;
   if (ev) HIP_TRY(hipEventRecord(ev[0], s));
   hipLaunchKernelGGL(k_hero, dim3((n + c->hero_ne - 1) / c->hero_ne), dim3(256),
-                     (size_t)c->hero_ne * (c->hero_sb + 8 * c->C.route_cap + 16), s, K,
+                     (size_t)c->hero_ne * (c->hero_sb + 8 * c->C.route_cap + 32), s, K,
                      (uint8_t*)records, n, actions, c->hero_ne, c->hero_sb);
   if (c->C.actor_cap > 0) hipLaunchKernelGGL(k_actors, dim3(wg4), dim3(256), 0, s, K, (uint8_t*)records, n);
   if (ev) HIP_TRY(hipEventRecord(ev[1], s));
@@ -1756,13 +1850,13 @@ int cbev_expand_obs(cbev_ctx* c, const uint8_t* ring, int n, int n_frames, int h
 }
 
 #ifdef CBEV_TIMING
-// timing builds only: copy the phase stamps [3][4096][4] (u64 s_memtime ticks)
+// timing builds only: copy the phase stamps [6][4096][4] (u64 s_memtime ticks), realtime stamps, XCC ids
 int cbev_debug_times(unsigned long long* out_host) {
   if (hipMemcpyFromSymbol(out_host, HIP_SYMBOL(g_stamps), sizeof(g_stamps)) != hipSuccess) return -1;
-  if (hipMemcpyFromSymbol(out_host + 3 * 4096 * 4, HIP_SYMBOL(g_rtstamps), sizeof(g_rtstamps)) != hipSuccess) return -1;
-  unsigned x[3 * 4096];
+  if (hipMemcpyFromSymbol(out_host + 6 * 4096 * 4, HIP_SYMBOL(g_rtstamps), sizeof(g_rtstamps)) != hipSuccess) return -1;
+  static unsigned x[6 * 4096];
   if (hipMemcpyFromSymbol(x, HIP_SYMBOL(g_xcc), sizeof(x)) != hipSuccess) return -1;
-  for (int i = 0; i < 3 * 4096; ++i) out_host[6 * 4096 * 4 + i] = x[i];
+  for (int i = 0; i < 6 * 4096; ++i) out_host[12 * 4096 * 4 + i] = x[i];
   return 0;
 }
 #endif

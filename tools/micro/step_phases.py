@@ -41,11 +41,13 @@ L.cbev_debug_times.argtypes = [ctypes.c_void_p]
 for t in range(a.steps):
     env.step_async_only(acts[t])
 torch.cuda.synchronize()
-buf = np.zeros(2 * 3 * 4096 * 4 + 3 * 4096, np.uint64)
+buf = np.zeros(2 * 6 * 4096 * 4 + 6 * 4096, np.uint64)
 assert L.cbev_debug_times(buf.ctypes.data_as(ctypes.c_void_p)) == 0
-xcc = buf[2 * 3 * 4096 * 4:].reshape(3, 4096).astype(np.int64)
-buf = buf[:2 * 3 * 4096 * 4].reshape(2, 3, 4096, 4)
-for k, name in enumerate(("k_hero", "k_collide", "k_raster")):
+xcc = buf[2 * 6 * 4096 * 4:].reshape(6, 4096).astype(np.int64)
+buf = buf[:2 * 6 * 4096 * 4].reshape(2, 6, 4096, 4)
+for k, name in enumerate(("k_hero", "k_collide", "k_raster", "hero_env(thread0)", "collide_env(thread0)", "k_collide pre-pass: segs/targets/actors+sync")):
+    if not (buf[0, k, :, 0] > 0).any():
+        continue
     st = buf[0, k].astype(np.int64)
     rt = buf[1, k].astype(np.int64)
     used = st[:, 0] > 0
