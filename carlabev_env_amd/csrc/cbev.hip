@@ -336,19 +336,6 @@ __device__ __forceinline__ void lds_set_nib(uint8_t* lds, uint32_t na, uint32_t 
 }
 __host__ __device__ __forceinline__ int raster_image_bytes(int C) { return C * raster_stride_dwords(C) * 4; }
 
-// Paint a square rect of side sz (<= 4 * nb) into the LDS crop: 16 lanes per
-// rect, lane p covers pixel (p & 3, p >> 2) of each 4x4 block of the rect.
-__device__ __forceinline__ void lds_paint_rect(uint8_t* lds, int sb, int shift, int C, int rx, int ry, int sz, int nb,
-                                               int p, uint8_t col) {
-  const int ox = p & 3, oy = p >> 2;
-  for (int by = 0; by < nb; ++by)
-    for (int bx = 0; bx < nb; ++bx) {
-      const int qx = 4 * bx + ox, qy = 4 * by + oy;
-      const int px = rx + qx, py = ry + qy;
-      if (qx < sz && qy < sz && px >= 0 && py >= 0 && px < C && py < C) lds_set_nib(lds, py * 2 * sb + shift + px, col);
-    }
-}
-
 // Per-env rotation parameters (pygame transform.rotate, 16.16 fixed point;
 // rotate90 for exact multiples of 90 degrees) and the compose placement.
 struct RotSetup {
@@ -485,6 +472,24 @@ __device__ __forceinline__ void stage_out(const uint8_t* lds, uint8_t* __restric
   }
 }
 
+// Does the whole output sample inside the crop with the rotated surface covering
+// it? Then raster_out runs without per-pixel tests and only the crop texels
+// the output can sample need staging. The map from output pixels to source
+// coordinates is affine, so checking the four output corners is exact.
+__device__ __forceinline__ bool raster_fast(const cbev_params& P, const RotSetup& R) {
+  const int S = P.size;
+  const bool full = R.rx0 <= 0 && R.ry0 <= 0 && R.rx0 + R.nx >= S && R.ry0 + R.ny >= S;
+  if (R.r90 || !full) return full;
+  bool inb = true;
+  const uint32_t vmax = (uint32_t)((P.crop << 16) - 1);
+  for (int c = 0; c < 4 && inb; ++c) {
+    const int64_t xx = (int64_t)((c & 1) ? S - 1 : 0) - R.rx0, yy = (int64_t)((c & 2) ? S - 1 : 0) - R.ry0;
+    const int64_t dx = R.dx00 + xx * R.icos - yy * R.isin, dy = R.dy00 + xx * R.isin + yy * R.icos;
+    inb = dx >= 0 && dy >= 0 && dx <= (int64_t)vmax && dy <= (int64_t)vmax;
+  }
+  return inb;
+}
+
 // The render set-up lives in the record's RS_* ints (written by k_hero, read by k_raster).
 __device__ __forceinline__ void d_store_render_setup(const cbev_params& P, int32_t* hi, double x, double y,
                                                      float angle) {
@@ -496,6 +501,7 @@ __device__ __forceinline__ void d_store_render_setup(const cbev_params& P, int32
   const int32_t* w = (const int32_t*)&R;
 #pragma unroll
   for (int k = 0; k < CBEV_RS_WORDS; ++k) hi[CBEV_HI_RS_R90 + k] = w[k];
+  hi[CBEV_HI_RS_FAST] = raster_fast(P, R);  // so every raster wave does not redo the corner test
 }
 
 // ============================================================== k_hero / k_actors
@@ -749,7 +755,8 @@ __device__ __forceinline__ void raster_out(const cbev_params& P, const RotSetup&
                                            int shift, uint32_t bg, uint8_t* __restrict__ out, int nout,
                                            int64_t out_stride, int lane, int wave) {
   constexpr int RPC = 16 / G;  // output rows per chunk
-  const int S = P.size, C = P.crop;
+  constexpr int S = 64 * G;    // == P.size
+  const int C = P.crop;
   const uint32_t vmax = (uint32_t)((C << 16) - 1);
   const int hero_w = P.hero_w;
   const int hx0 = P.anchor_x - hero_w / 2, hy0 = P.anchor_y - hero_w / 2;
@@ -775,10 +782,21 @@ __device__ __forceinline__ void raster_out(const cbev_params& P, const RotSetup&
   const uint32_t sb = 4u * (uint32_t)raster_stride_dwords(C);  // LDS bytes per crop row
   const int chunk_rows = 4 * RPC;                 // the 4 waves interleave chunks
   const int nchunks = S / RPC;
+  // general path: (sx, sy) packed in one 64-bit value, so one 64-bit add steps
+  // both coordinates (the low word stays in [0, 2^32): no carry crosses over)
+  uint64_t pxy = ((uint64_t)(uint32_t)sy << 32) | (uint32_t)sx;
+  const uint64_t chunk_step =
+      (uint64_t)(((int64_t)(chunk_rows * R.icos) << 32) + (int64_t)(-chunk_rows * R.isin));
+  // one output row down: (dx, dy) += (-isin, icos); 64 columns right: += 64 (icos, isin)
+  const uint64_t row_step = (uint64_t)(((int64_t)R.icos << 32) + (int64_t)(-R.isin));
+  const uint64_t col_step = (uint64_t)(((int64_t)(64 * R.isin) << 32) + (int64_t)(64 * R.icos));
   for (int ch = wave, r = r0; ch < nchunks; ch += 4, r += chunk_rows) {
-    uint8_t* o = out + (int64_t)r * S + lane;
+    // the frame is written through the uniform base `out` plus a per-lane offset
+    const uint32_t vo = (uint32_t)(r * S + lane);
     const bool hero_rows = (unsigned)(r + RPC - 1 - hy0) < (unsigned)(RPC - 1 + hero_w);  // chunk meets the hero rows
+    asm volatile("" : "+v"(pxy), "+v"(sa));  // keep the per-gather offsets as scalar adds
     uint32_t px[16];
+    uint64_t qrow = pxy;  // general path: source coordinates of (row r + rj, column lane)
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
       const int rj = j / G, cj = j % G;
@@ -792,14 +810,16 @@ __device__ __forceinline__ void raster_out(const cbev_params& P, const RotSetup&
           v = lds_nib(img, a);
         }
       } else {
-        const int dx = sx + (64 * cj * R.icos - rj * R.isin);
-        const int dy = sy + (64 * cj * R.isin + rj * R.icos);
-        const uint32_t byte = __umul24((uint32_t)dy >> 16, sb) + ((uint32_t)dx >> 17);
-        const uint32_t nsh = ((uint32_t)dx >> 14) & 4u;
+        // one 64-bit add per gather: column blocks step by col_step, rows by row_step
+        const uint64_t q = cj == 0 ? qrow : qrow + (uint64_t)cj * col_step;
+        if (cj == G - 1) qrow += row_step;
+        const uint32_t dx = (uint32_t)q, dy = (uint32_t)(q >> 32);
+        const uint32_t byte = __umul24(dy >> 16, sb) + (dx >> 17);
+        const uint32_t nsh = (dx >> 14) & 4u;
         if (CHECK) {  // bounds on the unshifted source coordinate
-          const int ux = dx - (shift << 16);
+          const int ux = (int)dx - (shift << 16);
           const bool ok = ((xok >> cj) & 1u) && (unsigned)(r + rj - R.ry0) < (unsigned)R.ny;
-          const bool in = (uint32_t)ux <= vmax && (uint32_t)dy <= vmax;
+          const bool in = (uint32_t)ux <= vmax && dy <= vmax;
           const uint32_t s = (img[(in && ok) ? byte : 0u] >> nsh) & 15u;
           v = !ok ? (uint32_t)CBEV_PX_BLACK : (in ? s : bg);
         } else {
@@ -817,89 +837,119 @@ __device__ __forceinline__ void raster_out(const cbev_params& P, const RotSetup&
     }
     if (CBEV_RASTER_PHASES & 8) {
       for (int k = 0; k < nout; ++k) {
+        uint8_t* ob = out + (int64_t)k * out_stride;
 #pragma unroll
         for (int j = 0; j < 16; ++j)  // streamed out: keep the L2 for the map and the records
-          __builtin_nontemporal_store((uint8_t)px[j], o + (int64_t)k * out_stride + (j / G) * S + 64 * (j % G));
+          __builtin_nontemporal_store((uint8_t)px[j], ob + (vo + (uint32_t)((j / G) * S + 64 * (j % G))));
       }
     } else {
       uint32_t acc = 0;
 #pragma unroll
       for (int j = 0; j < 16; ++j) acc += px[j];
-      if (acc == 0x7fffffffu) o[0] = 1;  // keeps the gathers live
+      if (acc == 0x7fffffffu) out[vo] = 1;  // keeps the gathers live
     }
-    sx -= chunk_rows * R.isin;
-    sy += chunk_rows * R.icos;
+    pxy += chunk_step;
     sa += chunk_rows * R.vstep;
   }
 }
 
 template <int G>
-__device__ __forceinline__ void raster_out_dispatch(const cbev_params& P, const RotSetup& R, const uint8_t* lds,
-                                                    int shift, uint32_t bg, uint8_t* out, int nout, int64_t out_stride,
-                                                    int lane, int wave) {
-  const int S = P.size;
-  // compose: does the rotated surface cover the whole output?
-  const bool full = R.rx0 <= 0 && R.ry0 <= 0 && R.rx0 + R.nx >= S && R.ry0 + R.ny >= S;
+__device__ __forceinline__ void raster_out_dispatch(const cbev_params& P, const RotSetup& R, bool fast,
+                                                    const uint8_t* lds, int shift, uint32_t bg, uint8_t* out, int nout,
+                                                    int64_t out_stride, int lane, int wave) {
   if (R.r90) {
-    if (full) raster_out<G, true, false>(P, R, lds, shift, bg, out, nout, out_stride, lane, wave);
+    if (fast) raster_out<G, true, false>(P, R, lds, shift, bg, out, nout, out_stride, lane, wave);
     else      raster_out<G, true, true>(P, R, lds, shift, bg, out, nout, out_stride, lane, wave);
-    return;
+  } else {
+    if (fast) raster_out<G, false, false>(P, R, lds, shift, bg, out, nout, out_stride, lane, wave);
+    else      raster_out<G, false, true>(P, R, lds, shift, bg, out, nout, out_stride, lane, wave);
   }
-  // every output pixel inside the source: check the four output corners
-  bool inb = full;
-  const uint32_t vmax = (uint32_t)((P.crop << 16) - 1);
-  for (int c = 0; c < 4 && inb; ++c) {
-    const int64_t xx = (int64_t)((c & 1) ? S - 1 : 0) - R.rx0, yy = (int64_t)((c & 2) ? S - 1 : 0) - R.ry0;
-    const int64_t dx = R.dx00 + xx * R.icos - yy * R.isin, dy = R.dy00 + xx * R.isin + yy * R.icos;
-    inb = dx >= 0 && dy >= 0 && dx <= (int64_t)vmax && dy <= (int64_t)vmax;
-  }
-  if (inb) raster_out<G, false, false>(P, R, lds, shift, bg, out, nout, out_stride, lane, wave);
-  else     raster_out<G, false, true>(P, R, lds, shift, bg, out, nout, out_stride, lane, wave);
 }
 
 // Render one env's observation (whole 256-thread workgroup). RESET: BaseMap.reset's
 // frame (theta = 0, no actors drawn, world.py:92-100). The frame is written to
 // `nout` destinations out + k*out_stride (the frame-stack ring on reset).
 // Paint actors / visible targets / traffic lights into the LDS crop in the
-// reference's draw order (scene.py:93-95, actor_manager.py:121-132).
-__device__ __forceinline__ void raster_paint(const KArgs& K, const DRec& r, int xmin, int ymin, int shift, int lane,
-                                             int wave, uint8_t* __restrict__ lds) {
+// reference's draw order (scene.py:93-95, actor_manager.py:121-132): vehicles,
+// pedestrians, visible targets, traffic lights, later wins. Four threads per
+// rect (actor or target tid >> 2); their record fields are fetched into
+// registers before the crop staging, so the loads' latency hides under it.
+struct PaintPre {
+  int nact, nveh, nt, ntl;
+  double ax, ay;  // actor tid >> 2
+  int asz;
+  double tx, ty;  // target tid >> 2
+  int tvis;
+};
+
+__device__ __forceinline__ PaintPre raster_paint_fetch(const DRec& r) {
+  PaintPre q;
+  q.nact = r.hi[CBEV_HI_NACT];
+  q.nveh = r.hi[CBEV_HI_NVEH];
+  q.nt = r.hi[CBEV_HI_NROUTE];
+  q.ntl = r.hi[CBEV_HI_NTL];
+  const int k = threadIdx.x >> 2;
+  q.ax = q.ay = q.tx = q.ty = 0.0;
+  q.asz = 0;
+  q.tvis = 0;
+  if (k < q.nact) {
+    q.ax = RAD(r, CBEV_AD_X, k);
+    q.ay = RAD(r, CBEV_AD_Y, k);
+    q.asz = RAI(r, CBEV_AI_SIZE, k);
+  }
+  if (k < q.nt) {
+    q.tvis = (r.vis[k >> 5] >> (k & 31)) & 1u;
+    q.tx = r.cx[k];
+    q.ty = r.cy[k];
+  }
+  return q;
+}
+
+// one rect of side sz (rect_from_world_center, transforms.py:46-51) by the 4
+// threads of tid >> 2: thread tq covers columns tq, tq + 4, ...
+__device__ __forceinline__ void paint_rect4(uint8_t* lds, int sb, int shift, int C, int pad, int xmin, int ymin,
+                                            double wx, double wy, int sz, int tq, uint32_t col) {
+  const int rx = d_rect_lo(wx, pad, sz) - xmin, ry = d_rect_lo(wy, pad, sz) - ymin;
+  for (int qy = 0; qy < sz; ++qy) {
+    const int py = ry + qy;
+    if (py < 0 || py >= C) continue;
+    for (int qx = tq; qx < sz; qx += 4) {
+      const int px = rx + qx;
+      if (px >= 0 && px < C) lds_set_nib(lds, py * 2 * sb + shift + px, col);
+    }
+  }
+}
+
+__device__ __forceinline__ void raster_paint(const KArgs& K, const DRec& r, const PaintPre& q, int xmin, int ymin,
+                                             int shift, uint8_t* __restrict__ lds) {
   const cbev_params& P = K.P;
   const int C = P.crop;
   const int sb = 4 * raster_stride_dwords(C);
+  const int k = threadIdx.x >> 2, tq = threadIdx.x & 3;
   if (CBEV_RASTER_PHASES & 2) {
-    const int nact = r.hi[CBEV_HI_NACT], nveh = r.hi[CBEV_HI_NVEH];
-    const int nb = (P.hero_w + 3) >> 2;  // 4x4 blocks per rect side: vehicles are hero_w wide (vehicle.py:24)
     for (int pass = 0; pass < 2; ++pass) {  // vehicles, then pedestrians
-      const int a0 = pass == 0 ? 0 : nveh, a1 = pass == 0 ? nveh : nact;
-      for (int base = a0 + 4 * wave; base < a1; base += 16) {
-        const int a = base + (lane >> 4);
-        if (a < a1) {
-          const int sz = RAI(r, CBEV_AI_SIZE, a);
-          const int rx = d_rect_lo(RAD(r, CBEV_AD_X, a), P.pad, sz) - xmin;
-          const int ry = d_rect_lo(RAD(r, CBEV_AD_Y, a), P.pad, sz) - ymin;
-          lds_paint_rect(lds, sb, shift, C, rx, ry, sz, nb, lane & 15,
-                         pass == 0 ? CBEV_PX_VEHICLE : CBEV_PX_PEDESTRIAN);
-        }
-      }
-      if (a1 > a0) __syncthreads();
+      const int a0 = pass == 0 ? 0 : q.nveh, a1 = pass == 0 ? q.nveh : q.nact;
+      if (a1 <= a0) continue;
+      const uint32_t col = pass == 0 ? CBEV_PX_VEHICLE : CBEV_PX_PEDESTRIAN;
+      if (k >= a0 && k < a1) paint_rect4(lds, sb, shift, C, P.pad, xmin, ymin, q.ax, q.ay, q.asz, tq, col);
+      for (int a = 64 + k; a < a1; a += 64)  // more than 64 actors: fetched here
+        if (a >= a0)
+          paint_rect4(lds, sb, shift, C, P.pad, xmin, ymin, RAD(r, CBEV_AD_X, a), RAD(r, CBEV_AD_Y, a),
+                      RAI(r, CBEV_AI_SIZE, a), tq, col);
+      __syncthreads();
     }
-    const int nt = r.hi[CBEV_HI_NROUTE];
-    for (int base = 4 * wave; base < nt; base += 16) {
-      const int i = base + (lane >> 4);
-      if (i < nt && ((r.vis[i >> 5] >> (i & 31)) & 1u)) {
-        const int sz = (i < nt - 1) ? 2 : 4;  // checkpoints 2x2, goal 4x4 (scenes/utils.py:114-122)
-        const int rx = d_rect_lo(r.cx[i], P.pad, sz) - xmin;
-        const int ry = d_rect_lo(r.cy[i], P.pad, sz) - ymin;
-        lds_paint_rect(lds, sb, shift, C, rx, ry, sz, 1, lane & 15, CBEV_PX_ROUTE);
-      }
-    }
+    const int nt = q.nt;
+    // checkpoints 2x2, goal 4x4 (scenes/utils.py:114-122)
+    if (k < nt && q.tvis) paint_rect4(lds, sb, shift, C, P.pad, xmin, ymin, q.tx, q.ty, k < nt - 1 ? 2 : 4, tq,
+                                      CBEV_PX_ROUTE);
+    for (int i = 64 + k; i < nt; i += 64)
+      if ((r.vis[i >> 5] >> (i & 31)) & 1u)
+        paint_rect4(lds, sb, shift, C, P.pad, xmin, ymin, r.cx[i], r.cy[i], i < nt - 1 ? 2 : 4, tq, CBEV_PX_ROUTE);
     __syncthreads();
-    const int ntl = r.hi[CBEV_HI_NTL];
-    for (int k = 0; k < ntl; ++k) {  // traffic lights one at a time (colours may differ)
-      const int rx = r.ti[CBEV_TI_RX * r.T + k] - xmin, ry = r.ti[CBEV_TI_RY * r.T + k] - ymin;
-      const int rw = r.ti[CBEV_TI_RW * r.T + k], rh = r.ti[CBEV_TI_RH * r.T + k];
-      const uint8_t col = (uint8_t)r.ti[CBEV_TI_COLOR * r.T + k];
+    for (int t = 0; t < q.ntl; ++t) {  // traffic lights one at a time (colours may differ)
+      const int rx = r.ti[CBEV_TI_RX * r.T + t] - xmin, ry = r.ti[CBEV_TI_RY * r.T + t] - ymin;
+      const int rw = r.ti[CBEV_TI_RW * r.T + t], rh = r.ti[CBEV_TI_RH * r.T + t];
+      const uint8_t col = (uint8_t)r.ti[CBEV_TI_COLOR * r.T + t];
       for (int qy = threadIdx.x >> 4; qy < rh; qy += 16)
         for (int qx = threadIdx.x & 15; qx < rw; qx += 16) {
           const int px = rx + qx, py = ry + qy;
@@ -908,7 +958,6 @@ __device__ __forceinline__ void raster_paint(const KArgs& K, const DRec& r, int 
       __syncthreads();
     }
   }
-
 }
 
 template <bool RESET, int G>
@@ -932,6 +981,9 @@ __device__ __forceinline__ void raster_env(const KArgs& K, const DRec& r, uint8_
     xmin = ymin = 1000;
     R = rot_setup(P, 90.0f, 2 * sb);
   }
+  const bool fast = (!RESET && (CBEV_RASTER_PHASES & 16)) ? r.hi[CBEV_HI_RS_FAST] != 0 : raster_fast(P, R);
+  PaintPre pq{};
+  if (!RESET && (CBEV_RASTER_PHASES & 2)) pq = raster_paint_fetch(r);
   const int xa = (xmin >> 1) & ~15, shift = xmin - 2 * xa;  // packed byte column, nibble offset
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -974,13 +1026,13 @@ __device__ __forceinline__ void raster_env(const KArgs& K, const DRec& r, uint8_
 
   if (!RESET) {
     CBEV_STAMP(2, 1);
-    raster_paint(K, r, xmin, ymin, shift, lane, wave, lds);
+    raster_paint(K, r, pq, xmin, ymin, shift, lds);
     CBEV_STAMP(2, 2);
   }
 
   // ---- rotate (pygame transform.rotate / rotate90) + compose + ego overlay
   const uint32_t bg = lds_nib(lds, shift);  // crop top-left pixel after painting
-  if (CBEV_RASTER_PHASES & 32) raster_out_dispatch<G>(P, R, lds, shift, bg, out, nout, out_stride, lane, wave);
+  if (CBEV_RASTER_PHASES & 32) raster_out_dispatch<G>(P, R, fast, lds, shift, bg, out, nout, out_stride, lane, wave);
 }
 
 // G = size / 64 (64-pixel gathers per output row)

@@ -65,7 +65,8 @@
   /* render set-up of the current observation (device scratch, k_hero -> k_raster): */ \
   F_(RS_XMIN) F_(RS_YMIN) /* crop origin in the padded map (fov.py:70-79) */        \
   F_(RS_R90) F_(RS_NX) F_(RS_NY) F_(RS_ISIN) F_(RS_ICOS) F_(RS_DX00) F_(RS_DY00)      \
-  F_(RS_A00) F_(RS_USTEP) F_(RS_VSTEP) F_(RS_RX0) F_(RS_RY0)
+  F_(RS_A00) F_(RS_USTEP) F_(RS_VSTEP) F_(RS_RX0) F_(RS_RY0)                        \
+  F_(RS_FAST)        /* whole output samples inside the crop: no per-pixel tests */
 
 /* ---- actor scalars, float64, field-major [field][actor_cap] ----------- */
 #define CBEV_AD_FIELDS(F_)                                                     \

@@ -21,4 +21,6 @@ run pmc_write 400 --kernel-trace --pmc WRITE_SIZE
 run pmc_sq 400 --kernel-trace --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT
 run pmc_sq2 400 --kernel-trace --pmc SQ_WAIT_INST_LDS SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VMEM_RD
 run pmc_tcc 400 --kernel-trace --pmc TCC_HIT_sum TCC_MISS_sum
+run pmc_wait 400 --kernel-trace --pmc SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU
+run pmc_lds 400 --kernel-trace --pmc SQ_ACTIVE_INST_LDS SQ_LDS_IDX_ACTIVE SQ_INSTS_VMEM_WR SQ_INSTS_SALU
 exit 0
