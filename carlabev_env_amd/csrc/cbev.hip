@@ -319,11 +319,13 @@ __device__ __forceinline__ int d_rect_lo(double w, int pad, int size) { return (
 // at dword r * sd and holds the packed map bytes from xa = (xmin >> 1) & ~15 on,
 // so crop pixel (c, r) is nibble shift + c of the row (shift = xmin - 2 xa, 0..31),
 // i.e. "nibble address" r * 8 sd + shift + c: byte >> 1 of it, high nibble when odd.
-// Rows are copied as 16-byte chunks; sd is odd so that successive crop rows start
-// in different LDS banks and gathers along a rotated row spread over the banks at
-// every angle. 182 x 29 dwords = 21 KB at S=128: 7 workgroups per CU.
-__host__ __device__ __forceinline__ int raster_row_chunks(int C) { return (C + 63) / 32; }
-__host__ __device__ __forceinline__ int raster_stride_dwords(int C) { return (4 * raster_row_chunks(C)) | 1; }
+// sd = the dwords a row needs (31 + C nibbles), rounded up to odd so that
+// successive crop rows start in different LDS banks and gathers along a rotated
+// row spread over the banks at every angle. Rows are staged as 16-byte chunks
+// (the last one clipped to sd). 182 x 27 dwords = 19.7 KB at S=128: 8 workgroups
+// per CU.
+__host__ __device__ __forceinline__ int raster_stride_dwords(int C) { return ((C + 31 + 7) / 8) | 1; }
+__host__ __device__ __forceinline__ int raster_row_chunks(int C) { return (raster_stride_dwords(C) + 3) / 4; }
 // nibble-level helpers on the LDS image
 __device__ __forceinline__ uint32_t lds_nib(const uint8_t* lds, uint32_t na) {
   return (lds[na >> 1] >> ((na & 1u) << 2)) & 15u;
@@ -1014,7 +1016,7 @@ __device__ __forceinline__ void raster_env(const KArgs& K, const DRec& r, uint8_
           d[0] = v[u].x;
           d[1] = v[u].y;
           d[2] = v[u].z;
-          d[3] = v[u].w;
+          if (4 * j + 3 < sd) d[3] = v[u].w;  // the last chunk of a row may overhang the stride
         }
         row += dr;
         j += dj;
