@@ -1055,29 +1055,43 @@ __global__ __launch_bounds__(256) void k_raster(KArgs K, uint8_t* __restrict__ r
 // every slot of the frame-stack ring (FrameStackObservation padding "reset").
 // The frame is rendered from the bank record itself, so no other workgroup's
 // stores need to be visible.
+#define RESET_WGS 1024  // multiple of 8: keeps xcd_env_of_wg's XCD placement
+
 template <int G>
 __global__ __launch_bounds__(256) void k_reset(KArgs K, uint8_t* __restrict__ recs, int n,
                                                const uint8_t* __restrict__ bank, int n_bank,
                                                const uint8_t* __restrict__ mask, const int32_t* __restrict__ bank_idx,
                                                int bank_offset, uint8_t* __restrict__ ring, int n_frames) {
+  // A grid of at most RESET_WGS workgroups strides over the envs: the masks of a
+  // workgroup's 64 next positions are read at once (one lane each) and only the
+  // selected envs are copied and rendered, so a mostly-empty mask costs little.
   extern __shared__ __align__(16) uint8_t lds[];
-  const int e = xcd_env_of_wg(blockIdx.x, n);
-  if (e >= n) return;
-  if (mask != nullptr && mask[e] == 0) return;  // uniform per workgroup
   const int64_t rb = K.L.record_bytes;
-  uint8_t* dst = recs + (int64_t)e * rb;
-  const uint8_t* src = dst;
-  if (bank != nullptr) {
-    int b = bank_idx ? bank_idx[e] : (int)(((int64_t)e + bank_offset) % n_bank);
-    b = b < 0 ? 0 : (b >= n_bank ? n_bank - 1 : b);
-    src = bank + (int64_t)b * rb;
-    const uint4* s4 = (const uint4*)src;
-    uint4* d4 = (uint4*)dst;
-    for (int64_t i = threadIdx.x; i < rb / 16; i += 256) d4[i] = s4[i];
-  }
-  DRec r = bind_rec((uint8_t*)src, K.L, K.C);  // read-only use below
   const int64_t SS = (int64_t)K.P.size * K.P.size;
-  raster_env<true, G>(K, r, ring + (int64_t)e * SS, n_frames, (int64_t)n * SS, lds);
+  const int lane = threadIdx.x & 63;
+  for (int p0 = blockIdx.x; p0 < n; p0 += 64 * gridDim.x) {
+    const int pl = p0 + lane * gridDim.x;
+    const bool sel = pl < n && (mask == nullptr || mask[xcd_env_of_wg(pl, n)] != 0);
+    uint64_t todo = __ballot(sel);  // identical in every wave
+    while (todo) {
+      const int k = __builtin_ctzll(todo);
+      todo &= todo - 1;
+      const int e = xcd_env_of_wg(p0 + k * gridDim.x, n);
+      uint8_t* dst = recs + (int64_t)e * rb;
+      const uint8_t* src = dst;
+      if (bank != nullptr) {
+        int b = bank_idx ? bank_idx[e] : (int)(((int64_t)e + bank_offset) % n_bank);
+        b = b < 0 ? 0 : (b >= n_bank ? n_bank - 1 : b);
+        src = bank + (int64_t)b * rb;
+        const uint4* s4 = (const uint4*)src;
+        uint4* d4 = (uint4*)dst;
+        for (int64_t i = threadIdx.x; i < rb / 16; i += 256) d4[i] = s4[i];
+      }
+      DRec r = bind_rec((uint8_t*)src, K.L, K.C);  // read-only use below
+      raster_env<true, G>(K, r, ring + (int64_t)e * SS, n_frames, (int64_t)n * SS, lds);
+      __syncthreads();  // the LDS image is reused by the next env
+    }
+  }
 }
 
 // ============================================================== k_collide
@@ -1867,9 +1881,10 @@ int cbev_reset(cbev_ctx* c, void* records, int n, const void* bank, int n_bank, 
   KArgs K = kargs(c);
   const size_t lb = raster_lds_bytes(c->P);
   hipStream_t s = (hipStream_t)stream;
+  const int grid = n < RESET_WGS ? n : RESET_WGS;
 #define CBEV_LAUNCH_RESET(G_)                                                                                          \
-  hipLaunchKernelGGL(k_reset<G_>, dim3(n), dim3(256), lb, s, K, (uint8_t*)records, n, (const uint8_t*)bank, n_bank, mask, \
-                     bank_idx, bank_offset, frames, n_frames)
+  hipLaunchKernelGGL(k_reset<G_>, dim3(grid), dim3(256), lb, s, K, (uint8_t*)records, n, (const uint8_t*)bank, n_bank,  \
+                     mask, bank_idx, bank_offset, frames, n_frames)
   switch (c->P.size) {
     case 64: CBEV_LAUNCH_RESET(1); break;
     case 128: CBEV_LAUNCH_RESET(2); break;
