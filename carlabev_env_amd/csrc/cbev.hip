@@ -1595,10 +1595,16 @@ struct cbev_ctx {
 
 // envs per workgroup for a staged kernel: the largest divisor of 64 whose
 // records fit the LDS budget
+// Envs per workgroup for a staged kernel: small groups spread the record
+// staging (LDS-DMA throughput is per CU) and the chains over more CUs; the
+// largest divisor of 64 not above CBEV_STAGED_NE (default 8) whose records fit
+// the LDS budget.
 static int staged_ne(int sbytes) {
   const int budget = 128 * 1024;
-  int ne = 64;
-  while (ne > 1 && ne * sbytes > budget) ne >>= 1;
+  const char* v = getenv("CBEV_STAGED_NE");
+  int ne = v ? atoi(v) : 16;
+  ne = ne >= 64 ? 64 : ne >= 32 ? 32 : ne >= 16 ? 16 : ne >= 8 ? 8 : 4;
+  while (ne > 4 && ne * sbytes > budget) ne >>= 1;
   return ne;
 }
 
