@@ -171,7 +171,8 @@ __device__ __forceinline__ int d_target_index_serial(double x, double y, double 
   // smallest one; hypot is evaluated only for those candidates (almost always
   // exactly one), in index order, with the reference's strict '<'.
   double m2 = INFINITY;
-  for (int i = 0; i < n; ++i) {
+#pragma unroll 8
+  for (int i = 0; i < n; ++i) {  // unrolled: 8 route points' loads in flight
     const double dx = fx - cx[i], dy = fy - cy[i];
     const double d2 = dx * dx + dy * dy;
     m2 = d2 < m2 ? d2 : m2;
@@ -180,6 +181,7 @@ __device__ __forceinline__ int d_target_index_serial(double x, double y, double 
   int best = 0;
   double bd = 0.0;
   bool first = true;
+#pragma unroll 8
   for (int i = 0; i < n; ++i) {
     const double dx = fx - cx[i], dy = fy - cy[i];
     if (!(dx * dx + dy * dy <= lim)) continue;
