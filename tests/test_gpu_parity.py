@@ -58,9 +58,11 @@ def compare_records(a: np.ndarray, b: np.ndarray, layout, tag=""):
 
 
 def run_parity(kinds, n_envs, steps, size=128, profile="discrete9_v1", reward="carl_base_v1", seed0=0, anchor_y=0.5,
-               act_seed=1234):
+               act_seed=1234, edit=None):
     cfg, P, padded, layout, builder = world(size, profile, reward, anchor_y)
     recs, _ = build_records(builder, n_envs, kinds, seed0=seed0)
+    if edit is not None:  # hand-made states on top of the seeded scenes
+        edit(recs, layout, P)
     dw = DevWorld(P, padded, CAPS_FULL)
     L = lib()
     S = P.size
@@ -119,6 +121,33 @@ def test_parity_scenarios_size256_config5():
 
 def test_parity_shaping_reward_and_offcentre_anchor():
     run_parity(["rt_easy_v1", "jaywalk"], 16, 80, reward="shaping_base_v1", anchor_y=0.2, seed0=5)
+
+
+def _edge_states(recs, layout, P):
+    """One env per branch the seeded rollouts rarely reach."""
+    V = [LY.RecordView(recs[e], layout) for e in range(recs.shape[0])]
+    X, Y, YAW, VEL = (LY.HD[k] for k in ("X", "Y", "YAW", "V"))
+    V[1].hd[X] += 40.0  # off the road: NON_DRIVABLE tile (collision) or sidewalk
+    V[2].hd[X], V[2].hd[Y] = V[2].hd[LY.HD["GOAL_X"]], V[2].hd[LY.HD["GOAL_Y"]]  # on the goal: success
+    V[3].hd[X] += 120.0  # far from the route: out of bounds or off-road
+    V[4].hd[VEL] = 60.0  # over the CaRL speed limit, brake/clip paths
+    if V[5].i("NACT") > 0:  # on an actor: vehicle / pedestrian collision
+        V[5].hd[X], V[5].hd[Y] = V[5].ad[LY.AD["X"], 0], V[5].ad[LY.AD["Y"], 0]
+    V[6].hd[YAW], V[6].hd[VEL] = -np.pi / 2, 0.0  # exact multiple of 90 degrees: rotate90 in the step raster
+    V[7].hd[YAW] = np.pi  # yaw at the angle_mod wrap
+    V[8].hd[VEL] = -3.0  # reversing
+    V[9].hd[X] = 3.0  # at the map's left edge: crop clamped against the padding
+
+
+def test_parity_edge_states_carl():
+    run_parity(["rt_medium_v1"], 10, 6, seed0=777, edit=_edge_states)
+
+
+def test_parity_edge_states_shaping_and_truncation():
+    def edit(recs, layout, P):
+        _edge_states(recs, layout, P)
+        LY.RecordView(recs[0], layout).hi[LY.HI["KSTEPS"]] = P.max_actions - 2  # truncation on step 2
+    run_parity(["rt_easy_v1"], 10, 4, reward="shaping_base_v1", seed0=4242, edit=edit)
 
 
 def test_bank_reset_and_wrapper_expansion():
