@@ -1268,7 +1268,10 @@ __device__ __forceinline__ void collide_env(const KArgs& K, DRec r, int e, const
       RC = d_clip(RC * 100, 0.0, 1.0);
       double d2r = d_lateral_error(x, y, r.cx + tidx, r.cy + tidx, nw);
       double dist_m = fabs(d2r) * CB_MPP;
-      double p_route = dist_m <= 0.0 ? 1.0 : d_pymax(P.lane_center_floor, 1.0 - pow(dist_m / 3.0, P.lane_center_exponent));
+      // pow(x, 1.0) is exactly x (IEEE 754 / C99 F.9.4.4); skip the log/exp of the general pow
+      const double lx = dist_m / 3.0;
+      const double lp = P.lane_center_exponent == 1.0 ? lx : pow(lx, P.lane_center_exponent);
+      double p_route = dist_m <= 0.0 ? 1.0 : d_pymax(P.lane_center_floor, 1.0 - lp);
       bool off_lane = (tile == 2) || (dist_m > (1.5 * 3.0));
       double p_off = off_lane ? P.off_lane_penalty : 1.0;
       double speed_mps = v * CB_MPP;
