@@ -48,6 +48,10 @@ def lib():
     L.cbev_step.restype = _I
     L.cbev_reset.argtypes = [_P, _P, _I, _P, _I, _P, _P, _I, _P, _I, _P]
     L.cbev_reset.restype = _I
+    L.cbev_bank_frames.argtypes = [_P, _P, _I, _P, _P]
+    L.cbev_bank_frames.restype = _I
+    L.cbev_reset_frames.argtypes = [_P, _P, _I, _P, _I, _P, _P, _I, _P, _P, _I, _P]
+    L.cbev_reset_frames.restype = _I
     L.cbev_expand_obs.argtypes = [_P, _P, _I, _I, _I, _I, _I, _P, _P, _P]
     L.cbev_expand_obs.restype = _I
     L.cbev_profile.argtypes = [_P, _I]
@@ -65,5 +69,6 @@ def check(rc: int, what: str = "cbev call"):
 
 
 EXPORTED_SYMBOLS = ("cbev_abi_version", "cbev_params_size", "cbev_layout_of", "cbev_field_names", "cbev_last_error",
-                    "cbev_create", "cbev_destroy", "cbev_set_map", "cbev_step", "cbev_reset",
+                    "cbev_create", "cbev_destroy", "cbev_set_map", "cbev_step", "cbev_reset", "cbev_bank_frames",
+                    "cbev_reset_frames",
                     "cbev_expand_obs", "cbev_profile", "cbev_profile_read")

@@ -1094,6 +1094,55 @@ __global__ __launch_bounds__(256) void k_reset(KArgs K, uint8_t* __restrict__ re
   }
 }
 
+// Reset observations of a static scene bank, rendered once (BaseMap.reset draws
+// no actors, world.py:92-100, so the frame depends only on the bank record):
+// frames[b] = reset render of bank[b].
+template <int G>
+__global__ __launch_bounds__(256) void k_bank_frames(KArgs K, const uint8_t* __restrict__ bank, int n_bank,
+                                                     uint8_t* __restrict__ frames) {
+  extern __shared__ __align__(16) uint8_t lds[];
+  const int64_t SS = (int64_t)K.P.size * K.P.size;
+  for (int b = blockIdx.x; b < n_bank; b += gridDim.x) {
+    DRec r = bind_rec((uint8_t*)bank + (int64_t)b * K.L.record_bytes, K.L, K.C);
+    raster_env<true, G>(K, r, frames + b * SS, 1, 0, lds);
+    __syncthreads();
+  }
+}
+
+// Partial reset from a bank with cached reset frames: records[e] <- bank[b] and
+// bank_frames[b] into every frame-stack slot of env e, for the envs selected by
+// mask. Pure copies (16-byte), strided over a RESET_WGS grid like k_reset.
+__global__ __launch_bounds__(256) void k_reset_copy(KArgs K, uint8_t* __restrict__ recs, int n,
+                                                    const uint8_t* __restrict__ bank, int n_bank,
+                                                    const uint8_t* __restrict__ mask,
+                                                    const int32_t* __restrict__ bank_idx, int bank_offset,
+                                                    const uint8_t* __restrict__ bank_frames,
+                                                    uint8_t* __restrict__ ring, int n_frames) {
+  const int64_t rb = K.L.record_bytes;
+  const int64_t SS = (int64_t)K.P.size * K.P.size;
+  const int lane = threadIdx.x & 63;
+  for (int p0 = blockIdx.x; p0 < n; p0 += 64 * gridDim.x) {
+    const int pl = p0 + lane * gridDim.x;
+    const bool sel = pl < n && (mask == nullptr || mask[xcd_env_of_wg(pl, n)] != 0);
+    uint64_t todo = __ballot(sel);
+    while (todo) {
+      const int k = __builtin_ctzll(todo);
+      todo &= todo - 1;
+      const int e = xcd_env_of_wg(p0 + k * gridDim.x, n);
+      int b = bank_idx ? bank_idx[e] : (int)(((int64_t)e + bank_offset) % n_bank);
+      b = b < 0 ? 0 : (b >= n_bank ? n_bank - 1 : b);
+      const uint4* s4 = (const uint4*)(bank + (int64_t)b * rb);
+      uint4* d4 = (uint4*)(recs + (int64_t)e * rb);
+      for (int64_t i = threadIdx.x; i < rb / 16; i += 256) d4[i] = s4[i];
+      const uint4* f4 = (const uint4*)(bank_frames + (int64_t)b * SS);
+      for (int64_t i = threadIdx.x; i < SS / 16; i += 256) {
+        const uint4 v = f4[i];
+        for (int f = 0; f < n_frames; ++f) ((uint4*)(ring + ((int64_t)f * n + e) * SS))[i] = v;
+      }
+    }
+  }
+}
+
 // ============================================================== k_collide
 // squared distance from (x, y) to raw-route segment i (carl_reward_fn.py:36-48)
 __device__ __forceinline__ double d_seg_dist2(const DRec& r, int i, double x, double y) {
@@ -1696,6 +1745,10 @@ static KArgs kargs(const cbev_ctx* c) {
 static const void* raster_kernel(int size) {
   return size == 64 ? (const void*)k_raster<1> : size == 128 ? (const void*)k_raster<2> : (const void*)k_raster<4>;
 }
+static const void* bank_frames_kernel(int size) {
+  return size == 64 ? (const void*)k_bank_frames<1> : size == 128 ? (const void*)k_bank_frames<2>
+                                                                   : (const void*)k_bank_frames<4>;
+}
 static const void* reset_kernel(int size) {
   return size == 64 ? (const void*)k_reset<1> : size == 128 ? (const void*)k_reset<2> : (const void*)k_reset<4>;
 }
@@ -1771,6 +1824,9 @@ int cbev_create(const cbev_params* params, const cbev_caps* caps, int device, cb
     e = hipFuncSetAttribute(raster_kernel(P.size), hipFuncAttributeMaxDynamicSharedMemorySize, (int)raster_lds_bytes(P));
   if (e == hipSuccess)
     e = hipFuncSetAttribute(reset_kernel(P.size), hipFuncAttributeMaxDynamicSharedMemorySize, (int)raster_lds_bytes(P));
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute(bank_frames_kernel(P.size), hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)raster_lds_bytes(P));
   if (e != hipSuccess) {
     free(c);
     return set_err(CBEV_EHIP, "cbev_create: %s", hipGetErrorString(e));
@@ -1900,6 +1956,38 @@ int cbev_reset(cbev_ctx* c, void* records, int n, const void* bank, int n_bank, 
     default: CBEV_LAUNCH_RESET(4); break;
   }
 #undef CBEV_LAUNCH_RESET
+  HIP_TRY(hipGetLastError());
+  return CBEV_OK;
+}
+
+int cbev_bank_frames(cbev_ctx* c, const void* bank, int n_bank, uint8_t* frames, void* stream) {
+  if (!c || !bank || !frames) return set_err(CBEV_EINVAL, "null argument");
+  if (!c->map_dev) return set_err(CBEV_ESTATE, "cbev_set_map not called");
+  if (n_bank <= 0) return CBEV_OK;
+  KArgs K = kargs(c);
+  const size_t lb = raster_lds_bytes(c->P);
+  hipStream_t s = (hipStream_t)stream;
+  const int grid = n_bank < RESET_WGS ? n_bank : RESET_WGS;
+  switch (c->P.size) {
+    case 64: hipLaunchKernelGGL(k_bank_frames<1>, dim3(grid), dim3(256), lb, s, K, (const uint8_t*)bank, n_bank, frames); break;
+    case 128: hipLaunchKernelGGL(k_bank_frames<2>, dim3(grid), dim3(256), lb, s, K, (const uint8_t*)bank, n_bank, frames); break;
+    default: hipLaunchKernelGGL(k_bank_frames<4>, dim3(grid), dim3(256), lb, s, K, (const uint8_t*)bank, n_bank, frames); break;
+  }
+  HIP_TRY(hipGetLastError());
+  return CBEV_OK;
+}
+
+int cbev_reset_frames(cbev_ctx* c, void* records, int n, const void* bank, int n_bank, const uint8_t* mask,
+                      const int32_t* bank_idx, int bank_offset, const uint8_t* bank_frames, uint8_t* frames,
+                      int n_frames, void* stream) {
+  if (!c || !records || !bank || !bank_frames || !frames) return set_err(CBEV_EINVAL, "null argument");
+  if (n_bank <= 0) return set_err(CBEV_EINVAL, "empty bank");
+  if (n_frames < 1) return set_err(CBEV_EINVAL, "n_frames < 1");
+  if (n <= 0) return CBEV_OK;
+  KArgs K = kargs(c);
+  const int grid = n < RESET_WGS ? n : RESET_WGS;
+  hipLaunchKernelGGL(k_reset_copy, dim3(grid), dim3(256), 0, (hipStream_t)stream, K, (uint8_t*)records, n,
+                     (const uint8_t*)bank, n_bank, mask, bank_idx, bank_offset, bank_frames, frames, n_frames);
   HIP_TRY(hipGetLastError());
   return CBEV_OK;
 }

@@ -174,6 +174,11 @@ class CarlaBEVVectorEnv:
             raise ValueError("bank must be a (B, record_bytes) uint8 tensor on the env device")
         self.bank = bank_records.contiguous()
         self.bank_contexts = contexts
+        # reset observations of the bank, rendered once; reset_from_bank then only copies
+        B, S = self.bank.shape[0], self.S
+        self.bank_frames = torch.empty((B, S, S), dtype=torch.uint8, device=self.device)
+        check(lib().cbev_bank_frames(self._ctx, _ptr(self.bank), B, _ptr(self.bank_frames), self._stream()),
+              "cbev_bank_frames")
 
     def build_bank(self, seeds, options: dict | None = None) -> torch.Tensor:
         options = dict(options or {})
@@ -194,8 +199,9 @@ class CarlaBEVVectorEnv:
             self._bank_cursor = (self._bank_cursor + N) % B
         if mask is not None and (mask.dtype != torch.uint8 or mask.device != self.device):
             mask = mask.to(device=self.device, dtype=torch.uint8)
-        check(lib().cbev_reset(self._ctx, _ptr(self.records), N, _ptr(self.bank), B, _ptr(mask), _ptr(bank_idx),
-                               offset, _ptr(self.ring), self.F, self._stream()), "cbev_reset")
+        check(lib().cbev_reset_frames(self._ctx, _ptr(self.records), N, _ptr(self.bank), B, _ptr(mask),
+                                      _ptr(bank_idx), offset, _ptr(self.bank_frames), _ptr(self.ring), self.F,
+                                      self._stream()), "cbev_reset_frames")
         return self._obs() if self.auto_obs else None
 
     # ------------------------------------------------------------------ gymnasium surface

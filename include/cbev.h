@@ -74,6 +74,18 @@ int cbev_step(cbev_ctx* ctx, void* records, int n, const void* actions, uint8_t*
 int cbev_reset(cbev_ctx* ctx, void* records, int n, const void* bank, int n_bank, const uint8_t* mask,
                const int32_t* bank_idx, int bank_offset, uint8_t* frames, int n_frames, void* stream);
 
+/* Reset observations of a static scene bank, rendered once: frames = uint8[n_bank][S][S],
+ * frames[b] = the observation cbev_reset would render for bank[b] (BaseMap.reset draws
+ * no actors, world.py:92-100, so it depends on the bank record only). */
+int cbev_bank_frames(cbev_ctx* ctx, const void* bank, int n_bank, uint8_t* frames, void* stream);
+
+/* cbev_reset from a bank whose reset observations were rendered by cbev_bank_frames:
+ * the same records and ring contents as cbev_reset(ctx, records, n, bank, n_bank, mask,
+ * bank_idx, bank_offset, frames, n_frames, stream), by copies only. */
+int cbev_reset_frames(cbev_ctx* ctx, void* records, int n, const void* bank, int n_bank, const uint8_t* mask,
+                      const int32_t* bank_idx, int bank_offset, const uint8_t* bank_frames, uint8_t* frames,
+                      int n_frames, void* stream);
+
 /* Wrapper stack on the device (envs/__init__.py:62-83):
  *   kind 0: semantic one-hot (rgb_to_semantic.py:65-142) + FrameStack + Flatten
  *           -> float32[n][F*C][S][S]; channel_lut[id] = bitmask of channels set

@@ -211,6 +211,36 @@ def test_bank_reset_and_wrapper_expansion():
     assert np.array_equal(rgb.cpu().numpy(), PALETTE[ring_h[head].numpy()])
 
 
+def test_reset_from_cached_bank_frames_matches_render():
+    cfg, P, padded, layout, builder = world()
+    n, B, F = 48, 9, 4
+    recs, _ = build_records(builder, n, ["rt_medium_v1"], seed0=1300)
+    bank, _ = build_records(builder, B, ["rt_hard_v1", "jaywalk", "lead_brake"], seed0=1900)
+    dw = DevWorld(P, padded, CAPS_FULL)
+    L = lib()
+    S = P.size
+    d_bank = torch.from_numpy(bank.copy()).cuda()
+    mask = (torch.arange(n) % 4 != 1).to(torch.uint8).cuda()
+    bidx = ((torch.arange(n) * 7) % B).to(torch.int32).cuda()
+    outs = []
+    for cached in (False, True):
+        d_recs = torch.from_numpy(recs.copy()).cuda()
+        ring = torch.full((F, n, S, S), 13, dtype=torch.uint8, device="cuda")
+        for idx, off in ((bidx, 0), (None, 5)):
+            if cached:
+                bf = torch.zeros((B, S, S), dtype=torch.uint8, device="cuda")
+                check(L.cbev_bank_frames(dw.ctx, ptr(d_bank), B, ptr(bf), None), "bank_frames")
+                check(L.cbev_reset_frames(dw.ctx, ptr(d_recs), n, ptr(d_bank), B, ptr(mask), ptr(idx), off, ptr(bf),
+                                          ptr(ring), F, None), "reset_frames")
+            else:
+                check(L.cbev_reset(dw.ctx, ptr(d_recs), n, ptr(d_bank), B, ptr(mask), ptr(idx), off, ptr(ring), F,
+                                   None), "reset")
+        torch.cuda.synchronize()
+        outs.append((d_recs.cpu().numpy(), ring.cpu().numpy()))
+    assert np.array_equal(outs[0][0], outs[1][0])
+    assert np.array_equal(outs[0][1], outs[1][1])
+
+
 def test_vector_env_surface_and_partial_reset():
     from carlabev_env_amd import EnvConfig, make_env, build_random_navigation_options, RandomNavigationReset
     cfg = EnvConfig(size=128, obs_size=(128, 128), render_mode="rgb_array", obs_mode="bev_semantic")
