@@ -420,6 +420,7 @@ __device__ __forceinline__ int xcd_env4_of_wg(int w, int wave, int n) {
 __device__ unsigned long long g_stamps[6][4096][4];
 __device__ unsigned long long g_rtstamps[6][4096][4];  // s_memrealtime (constant 100 MHz)
 __device__ unsigned g_xcc[6][4096];                    // XCC (XCD) the workgroup ran on
+__device__ unsigned g_hwid[6][4096];                   // HW_ID (SE / SH / CU / SIMD) of its wave 0
 #define CBEV_STAMP(kern, slot)                                                  \
   if (threadIdx.x == 0 && blockIdx.x < 4096) {                                  \
     g_stamps[kern][blockIdx.x][slot] = __builtin_amdgcn_s_memtime();            \
@@ -427,6 +428,8 @@ __device__ unsigned g_xcc[6][4096];                    // XCC (XCD) the workgrou
     unsigned xcc_;                                                              \
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc_));         \
     g_xcc[kern][blockIdx.x] = xcc_;                                             \
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(xcc_));          \
+    g_hwid[kern][blockIdx.x] = xcc_;                                            \
   }
 #else
 #define CBEV_STAMP(kern, slot)
@@ -542,34 +545,21 @@ struct HeroPre {
   double cyaw, syaw, tdelta;
 };
 
-// Ego update, part A (one thread per env): target search reduction, throttle /
+// Ego update, part A (one thread per env): target index update, throttle /
 // brake, State.update, damping (BaseAgent.physics_step, hero.py:88-138).
 __device__ __forceinline__ void hero_env_a(const KArgs& K, DRec r, int e, const void* __restrict__ actions,
-                                           const double* __restrict__ route_dist, const HeroPre& hp) {
+                                           int bi, const HeroPre& hp) {
   double* hd = r.hd;
   int32_t* hi = r.hi;
   float g, sa, b;
   d_decode_action(K, actions, e, &g, &sa, &b);
   hd[CBEV_HD_T] += CB_DT;  // Scene._t += dt (scene.py:91)
-  CBEV_STAMP(3, 0);
 
   double s[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) s[k] = hd[CBEV_HD_X + k];
-  // stanley_control's target search (first arg-min of the precomputed hypots);
+  // stanley_control's target search (bi: first arg-min, reduced by the workgroup);
   // its steering output is unused by the hero
-  int bi = 0;
-  {
-    const int nr = hi[CBEV_HI_NROUTE];
-    double bd = 0.0;
-    for (int i = 0; i < nr; ++i) {
-      const double d = route_dist[i];
-      if (i == 0 || d < bd) {
-        bd = d;
-        bi = i;
-      }
-    }
-  }
   hi[CBEV_HI_TIDX] = hi[CBEV_HI_TIDX] >= bi ? hi[CBEV_HI_TIDX] : bi;
   const double v = s[3];
   const int scale = K.P.scale;
@@ -603,7 +593,6 @@ __device__ __forceinline__ void hero_env_a(const KArgs& K, DRec r, int e, const 
   hd[CBEV_HD_U_STEER] = (double)sa;
   hd[CBEV_HD_U_BRAKE] = (double)b;
   hd[CBEV_HD_U_DELTA] = delta;
-  CBEV_STAMP(3, 1);
 }
 
 // Ego update, part B1: compute_comfort_kinematics (comfort.py:17-61) and the
@@ -634,7 +623,6 @@ __device__ __forceinline__ void hero_env_comfort(DRec r) {
   hd[CBEV_HD_D2G_T1] = hd[CBEV_HD_D2G];
   const double gx = x - hd[CBEV_HD_GOAL_X], gy = y - hd[CBEV_HD_GOAL_Y];
   hd[CBEV_HD_D2G] = sqrt(gx * gx + gy * gy);
-  CBEV_STAMP(3, 2);
 }
 
 // Ego update, part B2: render set-up of this step's observation (crop origin +
@@ -642,7 +630,6 @@ __device__ __forceinline__ void hero_env_comfort(DRec r) {
 __device__ __forceinline__ void hero_env_render_setup(const KArgs& K, DRec r) {
   const double* hd = r.hd;
   d_store_render_setup(K.P, r.hi, hd[CBEV_HD_X], hd[CBEV_HD_Y], (float)(d_degrees(hd[CBEV_HD_YAW]) + 90));
-  CBEV_STAMP(3, 3);
 }
 
 __global__ __launch_bounds__(256) void k_hero(KArgs K, uint8_t* __restrict__ recs, int n,
@@ -652,10 +639,10 @@ __global__ __launch_bounds__(256) void k_hero(KArgs K, uint8_t* __restrict__ rec
   const int ne_eff = min(ne, n - e0);
   if (ne_eff <= 0) return;
   const int64_t rb = K.L.record_bytes;
-  const int R = K.C.route_cap, tid = threadIdx.x;
+  const int tid = threadIdx.x;
   const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  double* dist = (double*)(lds + ne * sbytes);  // [ne][R] hypot(front axle - route point), +inf off-candidate
-  HeroPre* pre = (HeroPre*)(dist + ne * R);      // [ne]
+  HeroPre* pre = (HeroPre*)(lds + ne * sbytes);  // [ne]
+  int* best = (int*)(pre + ne);                   // [ne] Stanley target search result
   CBEV_STAMP(0, 0);
   stage_in(lds, recs, e0, ne_eff, rb, sbytes);
   __syncthreads();
@@ -675,6 +662,7 @@ __global__ __launch_bounds__(256) void k_hero(KArgs K, uint8_t* __restrict__ rec
     }
   }
   __syncthreads();
+  CBEV_STAMP(3, 0);
   // P2: Controller.calc_target_index (stanley_controller.py:51-62) on the
   // pre-update state, over (env, route point) pairs, env k = tid / tpe. The
   // squared distance is within a few ulp of hypot^2, so only points within
@@ -703,18 +691,35 @@ __global__ __launch_bounds__(256) void k_hero(KArgs K, uint8_t* __restrict__ rec
         m2 = t < m2 ? t : m2;
       }
       const double lim = m2 * (1.0 + 1e-14);
+      double bd = INFINITY;
+      int bi = 0x7fffffff;
       for (int i = sub; i < nr; i += tpe) {
         const double dx = fx - cx[i], dy = fy - cy[i];
-        double d = INFINITY;
-        if (dx * dx + dy * dy <= lim) d = hypot(dx, dy);
-        dist[k * R + i] = d;
+        if (dx * dx + dy * dy <= lim) {
+          const double h = hypot(dx, dy);
+          if (h < bd) {  // first minimum within this thread's (increasing) indices
+            bd = h;
+            bi = i;
+          }
+        }
       }
+      for (int o = tpe >> 1; o > 0; o >>= 1) {  // smallest hypot, lowest index on ties
+        const double qd = __shfl_xor(bd, o, tpe);
+        const int qi = __shfl_xor(bi, o, tpe);
+        if (qd < bd || (qd == bd && qi < bi)) {
+          bd = qd;
+          bi = qi;
+        }
+      }
+      if (sub == 0) best[k] = bi == 0x7fffffff ? 0 : bi;
     }
   }
   __syncthreads();
+  CBEV_STAMP(3, 1);
   // A: the scalar chain, one thread per env
-  if (tid < ne_eff) hero_env_a(K, bind_rec(lds + tid * sbytes, K.L, K.C), e0 + tid, actions, dist + tid * R, pre[tid]);
+  if (tid < ne_eff) hero_env_a(K, bind_rec(lds + tid * sbytes, K.L, K.C), e0 + tid, actions, best[tid], pre[tid]);
   __syncthreads();
+  CBEV_STAMP(3, 2);
   // B: comfort + dist2goal (wave 1) beside the render set-up (wave 2)
   if (lane < ne_eff) {
     if (wave == 1) hero_env_comfort(bind_rec(lds + lane * sbytes, K.L, K.C));
@@ -722,6 +727,7 @@ __global__ __launch_bounds__(256) void k_hero(KArgs K, uint8_t* __restrict__ rec
   }
   CBEV_STAMP(0, 2);
   __syncthreads();
+  CBEV_STAMP(3, 3);
   stage_out(lds, recs, e0, ne_eff, rb, sbytes, 0, (int)K.L.cx);  // HD + HI
   CBEV_STAMP(0, 3);
 }
@@ -740,13 +746,15 @@ __global__ __launch_bounds__(256) void k_actors(KArgs K, uint8_t* __restrict__ r
   for (int a = lane; a < nact; a += 64) d_actor_step(r, a, t);
 }
 
-// Output pass over one wave's chunks of 1024 output pixels: gather j (0..15) of
-// a chunk has lane l sample output pixel (row r0 + j / G, column 64 (j % G) + l),
-// so a gather walks 64 consecutive pixels of one output row (consecutive lanes
-// read neighbouring source pixels: few distinct LDS dwords, spread banks) and
-// its byte store is a contiguous 64-byte run. Source coordinates are stepped,
-// not recomputed: per gather two adds, a shift/multiply-add for the LDS byte
-// address, the LDS read and the store.
+// Output pass over one wave's chunks of 1024 output pixels (16 / G rows). A
+// chunk is four 256-pixel dword groups: in group d lane l owns the 4
+// consecutive output pixels 256 d + 4 l .. + 3 of the chunk (row r + d (4 / G)
+// + l / (16 G), columns 4 (l % (16 G)) .. + 3), gathers them one column step
+// apart and packs them into one dword, so each group is ONE 256-byte dword
+// store. Source coordinates are stepped, not recomputed (pygame's rotozoom is
+// affine in the output pixel): per gather one 64-bit add, a 24-bit
+// multiply-add for the LDS byte address, the LDS read, the nibble extract and
+// the pack.
 //   CHECK = false: the rotated surface covers the whole output and every output
 //   pixel samples inside the crop (checked once per env at the four corners;
 //   the map is affine) -> no per-pixel tests.
@@ -758,22 +766,27 @@ __device__ __forceinline__ void raster_out(const cbev_params& P, const RotSetup&
                                            int64_t out_stride, int lane, int wave) {
   constexpr int RPC = 16 / G;  // output rows per chunk
   constexpr int S = 64 * G;    // == P.size
+  constexpr int LPR = S / 4;   // lanes per output row
+  constexpr int RPD = 4 / G;   // output rows per dword group
   const int C = P.crop;
   const uint32_t vmax = (uint32_t)((C << 16) - 1);
   const int hero_w = P.hero_w;
   const int hx0 = P.anchor_x - hero_w / 2, hy0 = P.anchor_y - hero_w / 2;
-  // per-lane hero columns (Hero.draw: black w x w rect at the anchor, hero.py:26-32)
-  uint32_t hcol = 0, xok = 0;
+  const int lrow = lane / LPR, lcol = 4 * (lane % LPR);
+  // this lane's columns: hero byte mask (Hero.draw: black w x w rect at the
+  // anchor, hero.py:26-32) and the compose-clip column test
+  uint32_t hmask = 0, xok = 0;
 #pragma unroll
-  for (int cj = 0; cj < G; ++cj) {
-    const int u = 64 * cj + lane;
-    if (u >= hx0 && u < hx0 + hero_w) hcol |= 1u << cj;
+  for (int b = 0; b < 4; ++b) {
+    const int u = lcol + b;
+    if (u >= hx0 && u < hx0 + hero_w) hmask |= 0xffu << (8 * b);
     const int xx = u - R.rx0;
-    if (xx >= 0 && xx < R.nx) xok |= 1u << cj;
+    if (xx >= 0 && xx < R.nx) xok |= 1u << b;
   }
+  const uint32_t hblack = hmask & (CBEV_PX_BLACK * 0x01010101u);
   const int r0 = wave * RPC;
-  const int xx0 = lane - R.rx0, yy0 = r0 - R.ry0;
-  // lane state at (output column lane, output row r0 of this wave's first chunk)
+  const int xx0 = lcol - R.rx0, yy0 = r0 + lrow - R.ry0;
+  // lane state at (output row r0 + lrow, column lcol) of this wave's first chunk
   int sx = R.dx00 + xx0 * R.icos - yy0 * R.isin;  // 16.16 source x (general)
   int sy = R.dy00 + xx0 * R.isin + yy0 * R.icos;  // 16.16 source y (general)
   int sa = R.a00 + shift + xx0 * R.ustep + yy0 * R.vstep;  // LDS nibble address (rotate90)
@@ -789,66 +802,64 @@ __device__ __forceinline__ void raster_out(const cbev_params& P, const RotSetup&
   uint64_t pxy = ((uint64_t)(uint32_t)sy << 32) | (uint32_t)sx;
   const uint64_t chunk_step =
       (uint64_t)(((int64_t)(chunk_rows * R.icos) << 32) + (int64_t)(-chunk_rows * R.isin));
-  // one output row down: (dx, dy) += (-isin, icos); 64 columns right: += 64 (icos, isin)
-  const uint64_t row_step = (uint64_t)(((int64_t)R.icos << 32) + (int64_t)(-R.isin));
-  const uint64_t col_step = (uint64_t)(((int64_t)(64 * R.isin) << 32) + (int64_t)(64 * R.icos));
+  // one output row down: (dx, dy) += (-isin, icos); one column right: += (icos, isin)
+  const uint64_t group_step = (uint64_t)(((int64_t)(RPD * R.icos) << 32) + (int64_t)(-RPD * R.isin));
+  const uint64_t col_step = (uint64_t)(((int64_t)R.isin << 32) + (int64_t)R.icos);
   for (int ch = wave, r = r0; ch < nchunks; ch += 4, r += chunk_rows) {
     // the frame is written through the uniform base `out` plus a per-lane offset
-    const uint32_t vo = (uint32_t)(r * S + lane);
+    const uint32_t vo = (uint32_t)(r * S + 4 * lane);
     const bool hero_rows = (unsigned)(r + RPC - 1 - hy0) < (unsigned)(RPC - 1 + hero_w);  // chunk meets the hero rows
     asm volatile("" : "+v"(pxy), "+v"(sa));  // keep the per-gather offsets as scalar adds
-    uint32_t px[16];
-    uint64_t qrow = pxy;  // general path: source coordinates of (row r + rj, column lane)
+    uint32_t w[4];
+    uint64_t qg = pxy;  // general path: source coordinates of (row r + d RPD + lrow, column lcol)
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const int rj = j / G, cj = j % G;
-      uint32_t v;
-      if (R90) {
-        const int a = sa + rj * R.vstep + 64 * cj * R.ustep;
-        if (CHECK) {
-          const bool ok = ((xok >> cj) & 1u) && (unsigned)(r + rj - R.ry0) < (unsigned)R.ny;
-          v = ok ? lds_nib(img, ok ? a : 0) : (uint32_t)CBEV_PX_BLACK;
+    for (int d = 0; d < 4; ++d) {
+      uint32_t acc = 0;
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        uint32_t v;
+        if (R90) {
+          const int a = sa + d * RPD * R.vstep + b * R.ustep;
+          if (CHECK) {
+            const bool ok = ((xok >> b) & 1u) && (unsigned)(r + d * RPD + lrow - R.ry0) < (unsigned)R.ny;
+            v = ok ? lds_nib(img, ok ? a : 0) : (uint32_t)CBEV_PX_BLACK;
+          } else {
+            v = lds_nib(img, a);
+          }
         } else {
-          v = lds_nib(img, a);
+          const uint64_t q = b == 0 ? qg : qg + (uint64_t)b * col_step;
+          const uint32_t dx = (uint32_t)q, dy = (uint32_t)(q >> 32);
+          const uint32_t byte = __umul24(dy >> 16, sb) + (dx >> 17);
+          const uint32_t nsh = (dx >> 14) & 4u;
+          if (CHECK) {  // bounds on the unshifted source coordinate
+            const int ux = (int)dx - (shift << 16);
+            const bool ok = ((xok >> b) & 1u) && (unsigned)(r + d * RPD + lrow - R.ry0) < (unsigned)R.ny;
+            const bool in = (uint32_t)ux <= vmax && dy <= vmax;
+            const uint32_t s = (img[(in && ok) ? byte : 0u] >> nsh) & 15u;
+            v = !ok ? (uint32_t)CBEV_PX_BLACK : (in ? s : bg);
+          } else {
+            v = (img[byte] >> nsh) & 15u;
+          }
         }
-      } else {
-        // one 64-bit add per gather: column blocks step by col_step, rows by row_step
-        const uint64_t q = cj == 0 ? qrow : qrow + (uint64_t)cj * col_step;
-        if (cj == G - 1) qrow += row_step;
-        const uint32_t dx = (uint32_t)q, dy = (uint32_t)(q >> 32);
-        const uint32_t byte = __umul24(dy >> 16, sb) + (dx >> 17);
-        const uint32_t nsh = (dx >> 14) & 4u;
-        if (CHECK) {  // bounds on the unshifted source coordinate
-          const int ux = (int)dx - (shift << 16);
-          const bool ok = ((xok >> cj) & 1u) && (unsigned)(r + rj - R.ry0) < (unsigned)R.ny;
-          const bool in = (uint32_t)ux <= vmax && dy <= vmax;
-          const uint32_t s = (img[(in && ok) ? byte : 0u] >> nsh) & 15u;
-          v = !ok ? (uint32_t)CBEV_PX_BLACK : (in ? s : bg);
-        } else {
-          v = (img[byte] >> nsh) & 15u;
-        }
+        acc |= ((CBEV_RASTER_PHASES & 4) ? v : (uint32_t)(lane + b)) << (8 * b);
       }
-      px[j] = (CBEV_RASTER_PHASES & 4) ? v : (uint32_t)(lane + j);
+      w[d] = acc;
+      if (!R90) qg += group_step;
     }
     if (hero_rows) {
 #pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        const int rj = j / G, cj = j % G;
-        if ((unsigned)(r + rj - hy0) < (unsigned)hero_w && ((hcol >> cj) & 1u)) px[j] = CBEV_PX_BLACK;
-      }
+      for (int d = 0; d < 4; ++d)
+        if ((unsigned)(r + d * RPD + lrow - hy0) < (unsigned)hero_w) w[d] = (w[d] & ~hmask) | hblack;
     }
     if (CBEV_RASTER_PHASES & 8) {
       for (int k = 0; k < nout; ++k) {
         uint8_t* ob = out + (int64_t)k * out_stride;
 #pragma unroll
-        for (int j = 0; j < 16; ++j)  // streamed out: keep the L2 for the map and the records
-          __builtin_nontemporal_store((uint8_t)px[j], ob + (vo + (uint32_t)((j / G) * S + 64 * (j % G))));
+        for (int d = 0; d < 4; ++d)  // streamed out: keep the L2 for the map and the records
+          __builtin_nontemporal_store(w[d], (uint32_t*)(ob + (vo + (uint32_t)(256 * d))));
       }
     } else {
-      uint32_t acc = 0;
-#pragma unroll
-      for (int j = 0; j < 16; ++j) acc += px[j];
-      if (acc == 0x7fffffffu) out[vo] = 1;  // keeps the gathers live
+      if ((w[0] ^ w[1] ^ w[2] ^ w[3]) == 0x7fffffffu) out[vo] = 1;  // keeps the gathers live
     }
     pxy += chunk_step;
     sa += chunk_rows * R.vstep;
@@ -1803,7 +1814,7 @@ int cbev_create(const cbev_params* params, const cbev_caps* caps, int device, cb
   c->device = device;
   c->hero_sb = (int)c->L.raw_x;  // HD, HI, ego route cx / cy / cyaw
   c->coll_sb = (int)c->L.acx;    // ... + raw route, visibility, actor AD / AI groups
-  c->hero_ne = staged_ne(c->hero_sb + 8 * c->C.route_cap + 32);
+  c->hero_ne = staged_ne(c->hero_sb + 32);
   c->coll_scr = coll_scratch_layout(c->C, c->L.vis_words).bytes;
   c->coll_ne = staged_ne(c->coll_sb + c->coll_scr);
   if (c->coll_ne * (c->coll_sb + c->coll_scr) > 160 * 1024 || c->hero_ne < 4 || c->coll_ne < 4) {
@@ -1816,7 +1827,7 @@ int cbev_create(const cbev_params* params, const cbev_caps* caps, int device, cb
   if (e == hipSuccess) e = hipMalloc(&c->lut_dev, 64 * sizeof(uint32_t));
   if (e == hipSuccess)
     e = hipFuncSetAttribute((const void*)k_hero, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            c->hero_ne * (c->hero_sb + 8 * c->C.route_cap + 32));
+                            c->hero_ne * (c->hero_sb + 32));
   if (e == hipSuccess)
     e = hipFuncSetAttribute((const void*)k_collide, hipFuncAttributeMaxDynamicSharedMemorySize,
                             c->coll_ne * (c->coll_sb + c->coll_scr));
@@ -1915,7 +1926,7 @@ int cbev_step(cbev_ctx* c, void* records, int n, const void* actions, uint8_t* f
   if (c->prof_on && c->prof_n < CBEV_PROF_MAX) ev = c->prof_ev + 4 * c->prof_n++;
   if (ev) HIP_TRY(hipEventRecord(ev[0], s));
   hipLaunchKernelGGL(k_hero, dim3((n + c->hero_ne - 1) / c->hero_ne), dim3(256),
-                     (size_t)c->hero_ne * (c->hero_sb + 8 * c->C.route_cap + 32), s, K,
+                     (size_t)c->hero_ne * (c->hero_sb + 32), s, K,
                      (uint8_t*)records, n, actions, c->hero_ne, c->hero_sb);
   if (c->C.actor_cap > 0) hipLaunchKernelGGL(k_actors, dim3(wg4), dim3(256), 0, s, K, (uint8_t*)records, n);
   if (ev) HIP_TRY(hipEventRecord(ev[1], s));
@@ -2016,14 +2027,24 @@ int cbev_expand_obs(cbev_ctx* c, const uint8_t* ring, int n, int n_frames, int h
 }
 
 #ifdef CBEV_TIMING
-// timing builds only: copy the phase stamps [6][4096][4] (u64 s_memtime ticks), realtime stamps, XCC ids
+// timing builds only: copy the phase stamps [6][4096][4] (u64 s_memtime ticks), realtime stamps,
+// XCC ids | HW_ID << 32
 int cbev_debug_times(unsigned long long* out_host) {
   if (hipMemcpyFromSymbol(out_host, HIP_SYMBOL(g_stamps), sizeof(g_stamps)) != hipSuccess) return -1;
   if (hipMemcpyFromSymbol(out_host + 6 * 4096 * 4, HIP_SYMBOL(g_rtstamps), sizeof(g_rtstamps)) != hipSuccess) return -1;
   static unsigned x[6 * 4096];
   if (hipMemcpyFromSymbol(x, HIP_SYMBOL(g_xcc), sizeof(x)) != hipSuccess) return -1;
-  for (int i = 0; i < 6 * 4096; ++i) out_host[12 * 4096 * 4 + i] = x[i];
+  static unsigned h[6 * 4096];
+  if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_hwid), sizeof(h)) != hipSuccess) return -1;
+  for (int i = 0; i < 6 * 4096; ++i) out_host[12 * 4096 * 4 + i] = x[i] | ((unsigned long long)h[i] << 32);
   return 0;
+}
+
+// timing builds only: hipOccupancyMaxActiveBlocksPerMultiprocessor of the raster kernel for `size`
+int cbev_debug_occupancy(int size, int lds_bytes) {
+  int occ = -1;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, raster_kernel(size), 256, lds_bytes) != hipSuccess) return -1;
+  return occ;
 }
 #endif
 }  // extern "C"

@@ -38,14 +38,19 @@ env, host = bench.build_env(cfgd, n, 0, torch.device("cuda", 0))
 acts = torch.from_numpy(bench.make_actions(env.params, n, a.steps, cfgd["act_seed"], 0)).cuda()
 L = lib()
 L.cbev_debug_times.argtypes = [ctypes.c_void_p]
+L.cbev_debug_occupancy.argtypes = [ctypes.c_int, ctypes.c_int]
+for b in (19656, 20480, 20481):
+    print(f"raster occupancy API (size {cfgd['size']}, {b} B LDS): {L.cbev_debug_occupancy(cfgd['size'], b)} WGs/CU")
 for t in range(a.steps):
     env.step_async_only(acts[t])
 torch.cuda.synchronize()
 buf = np.zeros(2 * 6 * 4096 * 4 + 6 * 4096, np.uint64)
 assert L.cbev_debug_times(buf.ctypes.data_as(ctypes.c_void_p)) == 0
 xcc = buf[2 * 6 * 4096 * 4:].reshape(6, 4096).astype(np.int64)
+hwid = xcc >> 32
+xcc = xcc & 0xFFFFFFFF
 buf = buf[:2 * 6 * 4096 * 4].reshape(2, 6, 4096, 4)
-for k, name in enumerate(("k_hero", "k_collide", "k_raster", "hero_env(thread0)", "collide_env(thread0)", "k_collide pre-pass: segs/targets/actors+sync")):
+for k, name in enumerate(("k_hero", "k_collide", "k_raster", "k_hero after P1 / P2 / A / B (slots 0-3)", "collide_env(thread0)", "k_collide pre-pass: segs/targets/actors+sync")):
     if not (buf[0, k, :, 0] > 0).any():
         continue
     st = buf[0, k].astype(np.int64)
@@ -62,6 +67,21 @@ for k, name in enumerate(("k_hero", "k_collide", "k_raster", "hero_env(thread0)"
     idx = np.flatnonzero(used)
     xs = xcc[k][used] & 0xF
     print(f"   XCC id: workgroups with xcc == w % 8: {(xs == (idx % 8)).mean() * 100:.1f}%; first 16: {list(xs[:16])}")
+    # residency: workgroups live at once on one CU (XCC, SE, SH, CU from HW_ID), from the realtime stamps
+    hw = hwid[k][used]
+    cu = (xs << 16) | (((hw >> 13) & 7) << 8) | (((hw >> 12) & 1) << 4) | ((hw >> 8) & 15)
+    peak = []
+    for c in np.unique(cu):
+        m = cu == c
+        ev = sorted([(t, 1) for t in rt[m, 0]] + [(t, -1) for t in rt[m, 3]], key=lambda z: (z[0], z[1]))
+        live = best = 0
+        for _, dlt in ev:
+            live += dlt
+            best = max(best, live)
+        peak.append((best, m.sum()))
+    peak = np.array(peak)
+    print(f"   CUs used {len(peak)}; WGs per CU mean {peak[:, 1].mean():.1f} (max {peak[:, 1].max()}); "
+          f"peak resident WGs per CU mean {peak[:, 0].mean():.2f} (min {peak[:, 0].min()}, max {peak[:, 0].max()})")
     for x in range(8):  # s_memtime is per XCD: spans within one XCD (workgroup w runs on XCD w % 8)
         m = (idx % 8) == x
         if m.any():
