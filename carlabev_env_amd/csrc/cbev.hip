@@ -30,6 +30,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <string>
 #include <vector>
 
@@ -1578,63 +1579,262 @@ __global__ __launch_bounds__(256) void k_collide(KArgs K, uint8_t* __restrict__ 
 }
 
 // ============================================================== reset / ring / expansion
-// semantic one-hot + frame stack + flatten: out[e][f*C + c][p] (rgb_to_semantic.py:65-142,256-272)
-__global__ __launch_bounds__(256) void k_expand_semantic(const uint8_t* __restrict__ ring, int n, int F, int head, int C,
-                                                         int SS, const uint32_t* __restrict__ lut,
-                                                         float* __restrict__ out) {
-  const int64_t total4 = (int64_t)n * F * (SS / 4);
-  for (int64_t q = blockIdx.x * 256ll + threadIdx.x; q < total4; q += (int64_t)gridDim.x * 256) {
-    const int64_t p4 = q % (SS / 4);
-    const int64_t ef = q / (SS / 4);
-    const int f = (int)(ef % F);
-    const int64_t e = ef / F;
-    const int slot = (head + 1 + f) % F;  // oldest first
-    const uint32_t ids = *(const uint32_t*)(ring + ((int64_t)slot * n + e) * SS + p4 * 4);
-    uint32_t m[4];
+// The 16 per-palette-id words of an expansion (channel bitmask / gray value /
+// 0xRRGGBB), passed by value in the kernel arguments.
+struct Lut16 {
+  uint32_t v[16];
+};
+
+// Semantic one-hot + frame stack + the stack's last wrapper, out[e][ch][p]:
+//   FUSE 0  FlattenStackedFrames: ch = f*C + c, oldest frame first
+//           (rgb_to_semantic.py:65-142, 256-272)
+//   FUSE 1  VehicleTemporalFusionWrapper: the newest frame's channels without the
+//           vehicle channel, then vehicle_t, vehicle_t-1, vehicle_t-2
+//           (rgb_to_semantic.py:152-166, 275-301)
+//   FUSE 2  WeightedVehicleHistoryWrapper: the newest frame's channels without the
+//           vehicle channel, then clip(1*v_t + 0.5*v_t-1 + 0.25*v_t-2, 0, 1) summed
+//           in float32 in that order (rgb_to_semantic.py:169-191, 304-332)
+// V pixels per thread (4: float4 stores; 1 when S*S is not a multiple of 4).
+// Outputs are streamed (non-temporal): the stack is written once per step and
+// read by the learner later, so it should not evict the map and records from L2.
+typedef float nt_f4 __attribute__((ext_vector_type(4)));
+typedef uint32_t nt_u4 __attribute__((ext_vector_type(4)));
+
+template <int V>
+__device__ __forceinline__ void store_nt(float* d, const float* v) {
+  if (V == 4) {
+    nt_f4 x = {v[0], v[V > 1 ? 1 : 0], v[V > 2 ? 2 : 0], v[V > 3 ? 3 : 0]};
+    __builtin_nontemporal_store(x, (nt_f4*)d);
+  } else {
+    __builtin_nontemporal_store(v[0], d);
+  }
+}
+
+template <int V>
+__device__ __forceinline__ void load_masks(const uint8_t* src, const Lut16& lut, uint32_t* m) {
+  if (V == 4) {
+    const uint32_t ids = *(const uint32_t*)src;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) m[k] = lut[(ids >> (8 * k)) & 15];
-    float* o = out + ((e * F + f) * C) * (int64_t)SS + p4 * 4;
-    for (int c = 0; c < C; ++c) {
-      float4 v4 = make_float4((float)((m[0] >> c) & 1), (float)((m[1] >> c) & 1), (float)((m[2] >> c) & 1),
-                              (float)((m[3] >> c) & 1));
-      *(float4*)(o + (int64_t)c * SS) = v4;
+    for (int k = 0; k < V; ++k) m[k] = lut.v[(ids >> (8 * k)) & 15];
+  } else {
+    m[0] = lut.v[src[0] & 15];
+  }
+}
+
+template <int FUSE, int V>
+__global__ __launch_bounds__(256) void k_expand_semantic(const uint8_t* __restrict__ ring, int n, int F, int head, int C,
+                                                         int vidx, int SS, Lut16 lut, float* __restrict__ out) {
+  const int nv = SS / V;
+  const int Cout = FUSE == 0 ? F * C : (FUSE == 1 ? C + 2 : C);
+  const int64_t total = (int64_t)n * nv;
+  for (int64_t q = blockIdx.x * 256ll + threadIdx.x; q < total; q += (int64_t)gridDim.x * 256) {
+    const int64_t e = q / nv;
+    const int64_t p = (q - e * nv) * V;
+    float* o = out + e * Cout * (int64_t)SS + p;
+    float vals[V];
+    if (FUSE == 0) {
+      for (int f = 0; f < F; ++f) {  // oldest -> newest
+        const int slot = (head + 1 + f) % F;
+        uint32_t m[V];
+        load_masks<V>(ring + ((int64_t)slot * n + e) * SS + p, lut, m);
+        for (int c = 0; c < C; ++c) {
+#pragma unroll
+          for (int k = 0; k < V; ++k) vals[k] = (float)((m[k] >> c) & 1);
+          store_nt<V>(o + (int64_t)(f * C + c) * SS, vals);
+        }
+      }
+    } else {
+      uint32_t m0[V], m1[V], m2[V];  // newest, newest-1, newest-2
+      load_masks<V>(ring + ((int64_t)head * n + e) * SS + p, lut, m0);
+      load_masks<V>(ring + ((int64_t)((head - 1 + F) % F) * n + e) * SS + p, lut, m1);
+      load_masks<V>(ring + ((int64_t)((head - 2 + 2 * F) % F) * n + e) * SS + p, lut, m2);
+      int oc = 0;
+      for (int c = 0; c < C; ++c) {  // static channels of the newest frame
+        if (c == vidx) continue;
+#pragma unroll
+        for (int k = 0; k < V; ++k) vals[k] = (float)((m0[k] >> c) & 1);
+        store_nt<V>(o + (int64_t)(oc++) * SS, vals);
+      }
+      float v0[V], v1[V], v2[V];
+#pragma unroll
+      for (int k = 0; k < V; ++k) {
+        v0[k] = (float)((m0[k] >> vidx) & 1);
+        v1[k] = (float)((m1[k] >> vidx) & 1);
+        v2[k] = (float)((m2[k] >> vidx) & 1);
+      }
+      if (FUSE == 1) {
+        store_nt<V>(o + (int64_t)oc * SS, v0);
+        store_nt<V>(o + (int64_t)(oc + 1) * SS, v1);
+        store_nt<V>(o + (int64_t)(oc + 2) * SS, v2);
+      } else {
+#pragma unroll
+        for (int k = 0; k < V; ++k) {
+          float acc = 0.0f;
+          acc += 1.0f * v0[k];
+          acc += 0.5f * v1[k];
+          acc += 0.25f * v2[k];
+          vals[k] = fminf(fmaxf(acc, 0.0f), 1.0f);
+        }
+        store_nt<V>(o + (int64_t)oc * SS, vals);
+      }
     }
   }
 }
 
-// grayscale + frame stack: out[e][f][p] (uint8)
+// Grayscale + frame stack: out[e][f][p] (uint8), oldest first. RAW: the ring
+// already holds gray values (the resize path), copied as they are.
+template <bool RAW, int V>
 __global__ __launch_bounds__(256) void k_expand_gray(const uint8_t* __restrict__ ring, int n, int F, int head, int SS,
-                                                     const uint32_t* __restrict__ lut, uint8_t* __restrict__ out) {
-  const int64_t total16 = (int64_t)n * F * (SS / 16);
-  for (int64_t q = blockIdx.x * 256ll + threadIdx.x; q < total16; q += (int64_t)gridDim.x * 256) {
-    const int64_t p16 = q % (SS / 16);
-    const int64_t ef = q / (SS / 16);
+                                                     Lut16 lut, uint8_t* __restrict__ out) {
+  const int nv = SS / V;
+  const int64_t total = (int64_t)n * F * nv;
+  for (int64_t q = blockIdx.x * 256ll + threadIdx.x; q < total; q += (int64_t)gridDim.x * 256) {
+    const int64_t pv = q % nv;
+    const int64_t ef = q / nv;
     const int f = (int)(ef % F);
     const int64_t e = ef / F;
     const int slot = (head + 1 + f) % F;
-    uint4 ids = *(const uint4*)(ring + ((int64_t)slot * n + e) * SS + p16 * 16);
-    uint32_t in[4] = {ids.x, ids.y, ids.z, ids.w}, o[4];
+    const uint8_t* src = ring + ((int64_t)slot * n + e) * SS + pv * V;
+    uint8_t* dst = out + (e * F + f) * (int64_t)SS + pv * V;
+    if (V == 16) {
+      uint4 ids = *(const uint4*)src;
+      if (!RAW) {
+        uint32_t in[4] = {ids.x, ids.y, ids.z, ids.w}, o[4];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      o[k] = 0;
+        for (int k = 0; k < 4; ++k) {
+          o[k] = 0;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) o[k] |= (lut[(in[k] >> (8 * j)) & 15] & 255u) << (8 * j);
+          for (int j = 0; j < 4; ++j) o[k] |= (lut.v[(in[k] >> (8 * j)) & 15] & 255u) << (8 * j);
+        }
+        ids = make_uint4(o[0], o[1], o[2], o[3]);
+      }
+      nt_u4 x = {ids.x, ids.y, ids.z, ids.w};
+      __builtin_nontemporal_store(x, (nt_u4*)dst);
+    } else {
+      dst[0] = RAW ? src[0] : (uint8_t)lut.v[src[0] & 15];
     }
-    *(uint4*)(out + (e * F + f) * (int64_t)SS + p16 * 16) = make_uint4(o[0], o[1], o[2], o[3]);
   }
 }
 
 // RGB of the newest frame: out[e][p][3]
-__global__ __launch_bounds__(256) void k_expand_rgb(const uint8_t* __restrict__ ring, int n, int head, int SS,
-                                                    const uint32_t* __restrict__ lut, uint8_t* __restrict__ out) {
+__global__ __launch_bounds__(256) void k_expand_rgb(const uint8_t* __restrict__ ring, int n, int head, int SS, Lut16 lut,
+                                                    uint8_t* __restrict__ out) {
   const int64_t total = (int64_t)n * SS;
   for (int64_t q = blockIdx.x * 256ll + threadIdx.x; q < total; q += (int64_t)gridDim.x * 256) {
     const int64_t e = q / SS, p = q % SS;
-    const uint32_t c = lut[ring[((int64_t)head * n + e) * SS + p] & 15];
+    const uint32_t c = lut.v[ring[((int64_t)head * n + e) * SS + p] & 15];
     uint8_t* o = out + q * 3;
     o[0] = (uint8_t)(c >> 16);
     o[1] = (uint8_t)(c >> 8);
     o[2] = (uint8_t)c;
+  }
+}
+
+// ---------------------------------------------------------------- resize
+// gymnasium ResizeObservation (cv2.resize INTER_AREA, opencv 4.11
+// imgproc/src/resize.cpp ResizeArea_Invoker / resizeAreaFast) of the RGB
+// render, fused with the next wrapper's colour test. One thread per output
+// pixel: for each y-table entry (sy, beta) of its row, buf = sum_k rgb(sy, sx_k)
+// * alpha_k (float32, table order), acc = beta*buf on the first entry, acc +=
+// beta*buf after; the channel is cvRound(acc) saturated to uint8. The output
+// byte is:
+//   GRAY 0  the palette id whose colour equals the resized RGB exactly, else
+//           CBEV_PX_OFF_PALETTE (every semantic channel zero,
+//           rgb_to_semantic.py:65-142 matches exact colours only)
+//   GRAY 1  the gymnasium GrayscaleObservation value of the resized RGB
+//           (float64 dot with (0.2125, 0.7154, 0.0721), truncated)
+// Integer scales use resizeAreaFast: scale 2 is (a+b+c+d+2)>>2, others
+// cvRound(sum * (1.f/area)). mask selects envs (NULL = all); the frame goes to
+// n_out destinations out + k*out_stride (the frame-stack ring on reset).
+__constant__ uint32_t c_palette_rgb[16];
+
+struct AreaTab {
+  const int32_t* xo;  // [w+1] offsets into xi/xa per output column
+  const int32_t* xi;
+  const float* xa;
+  const int32_t* yo;  // [h+1]
+  const int32_t* yi;
+  const float* ya;
+  int fast;  // integer scale (resizeAreaFast): sx, sy
+  int fsx, fsy;
+};
+
+__device__ __forceinline__ uint32_t resize_finish(float r, float g, float b, int gray) {
+  const int ir = min(max((int)__builtin_rintf(r), 0), 255);
+  const int ig = min(max((int)__builtin_rintf(g), 0), 255);
+  const int ib = min(max((int)__builtin_rintf(b), 0), 255);
+  if (gray) {
+    const double v = ((double)ir * 0.2125 + (double)ig * 0.7154) + (double)ib * 0.0721;
+    return (uint32_t)v;
+  }
+  const uint32_t rgb = ((uint32_t)ir << 16) | ((uint32_t)ig << 8) | (uint32_t)ib;
+  uint32_t id = CBEV_PX_OFF_PALETTE;
+#pragma unroll
+  for (int k = CBEV_PX_COUNT - 1; k >= 0; --k)
+    if (c_palette_rgb[k] == rgb) id = (uint32_t)k;
+  return id;
+}
+
+__global__ __launch_bounds__(256) void k_resize(const uint8_t* __restrict__ src, int n, int S,
+                                                const uint8_t* __restrict__ mask, int h, int w, int gray, AreaTab T,
+                                                uint8_t* __restrict__ out, int n_out, int64_t out_stride) {
+  const int64_t hw = (int64_t)h * w;
+  const int64_t total = (int64_t)n * hw;
+  for (int64_t q = blockIdx.x * 256ll + threadIdx.x; q < total; q += (int64_t)gridDim.x * 256) {
+    const int64_t e = q / hw;
+    if (mask && !mask[e]) continue;
+    const int p = (int)(q - e * hw);
+    const int dy = p / w, dx = p - dy * w;
+    const uint8_t* f = src + e * (int64_t)S * S;
+    uint32_t v;
+    if (T.fast) {
+      int sr = 0, sg = 0, sbl = 0;
+      for (int yy = 0; yy < T.fsy; ++yy)
+        for (int xx = 0; xx < T.fsx; ++xx) {
+          const uint32_t c = c_palette_rgb[f[(dy * T.fsy + yy) * S + dx * T.fsx + xx] & 15];
+          sr += (int)(c >> 16);
+          sg += (int)((c >> 8) & 255);
+          sbl += (int)(c & 255);
+        }
+      float r, g, b;
+      if (T.fsx == 2 && T.fsy == 2) {
+        r = (float)((sr + 2) >> 2);
+        g = (float)((sg + 2) >> 2);
+        b = (float)((sbl + 2) >> 2);
+      } else {
+        const float sc = 1.0f / (float)(T.fsx * T.fsy);
+        r = (float)sr * sc;
+        g = (float)sg * sc;
+        b = (float)sbl * sc;
+      }
+      v = resize_finish(r, g, b, gray);
+    } else {
+      float ar = 0.f, ag = 0.f, ab = 0.f;
+      const int y0 = T.yo[dy], y1 = T.yo[dy + 1], x0 = T.xo[dx], x1 = T.xo[dx + 1];
+      for (int j = y0; j < y1; ++j) {
+        const uint8_t* row = f + (int64_t)T.yi[j] * S;
+        float br = 0.f, bg = 0.f, bb = 0.f;
+        for (int k = x0; k < x1; ++k) {
+          const uint32_t c = c_palette_rgb[row[T.xi[k]] & 15];
+          const float a = T.xa[k];
+          br = br + (float)(c >> 16) * a;
+          bg = bg + (float)((c >> 8) & 255) * a;
+          bb = bb + (float)(c & 255) * a;
+        }
+        const float beta = T.ya[j];
+        if (j == y0) {
+          ar = beta * br;
+          ag = beta * bg;
+          ab = beta * bb;
+        } else {
+          ar = ar + beta * br;
+          ag = ag + beta * bg;
+          ab = ab + beta * bb;
+        }
+      }
+      v = resize_finish(ar, ag, ab, gray);
+    }
+    for (int k = 0; k < n_out; ++k) out[k * out_stride + q] = (uint8_t)v;
   }
 }
 
@@ -1654,6 +1854,9 @@ struct cbev_ctx {
   int npitch;            // nibble-packed map pitch (bytes)
   int hero_ne, hero_sb;  // staged thread-per-env kernels: envs per workgroup, staged bytes per record
   int coll_ne, coll_sb, coll_scr;
+  int obs_h, obs_w;   // wrapped frame size (ResizeObservation); == size when not resizing
+  void* area_dev;     // INTER_AREA tables of cbev_set_obs_size
+  AreaTab area;
 };
 
 // envs per workgroup for a staged kernel: the largest divisor of 64 whose
@@ -1825,6 +2028,11 @@ int cbev_create(const cbev_params* params, const cbev_caps* caps, int device, cb
   build_sg_tables(&T);
   hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(c_sg), &T, sizeof T);
   if (e == hipSuccess) e = hipMalloc(&c->lut_dev, 64 * sizeof(uint32_t));
+  if (e == hipSuccess) {
+    const uint32_t pal[16] = CBEV_PALETTE_RGB;
+    e = hipMemcpyToSymbol(HIP_SYMBOL(c_palette_rgb), pal, sizeof pal);
+  }
+  c->obs_h = c->obs_w = P.size;
   if (e == hipSuccess)
     e = hipFuncSetAttribute((const void*)k_hero, hipFuncAttributeMaxDynamicSharedMemorySize,
                             c->hero_ne * (c->hero_sb + 32));
@@ -1884,6 +2092,7 @@ void cbev_destroy(cbev_ctx* c) {
   }
   if (c->map_dev) (void)hipFree(c->map_dev);
   if (c->lut_dev) (void)hipFree(c->lut_dev);
+  if (c->area_dev) (void)hipFree(c->area_dev);
   free(c);
 }
 
@@ -2005,23 +2214,165 @@ int cbev_reset_frames(cbev_ctx* c, void* records, int n, const void* bank, int n
 
 int cbev_expand_obs(cbev_ctx* c, const uint8_t* ring, int n, int n_frames, int head, int kind, int n_channels,
                     const uint32_t* lut_host, void* out, void* stream) {
-  if (!c || !ring || !out || !lut_host) return set_err(CBEV_EINVAL, "null argument");
+  if (!c || !ring || !out) return set_err(CBEV_EINVAL, "null argument");
+  if (!lut_host && kind != 5) return set_err(CBEV_EINVAL, "null lut");
   if (n_frames < 1 || head < 0 || head >= n_frames) return set_err(CBEV_EINVAL, "bad frame ring");
-  if (kind == 0 && (n_channels < 1 || n_channels > 16)) return set_err(CBEV_EINVAL, "bad channel count");
+  const bool sem = kind == 0 || kind == 3 || kind == 4;
+  if (sem && (n_channels < 1 || n_channels > 16)) return set_err(CBEV_EINVAL, "bad channel count");
+  Lut16 lut{};
+  if (lut_host) memcpy(lut.v, lut_host, sizeof lut.v);
+  int vidx = -1;
+  if (kind == 3 || kind == 4) {
+    // the vehicle channel is the one bit the vehicle colour sets (vehicle_channel_index,
+    // rgb_to_semantic.py:55-62); the fusions keep 3 frames (:152-191)
+    const uint32_t vm = lut.v[CBEV_PX_VEHICLE];
+    if (vm == 0 || (vm & (vm - 1)) != 0 || vm >= (1u << n_channels))
+      return set_err(CBEV_EINVAL, "vehicle history fusion needs a semantic mode with a vehicle channel");
+    vidx = __builtin_ctz(vm);
+    if (n_frames < 3) return set_err(CBEV_EINVAL, "vehicle history fusion requires frame_stack >= 3");
+  }
   if (n <= 0) return CBEV_OK;
   hipStream_t s = (hipStream_t)stream;
-  HIP_TRY(hipMemcpyAsync(c->lut_dev, lut_host, 16 * sizeof(uint32_t), hipMemcpyHostToDevice, s));
-  const int SS = c->P.size * c->P.size;
-  const int grid = 2048;
-  if (kind == 0)
-    hipLaunchKernelGGL(k_expand_semantic, dim3(grid), dim3(256), 0, s, ring, n, n_frames, head, n_channels, SS, c->lut_dev,
-                       (float*)out);
-  else if (kind == 1)
-    hipLaunchKernelGGL(k_expand_gray, dim3(grid), dim3(256), 0, s, ring, n, n_frames, head, SS, c->lut_dev, (uint8_t*)out);
-  else if (kind == 2)
-    hipLaunchKernelGGL(k_expand_rgb, dim3(grid), dim3(256), 0, s, ring, n, head, SS, c->lut_dev, (uint8_t*)out);
-  else
-    return set_err(CBEV_EINVAL, "unknown expansion kind %d", kind);
+  const int SS = c->obs_h * c->obs_w;
+  const int grid = 4096;
+  const bool v4 = SS % 4 == 0, v16 = SS % 16 == 0;
+  switch (kind) {
+#define SEM_CASE(K, FUSE)                                                                                          \
+  case K:                                                                                                          \
+    if (v4)                                                                                                        \
+      hipLaunchKernelGGL((k_expand_semantic<FUSE, 4>), dim3(grid), dim3(256), 0, s, ring, n, n_frames, head,        \
+                         n_channels, vidx, SS, lut, (float*)out);                                                   \
+    else                                                                                                           \
+      hipLaunchKernelGGL((k_expand_semantic<FUSE, 1>), dim3(grid), dim3(256), 0, s, ring, n, n_frames, head,        \
+                         n_channels, vidx, SS, lut, (float*)out);                                                   \
+    break;
+    SEM_CASE(0, 0)
+    SEM_CASE(3, 1)
+    SEM_CASE(4, 2)
+#undef SEM_CASE
+    case 1:
+    case 5:
+      if (v16 && kind == 1)
+        hipLaunchKernelGGL((k_expand_gray<false, 16>), dim3(grid), dim3(256), 0, s, ring, n, n_frames, head, SS, lut,
+                           (uint8_t*)out);
+      else if (v16)
+        hipLaunchKernelGGL((k_expand_gray<true, 16>), dim3(grid), dim3(256), 0, s, ring, n, n_frames, head, SS, lut,
+                           (uint8_t*)out);
+      else if (kind == 1)
+        hipLaunchKernelGGL((k_expand_gray<false, 1>), dim3(grid), dim3(256), 0, s, ring, n, n_frames, head, SS, lut,
+                           (uint8_t*)out);
+      else
+        hipLaunchKernelGGL((k_expand_gray<true, 1>), dim3(grid), dim3(256), 0, s, ring, n, n_frames, head, SS, lut,
+                           (uint8_t*)out);
+      break;
+    case 2:
+      hipLaunchKernelGGL(k_expand_rgb, dim3(grid), dim3(256), 0, s, ring, n, head, c->P.size * c->P.size, lut,
+                         (uint8_t*)out);
+      break;
+    default:
+      return set_err(CBEV_EINVAL, "unknown expansion kind %d", kind);
+  }
+  HIP_TRY(hipGetLastError());
+  return CBEV_OK;
+}
+
+// computeResizeAreaTab (opencv 4.11 imgproc/src/resize.cpp), double arithmetic,
+// float weights; entries grouped per destination index in increasing order.
+static void area_tab(int ssize, int dsize, double scale, std::vector<int32_t>& off, std::vector<int32_t>& si,
+                     std::vector<float>& alpha) {
+  off.assign(dsize + 1, 0);
+  si.clear();
+  alpha.clear();
+  for (int dx = 0; dx < dsize; ++dx) {
+    off[dx] = (int32_t)si.size();
+    const double fsx1 = dx * scale, fsx2 = fsx1 + scale;
+    const double cell = std::min(scale, ssize - fsx1);
+    int sx1 = (int)ceil(fsx1), sx2 = (int)floor(fsx2);
+    sx2 = std::min(sx2, ssize - 1);
+    sx1 = std::min(sx1, sx2);
+    if (sx1 - fsx1 > 1e-3) {
+      si.push_back(sx1 - 1);
+      alpha.push_back((float)((sx1 - fsx1) / cell));
+    }
+    for (int sx = sx1; sx < sx2; ++sx) {
+      si.push_back(sx);
+      alpha.push_back((float)(1.0 / cell));
+    }
+    if (fsx2 - sx2 > 1e-3) {
+      si.push_back(sx2);
+      alpha.push_back((float)(std::min(std::min(fsx2 - sx2, 1.), cell) / cell));
+    }
+  }
+  off[dsize] = (int32_t)si.size();
+}
+
+int cbev_set_obs_size(cbev_ctx* c, int h, int w) {
+  if (!c) return set_err(CBEV_EINVAL, "null argument");
+  const int S = c->P.size;
+  if (h < 1 || w < 1) return set_err(CBEV_EINVAL, "obs size %dx%d", h, w);
+  if (h > S || w > S)
+    return set_err(CBEV_EINVAL, "obs size %dx%d > render size %d: INTER_AREA upscaling (bilinear in OpenCV) is not "
+                   "supported", h, w, S);
+  if (c->area_dev) {
+    (void)hipSetDevice(c->device);
+    HIP_TRY(hipDeviceSynchronize());  // a queued resize may still read the old tables
+    (void)hipFree(c->area_dev);
+    c->area_dev = nullptr;
+  }
+  c->obs_h = h;
+  c->obs_w = w;
+  memset(&c->area, 0, sizeof c->area);
+  if (h == S && w == S) return CBEV_OK;
+  // hal::resize: scale = 1 / (dsize / ssize); integer scales take resizeAreaFast
+  const double sx = 1.0 / ((double)w / S), sy = 1.0 / ((double)h / S);
+  const int isx = (int)lrint(sx), isy = (int)lrint(sy);
+  if (fabs(sx - isx) < 2.220446049250313e-16 && fabs(sy - isy) < 2.220446049250313e-16) {
+    c->area.fast = 1;
+    c->area.fsx = isx;
+    c->area.fsy = isy;
+    return CBEV_OK;
+  }
+  std::vector<int32_t> xo, xi, yo, yi;
+  std::vector<float> xa, ya;
+  area_tab(S, w, sx, xo, xi, xa);
+  area_tab(S, h, sy, yo, yi, ya);
+  const size_t nb = 4 * (xo.size() + xi.size() + xa.size() + yo.size() + yi.size() + ya.size());
+  std::vector<uint8_t> blob(nb);
+  size_t o = 0;
+  auto put = [&](const void* p, size_t b) {
+    memcpy(blob.data() + o, p, b);
+    o += b;
+  };
+  put(xo.data(), 4 * xo.size());
+  put(xi.data(), 4 * xi.size());
+  put(xa.data(), 4 * xa.size());
+  put(yo.data(), 4 * yo.size());
+  put(yi.data(), 4 * yi.size());
+  put(ya.data(), 4 * ya.size());
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipMalloc(&c->area_dev, nb));
+  HIP_TRY(hipMemcpy(c->area_dev, blob.data(), nb, hipMemcpyHostToDevice));
+  const uint8_t* d = (const uint8_t*)c->area_dev;
+  c->area.xo = (const int32_t*)d;
+  c->area.xi = c->area.xo + xo.size();
+  c->area.xa = (const float*)(c->area.xi + xi.size());
+  c->area.yo = (const int32_t*)(c->area.xa + xa.size());
+  c->area.yi = c->area.yo + yo.size();
+  c->area.ya = (const float*)(c->area.yi + yi.size());
+  return CBEV_OK;
+}
+
+int cbev_resize_obs(cbev_ctx* c, const uint8_t* frames, int n, const uint8_t* mask, int gray, uint8_t* out, int n_out,
+                    int64_t out_stride, void* stream) {
+  if (!c || !frames || !out) return set_err(CBEV_EINVAL, "null argument");
+  if (n_out < 1) return set_err(CBEV_EINVAL, "n_out %d", n_out);
+  const int S = c->P.size;
+  if (c->obs_h == S && c->obs_w == S) return set_err(CBEV_ESTATE, "cbev_set_obs_size: no resize configured");
+  if (n <= 0) return CBEV_OK;
+  const int64_t total = (int64_t)n * c->obs_h * c->obs_w;
+  const int grid = (int)std::min<int64_t>((total + 255) / 256, 8192);
+  hipLaunchKernelGGL(k_resize, dim3(grid), dim3(256), 0, (hipStream_t)stream, frames, n, S, mask, c->obs_h, c->obs_w,
+                     gray ? 1 : 0, c->area, out, n_out, out_stride);
   HIP_TRY(hipGetLastError());
   return CBEV_OK;
 }

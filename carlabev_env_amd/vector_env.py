@@ -35,6 +35,7 @@ from .params import CbevParams, build_params, load_class_map, padded_map
 from .host_reset import HostResetBuilder, route_length_m
 from .scene_gen import SceneGenerator
 from .semantics import gray_lut, rgb_lut, semantic_lut, semantic_mask_channels, PALETTE
+from . import obs_pipeline as OP
 from .spaces import batch_space, make_box, make_discrete
 
 DEFAULT_CAPS = dict(route_cap=128, actor_cap=32, actor_route_cap=64, tl_cap=4)
@@ -69,12 +70,6 @@ class CarlaBEVVectorEnv:
         self.run_cfg = run
         self.cfg: EnvConfig = run.env
         self.num_envs = int(num_envs if num_envs is not None else run.num_envs)
-        if tuple(self.cfg.obs_size) != (self.cfg.size, self.cfg.size):
-            raise NotImplementedError(
-                f"obs_size={tuple(self.cfg.obs_size)} != (size, size): the INTER_AREA resize wrapper is not "
-                "implemented on the device yet; use obs_size=(size, size)")
-        if self.cfg.temporal_fusion_mode != "stack":
-            raise NotImplementedError("temporal_fusion_mode other than 'stack' is not implemented on the device yet")
         if self.cfg.fov_masked:
             raise NotImplementedError("fov_masked=True is not implemented on the device yet")
         self.info_mode = info_mode
@@ -104,8 +99,18 @@ class CarlaBEVVectorEnv:
         check(L.cbev_set_map(ctx, self.map_host.ctypes.data_as(ctypes.c_void_p), self.map_host.nbytes), "cbev_set_map")
         N, S, F = self.num_envs, self.S, self.F
         dev = self.device
+        # ResizeObservation(obs_size) (envs/__init__.py:62): frames are rendered at S x S and
+        # resized on the device into the (h, w) frame ring
+        self.obs_hw = (int(self.cfg.obs_size[0]), int(self.cfg.obs_size[1]))
+        self.resize = self.obs_hw != (S, S)
+        if self.resize:
+            check(L.cbev_set_obs_size(ctx, self.obs_hw[0], self.obs_hw[1]), "cbev_set_obs_size")
+        h, w = self.obs_hw
         self.records = torch.zeros((N, self.rb), dtype=torch.uint8, device=dev)
-        self.ring = torch.zeros((F, N, S, S), dtype=torch.uint8, device=dev)
+        self.ring = torch.zeros((F, N, h, w), dtype=torch.uint8, device=dev)
+        # render-size frame of the current step (render(), carlabev.py:233-249); the
+        # newest ring slot itself when there is no resize
+        self.full = torch.zeros((N, S, S), dtype=torch.uint8, device=dev) if self.resize else None
         self.head = 0
         self.reward = torch.zeros(N, dtype=torch.float64, device=dev)
         self.term = torch.zeros(N, dtype=torch.uint8, device=dev)
@@ -123,13 +128,16 @@ class CarlaBEVVectorEnv:
         if self.cfg.masked:
             self.channels = semantic_mask_channels(self.cfg.semantic_mask_ch)
             C = len(self.channels)
-            self.single_observation_space = make_box(0.0, 1.0, (F * C, S, S), np.float32)
-            self._obs_kind, self._obs_lut, self._obs_ch = 0, semantic_lut(self.cfg.semantic_mask_ch), C
-            self.obs_buf = torch.zeros((N, F * C, S, S), dtype=torch.float32, device=dev)
+            fusion = self.cfg.temporal_fusion_mode
+            Cw = OP.fused_channels(self.cfg.semantic_mask_ch, fusion, F)
+            self.single_observation_space = make_box(0.0, 1.0, (Cw, h, w), np.float32)
+            self._obs_kind, self._obs_lut, self._obs_ch = OP.FUSION_KIND[fusion], semantic_lut(self.cfg.semantic_mask_ch), C
+            self.obs_buf = torch.zeros((N, Cw, h, w), dtype=torch.float32, device=dev)
         else:
-            self.single_observation_space = make_box(0, 255, (F, S, S), np.uint8)
-            self._obs_kind, self._obs_lut, self._obs_ch = 1, gray_lut(), 1
-            self.obs_buf = torch.zeros((N, F, S, S), dtype=torch.uint8, device=dev)
+            self.single_observation_space = make_box(0, 255, (F, h, w), np.uint8)
+            self._obs_kind = OP.KIND_GRAY_RAW if self.resize else OP.KIND_GRAY
+            self._obs_lut, self._obs_ch = gray_lut(), 1
+            self.obs_buf = torch.zeros((N, F, h, w), dtype=torch.uint8, device=dev)
         self.observation_space = batch_space(self.single_observation_space, N)
         self.action_space = batch_space(self.single_action_space, N)
         seed = getattr(run, "seed", self.cfg.seed)
@@ -199,10 +207,25 @@ class CarlaBEVVectorEnv:
             self._bank_cursor = (self._bank_cursor + N) % B
         if mask is not None and (mask.dtype != torch.uint8 or mask.device != self.device):
             mask = mask.to(device=self.device, dtype=torch.uint8)
-        check(lib().cbev_reset_frames(self._ctx, _ptr(self.records), N, _ptr(self.bank), B, _ptr(mask),
-                                      _ptr(bank_idx), offset, _ptr(self.bank_frames), _ptr(self.ring), self.F,
-                                      self._stream()), "cbev_reset_frames")
+        if self.resize:
+            check(lib().cbev_reset_frames(self._ctx, _ptr(self.records), N, _ptr(self.bank), B, _ptr(mask),
+                                          _ptr(bank_idx), offset, _ptr(self.bank_frames), _ptr(self.full), 1,
+                                          self._stream()), "cbev_reset_frames")
+            self._resize_into_ring(mask, all_slots=True)
+        else:
+            check(lib().cbev_reset_frames(self._ctx, _ptr(self.records), N, _ptr(self.bank), B, _ptr(mask),
+                                          _ptr(bank_idx), offset, _ptr(self.bank_frames), _ptr(self.ring), self.F,
+                                          self._stream()), "cbev_reset_frames")
         return self._obs() if self.auto_obs else None
+
+    def _resize_into_ring(self, mask: torch.Tensor | None, all_slots: bool):
+        """ResizeObservation + the mask/grayscale colour test of self.full into the ring:
+        the newest slot after a step, every slot of the masked envs after a reset."""
+        h, w = self.obs_hw
+        N = self.num_envs
+        dst = self.ring[0] if all_slots else self.ring[self.head]
+        check(lib().cbev_resize_obs(self._ctx, _ptr(self.full), N, _ptr(mask), 0 if self.cfg.masked else 1, _ptr(dst),
+                                    self.F if all_slots else 1, N * h * w, self._stream()), "cbev_resize_obs")
 
     # ------------------------------------------------------------------ gymnasium surface
     def reset(self, seed=None, options=None):
@@ -231,8 +254,13 @@ class CarlaBEVVectorEnv:
             bank_idx[idx] = np.arange(len(idx), dtype=np.int32)
             bidx = torch.from_numpy(bank_idx).to(self.device)
             m = torch.from_numpy(mask.astype(np.uint8)).to(self.device)
-            check(lib().cbev_reset(self._ctx, _ptr(self.records), N, _ptr(staging), len(idx), _ptr(m), _ptr(bidx), 0,
-                                   _ptr(self.ring), self.F, self._stream()), "cbev_reset")
+            if self.resize:
+                check(lib().cbev_reset(self._ctx, _ptr(self.records), N, _ptr(staging), len(idx), _ptr(m), _ptr(bidx),
+                                       0, _ptr(self.full), 1, self._stream()), "cbev_reset")
+                self._resize_into_ring(m, all_slots=True)
+            else:
+                check(lib().cbev_reset(self._ctx, _ptr(self.records), N, _ptr(staging), len(idx), _ptr(m), _ptr(bidx),
+                                       0, _ptr(self.ring), self.F, self._stream()), "cbev_reset")
         obs = self._obs()
         infos = {}
         if len(idx):
@@ -260,10 +288,12 @@ class CarlaBEVVectorEnv:
         """Enqueue one step; returns nothing and never synchronises (bench path)."""
         a = self._actions_tensor(actions)
         self.head = (self.head + 1) % self.F
-        frames = self.ring[self.head]
+        frames = self.full if self.resize else self.ring[self.head]
         check(lib().cbev_step(self._ctx, _ptr(self.records), self.num_envs, _ptr(a), _ptr(frames), _ptr(self.reward),
                               _ptr(self.term), _ptr(self.trunc), _ptr(self.cause), _ptr(self.info), self._stream()),
               "cbev_step")
+        if self.resize:
+            self._resize_into_ring(None, all_slots=False)
         return a
 
     def step(self, actions):
@@ -335,20 +365,20 @@ class CarlaBEVVectorEnv:
 
     def render(self):
         """Tuple of per-env (S, S, 3) uint8 RGB frames, like SyncVectorEnv.render()."""
-        ids = self.ring[self.head].to("cpu").numpy()
+        ids = self.frames().to("cpu").numpy()
         rgb = PALETTE[ids]
         return tuple(rgb[i] for i in range(self.num_envs))
 
     def render_device(self) -> torch.Tensor:
         out = torch.empty((self.num_envs, self.S, self.S, 3), dtype=torch.uint8, device=self.device)
-        check(lib().cbev_expand_obs(self._ctx, _ptr(self.ring), self.num_envs, self.F, self.head, 2, 3,
+        check(lib().cbev_expand_obs(self._ctx, _ptr(self.frames()[None]), self.num_envs, 1, 0, 2, 3,
                                     rgb_lut().ctypes.data_as(ctypes.c_void_p), _ptr(out), self._stream()),
               "cbev_expand_obs")
         return out
 
     def frames(self) -> torch.Tensor:
-        """Newest palette-id frames (N, S, S) uint8 (compact observation)."""
-        return self.ring[self.head]
+        """Newest render-size palette-id frames (N, S, S) uint8 (compact observation)."""
+        return self.full if self.resize else self.ring[self.head]
 
     def records_host(self) -> np.ndarray:
         return self.records.to("cpu").numpy()

@@ -86,16 +86,43 @@ int cbev_reset_frames(cbev_ctx* ctx, void* records, int n, const void* bank, int
                       const int32_t* bank_idx, int bank_offset, const uint8_t* bank_frames, uint8_t* frames,
                       int n_frames, void* stream);
 
-/* Wrapper stack on the device (envs/__init__.py:62-83):
+/* Wrapper stack on the device (wrap_env, envs/__init__.py:62-83). `ring` holds
+ * n_frames frames per env (uint8[n_frames][n][h][w], slot `head` the newest;
+ * h x w = the cbev_set_obs_size size, the render size by default):
  *   kind 0: semantic one-hot (rgb_to_semantic.py:65-142) + FrameStack + Flatten
- *           -> float32[n][F*C][S][S]; channel_lut[id] = bitmask of channels set
+ *           -> float32[n][F*C][h][w]; channel_lut[id] = bitmask of channels set
+ *   kind 3: semantic + FrameStack + VehicleTemporalFusionWrapper
+ *           (rgb_to_semantic.py:152-166,275-301) -> float32[n][C+2][h][w]
+ *   kind 4: semantic + FrameStack + WeightedVehicleHistoryWrapper
+ *           (rgb_to_semantic.py:169-191,304-332) -> float32[n][C][h][w]
+ *           (kinds 3/4: the vehicle channel is the bit channel_lut[CBEV_PX_VEHICLE]
+ *           sets; n_frames >= 3)
  *   kind 1: grayscale (gymnasium GrayscaleObservation) + FrameStack
- *           -> uint8[n][F][S][S]; channel_lut[id] = gray value
- *   kind 2: RGB (render(), no wrappers) -> uint8[n][S][S][3] of the newest frame;
- *           channel_lut[id] = 0xRRGGBB
- * ring holds F frames per env, slot `head` is the newest. */
+ *           -> uint8[n][F][h][w]; channel_lut[id] = gray value
+ *   kind 5: FrameStack of a ring that already holds gray values (cbev_resize_obs
+ *           with gray = 1) -> uint8[n][F][h][w]; channel_lut unused (may be NULL)
+ *   kind 2: RGB (render(), no wrappers) -> uint8[n][S][S][3] of the newest
+ *           render-size frame; channel_lut[id] = 0xRRGGBB
+ * C = n_channels. */
 int cbev_expand_obs(cbev_ctx* ctx, const uint8_t* ring, int n, int n_frames, int head, int kind, int n_channels,
                     const uint32_t* channel_lut_host, void* out, void* stream);
+
+/* ResizeObservation(obs_size) (gymnasium; cv2.resize INTER_AREA) between the
+ * render and the mask / grayscale wrappers (envs/__init__.py:62-67). Sets the
+ * wrapped frame size h x w (<= size; h == w == size turns resizing off) and
+ * builds the INTER_AREA tables. Not stream-ordered: call it before queuing work. */
+int cbev_set_obs_size(cbev_ctx* ctx, int h, int w);
+
+/* Resize n palette-id frames (uint8[n][S][S], e.g. cbev_step's output) to the
+ * cbev_set_obs_size size, fused with the next wrapper's colour test:
+ *   gray = 0: out byte = the palette id whose colour equals the resized RGB,
+ *             else CBEV_PX_OFF_PALETTE (all semantic channels 0) -> expand kinds 0/3/4
+ *   gray = 1: out byte = the grayscale value of the resized RGB -> expand kind 5
+ * Envs with mask[e] == 0 are skipped (mask NULL = all). The frame is written to
+ * n_out destinations out + k*out_stride (e.g. every slot of the ring on reset).
+ * Returns CBEV_ESTATE when no resize is configured. */
+int cbev_resize_obs(cbev_ctx* ctx, const uint8_t* frames, int n, const uint8_t* mask, int gray, uint8_t* out,
+                    int n_out, int64_t out_stride, void* stream);
 
 /* Kernel timing with HIP events recorded on the step's own stream around each
  * of the three step kernels (used by bench.py for the roofline figure).

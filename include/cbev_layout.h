@@ -128,7 +128,13 @@ enum { CBEV_COLL_NONE = 0, CBEV_COLL_VEHICLE = 1, CBEV_COLL_PEDESTRIAN = 2,
 enum { CBEV_PX_NON_DRIVABLE = 0, CBEV_PX_DRIVABLE = 1, CBEV_PX_SIDEWALK = 2,
        CBEV_PX_VEHICLE = 3, CBEV_PX_PEDESTRIAN = 4, CBEV_PX_ROUTE = 5,
        CBEV_PX_TL_RED = 6, CBEV_PX_YELLOW = 7, CBEV_PX_BLACK = 8,
-       CBEV_PX_TL_UNKNOWN = 9, CBEV_PX_COUNT = 10 };
+       CBEV_PX_TL_UNKNOWN = 9, CBEV_PX_COUNT = 10,
+       /* a resized frame's pixel whose blended colour matches no palette colour
+        * (ResizeObservation INTER_AREA blends; every semantic channel is 0) */
+       CBEV_PX_OFF_PALETTE = 15 };
+/* 0xRRGGBB of each palette id */
+#define CBEV_PALETTE_RGB {0x969696u, 0xffffffu, 0xdcdcdcu, 0x0007afu, 0xff0000u, 0x00ff00u, \
+                          0xff4040u, 0xffff00u, 0x000000u, 0x646464u}
 
 /* capacities that size a record */
 typedef struct cbev_caps {

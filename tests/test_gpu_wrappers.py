@@ -1,0 +1,177 @@
+"""GPU parity of the device wrapper stack (cbev_expand_obs kinds 0-5,
+cbev_resize_obs) against the wrapper oracle (oracle/wrappers.py), through the
+C-ABI, and of the vector env's wrapped observations end to end.
+
+Bar: bit-exact. One-hot / fused float32 values are 0, 1 or exact sums of
+1, 0.5, 0.25; the resize accumulates in float32 in OpenCV's order on both
+sides (no FMA contraction: -ffp-contract=off), rounds half-to-even and
+matches exact colours; grayscale is the same float64 dot product, truncated.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+import wrappers as W
+from carlabev_env_amd._lib import check, lib
+from carlabev_env_amd.semantics import gray_lut, semantic_lut, semantic_mask_channels
+from helpers import CAPS_FULL, world
+
+pytestmark = pytest.mark.gpu
+
+P_ = ctypes.c_void_p
+MODES = ("binary", "2-class", "4-class", "5-class", "6-class", "7-class")
+VMODES = ("4-class", "5-class", "6-class", "7-class")
+
+
+def ptr(t):
+    return P_(t.data_ptr()) if t is not None else None
+
+
+class Ctx:
+    def __init__(self, size=128):
+        cfg, P, padded, layout, builder = world(size=size)
+        self.P = P
+        self.ctx = P_()
+        check(lib().cbev_create(ctypes.byref(P), ctypes.byref(CAPS_FULL.c()), 0, ctypes.byref(self.ctx)), "create")
+        check(lib().cbev_set_map(self.ctx, padded.ctypes.data_as(P_), padded.nbytes), "set_map")
+
+    def __del__(self):
+        lib().cbev_destroy(self.ctx)
+
+
+def blocky_ids(rng, n, S, k=8):
+    """Palette-id frames with blocks of one id (so resized pixels often land exactly
+    on palette colours) and random single pixels (blends)."""
+    base = rng.integers(0, 10, (n, S // k, S // k)).astype(np.uint8)
+    ids = np.repeat(np.repeat(base, k, axis=1), k, axis=2)
+    noise = rng.random((n, S, S)) < 0.05
+    ids[noise] = rng.integers(0, 10, int(noise.sum()))
+    return ids
+
+
+def expand(c, ring_d, n, F, head, kind, C, lut, out):
+    check(lib().cbev_expand_obs(c.ctx, ptr(ring_d), n, F, head, kind, C,
+                                None if lut is None else lut.ctypes.data_as(P_), ptr(out), None), "expand")
+    torch.cuda.synchronize()
+    return out.cpu().numpy()
+
+
+@pytest.mark.parametrize("F,head", [(4, 1), (3, 0), (5, 4)])
+def test_expand_semantic_stack_and_fusions(F, head):
+    c = Ctx()
+    S, n = 128, 9
+    rng = np.random.default_rng(F * 10 + head)
+    ring_h = rng.integers(0, 10, (F, n, S, S)).astype(np.uint8)
+    ring_h[:, 2] = np.where(rng.random((F, S, S)) < 0.5, 3, ring_h[:, 2])  # dense vehicles
+    ring_d = torch.from_numpy(ring_h).cuda()
+    order = [(head + 1 + f) % F for f in range(F)]  # oldest first
+    for mode in MODES:
+        C = len(semantic_mask_channels(mode))
+        lut = semantic_lut(mode)
+        kinds = [(0, F * C, "stack")]
+        if mode in VMODES:
+            kinds += [(3, C + 2, "vehicle_temporal"), (4, C, "vehicle_weighted")]
+        for kind, Cout, fusion in kinds:
+            out = torch.full((n, Cout, S, S), -7.0, dtype=torch.float32, device="cuda")
+            o = expand(c, ring_d, n, F, head, kind, C, lut, out)
+            for e in (0, 2, n - 1):
+                ref = W.wrap_obs_stack(ring_h[order, e], "bev_semantic", mode, fusion=fusion)
+                assert np.array_equal(o[e], ref), (mode, fusion, e)
+
+
+def test_expand_rejects_fusion_without_vehicle_channel():
+    c = Ctx()
+    ring = torch.zeros((4, 2, 128, 128), dtype=torch.uint8, device="cuda")
+    out = torch.zeros((2, 4, 128, 128), dtype=torch.float32, device="cuda")
+    for mode in ("binary", "2-class"):
+        rc = lib().cbev_expand_obs(c.ctx, ptr(ring), 2, 4, 0, 3, len(semantic_mask_channels(mode)),
+                                   semantic_lut(mode).ctypes.data_as(P_), ptr(out), None)
+        assert rc != 0
+    lut = semantic_lut("6-class")
+    assert lib().cbev_expand_obs(c.ctx, ptr(ring[:2]), 2, 2, 0, 4, 6, lut.ctypes.data_as(P_), ptr(out), None) != 0
+
+
+@pytest.mark.parametrize("hw", [(96, 96), (64, 64), (84, 84), (96, 80), (100, 128), (32, 32)])
+def test_resize_matches_inter_area_oracle(hw):
+    c = Ctx()
+    S, n = 128, 6
+    rng = np.random.default_rng(hw[0] * 1000 + hw[1])
+    ids = blocky_ids(rng, n, S)
+    ids_d = torch.from_numpy(ids).cuda()
+    h, w = hw
+    check(lib().cbev_set_obs_size(c.ctx, h, w), "set_obs_size")
+    for gray in (0, 1):
+        out = torch.full((n, h, w), 77, dtype=torch.uint8, device="cuda")
+        check(lib().cbev_resize_obs(c.ctx, ptr(ids_d), n, None, gray, ptr(out), 1, n * h * w, None), "resize")
+        torch.cuda.synchronize()
+        o = out.cpu().numpy()
+        for e in range(n):
+            rgb = W.resize_area(W.PALETTE[ids[e]], (h, w))
+            if gray:
+                assert np.array_equal(o[e], W.grayscale(rgb)), (hw, e)
+            else:
+                for mode in MODES:
+                    m = semantic_lut(mode)[o[e]]
+                    got = np.stack([((m >> k) & 1).astype(np.float32)
+                                    for k in range(len(semantic_mask_channels(mode)))])
+                    assert np.array_equal(got, W.rgb_to_semantic_mask(rgb, mode)), (hw, e, mode)
+    # masked, multi-destination (reset into every ring slot)
+    F = 3
+    ring = torch.full((F, n, h, w), 200, dtype=torch.uint8, device="cuda")
+    mask = torch.tensor([1, 0, 1, 1, 0, 1], dtype=torch.uint8, device="cuda")
+    check(lib().cbev_resize_obs(c.ctx, ptr(ids_d), n, ptr(mask), 1, ptr(ring), F, n * h * w, None), "resize")
+    torch.cuda.synchronize()
+    r = ring.cpu().numpy()
+    for e in range(n):
+        for f in range(F):
+            if mask[e]:
+                assert np.array_equal(r[f, e], W.grayscale(W.resize_area(W.PALETTE[ids[e]], (h, w))))
+            else:
+                assert np.all(r[f, e] == 200)
+
+
+def test_resize_rejects_upscale():
+    c = Ctx()
+    assert lib().cbev_set_obs_size(c.ctx, 160, 128) != 0
+
+
+@pytest.mark.parametrize("obs_mode,fusion,obs_size", [
+    ("bev_semantic", "vehicle_temporal", (96, 96)),
+    ("bev_semantic", "vehicle_weighted", (128, 128)),
+    ("bev_semantic", "stack", (96, 96)),
+    ("bev_rgb", "stack", (84, 84)),
+])
+def test_vector_env_wrapped_obs_match_oracle(obs_mode, fusion, obs_size):
+    """make_env with resize / fusion: every step's observation equals the wrapper
+    oracle applied to the env's own render-size frames (the reset frame fills the
+    stack, FrameStackObservation padding)."""
+    from carlabev_env_amd import EnvConfig, make_env, build_random_navigation_options, RandomNavigationReset
+    cfg = EnvConfig(size=128, obs_size=obs_size, render_mode="rgb_array", obs_mode=obs_mode,
+                    semantic_mask_ch="6-class", temporal_fusion_mode=fusion, max_vehicles=10)
+    n = 6
+    env = make_env({"env": cfg, "num_envs": n})
+    obs, _ = env.reset(seed=11, options=build_random_navigation_options(
+        RandomNavigationReset(difficulty_id="rt_medium_v1")))
+    F = cfg.frame_stack
+    hist = [env.frames().cpu().numpy().copy() for _ in range(F)]
+    rng = np.random.default_rng(3)
+
+    def check_obs(o):
+        o = o.cpu().numpy()
+        for e in range(n):
+            ref = W.wrap_obs_stack(np.stack([h[e] for h in hist[-F:]]), obs_mode, "6-class",
+                                   obs_size=None if obs_size == (128, 128) else obs_size, fusion=fusion)
+            assert np.array_equal(o[e], ref), (e, len(hist))
+
+    assert tuple(obs.shape[1:]) == env.single_observation_space.shape
+    check_obs(obs)
+    for t in range(6):
+        obs, r, term, trunc, infos = env.step(rng.integers(0, 9, n))
+        hist.append(env.frames().cpu().numpy().copy())
+        check_obs(obs)
+    env.close()
