@@ -54,6 +54,10 @@ def lib():
     L.cbev_reset_frames.restype = _I
     L.cbev_expand_obs.argtypes = [_P, _P, _I, _I, _I, _I, _I, _P, _P, _P]
     L.cbev_expand_obs.restype = _I
+    L.cbev_vector_obs.argtypes = [_P, _P, _I, _P, _P]
+    L.cbev_vector_obs.restype = _I
+    L.cbev_set_fov_mask.argtypes = [_P, _P]
+    L.cbev_set_fov_mask.restype = _I
     L.cbev_set_obs_size.argtypes = [_P, _I, _I]
     L.cbev_set_obs_size.restype = _I
     L.cbev_resize_obs.argtypes = [_P, _P, _I, _P, _I, _P, _I, _I64, _P]
@@ -75,4 +79,4 @@ def check(rc: int, what: str = "cbev call"):
 EXPORTED_SYMBOLS = ("cbev_abi_version", "cbev_params_size", "cbev_layout_of", "cbev_field_names", "cbev_last_error",
                     "cbev_create", "cbev_destroy", "cbev_set_map", "cbev_step", "cbev_reset", "cbev_bank_frames",
                     "cbev_reset_frames",
-                    "cbev_expand_obs", "cbev_set_obs_size", "cbev_resize_obs", "cbev_profile", "cbev_profile_read")
+                    "cbev_expand_obs", "cbev_vector_obs", "cbev_set_fov_mask", "cbev_set_obs_size", "cbev_resize_obs", "cbev_profile", "cbev_profile_read")

@@ -764,7 +764,8 @@ __global__ __launch_bounds__(256) void k_actors(KArgs K, uint8_t* __restrict__ r
 template <int G, bool R90, bool CHECK>
 __device__ __forceinline__ void raster_out(const cbev_params& P, const RotSetup& R, const uint8_t* __restrict__ lds,
                                            int shift, uint32_t bg, uint8_t* __restrict__ out, int nout,
-                                           int64_t out_stride, int lane, int wave) {
+                                           int64_t out_stride, int lane, int wave,
+                                           const uint32_t* __restrict__ fov) {
   constexpr int RPC = 16 / G;  // output rows per chunk
   constexpr int S = 64 * G;    // == P.size
   constexpr int LPR = S / 4;   // lanes per output row
@@ -852,6 +853,13 @@ __device__ __forceinline__ void raster_out(const cbev_params& P, const RotSetup&
       for (int d = 0; d < 4; ++d)
         if ((unsigned)(r + d * RPD + lrow - hy0) < (unsigned)hero_w) w[d] = (w[d] & ~hmask) | hblack;
     }
+    if (fov) {  // FovRenderer.apply_mask (fov.py:96-99): black corner triangles (uniform branch)
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        const uint32_t fm = fov[(vo >> 2) + 64 * d];
+        w[d] = (w[d] & ~fm) | (fm & (CBEV_PX_BLACK * 0x01010101u));
+      }
+    }
     if (CBEV_RASTER_PHASES & 8) {
       for (int k = 0; k < nout; ++k) {
         uint8_t* ob = out + (int64_t)k * out_stride;
@@ -870,13 +878,13 @@ __device__ __forceinline__ void raster_out(const cbev_params& P, const RotSetup&
 template <int G>
 __device__ __forceinline__ void raster_out_dispatch(const cbev_params& P, const RotSetup& R, bool fast,
                                                     const uint8_t* lds, int shift, uint32_t bg, uint8_t* out, int nout,
-                                                    int64_t out_stride, int lane, int wave) {
+                                                    int64_t out_stride, int lane, int wave, const uint32_t* fov) {
   if (R.r90) {
-    if (fast) raster_out<G, true, false>(P, R, lds, shift, bg, out, nout, out_stride, lane, wave);
-    else      raster_out<G, true, true>(P, R, lds, shift, bg, out, nout, out_stride, lane, wave);
+    if (fast) raster_out<G, true, false>(P, R, lds, shift, bg, out, nout, out_stride, lane, wave, fov);
+    else      raster_out<G, true, true>(P, R, lds, shift, bg, out, nout, out_stride, lane, wave, fov);
   } else {
-    if (fast) raster_out<G, false, false>(P, R, lds, shift, bg, out, nout, out_stride, lane, wave);
-    else      raster_out<G, false, true>(P, R, lds, shift, bg, out, nout, out_stride, lane, wave);
+    if (fast) raster_out<G, false, false>(P, R, lds, shift, bg, out, nout, out_stride, lane, wave, fov);
+    else      raster_out<G, false, true>(P, R, lds, shift, bg, out, nout, out_stride, lane, wave, fov);
   }
 }
 
@@ -1046,7 +1054,7 @@ __device__ __forceinline__ void raster_env(const KArgs& K, const DRec& r, uint8_
 
   // ---- rotate (pygame transform.rotate / rotate90) + compose + ego overlay
   const uint32_t bg = lds_nib(lds, shift);  // crop top-left pixel after painting
-  if (CBEV_RASTER_PHASES & 32) raster_out_dispatch<G>(P, R, fast, lds, shift, bg, out, nout, out_stride, lane, wave);
+  if (CBEV_RASTER_PHASES & 32) raster_out_dispatch<G>(P, R, fast, lds, shift, bg, out, nout, out_stride, lane, wave, K.fov);
 }
 
 // G = size / 64 (64-pixel gathers per output row)
@@ -1730,6 +1738,25 @@ __global__ __launch_bounds__(256) void k_expand_rgb(const uint8_t* __restrict__ 
   }
 }
 
+// obs_mode "vector" (carlabev.py:237-244): float32 [x, y, yaw, v] of the hero
+// (State.state, state.py:53-60) + set_point [cx, cy, cyaw][target_idx]
+// (stanley_controller.py:140-148), one thread per env.
+__global__ __launch_bounds__(256) void k_vector_obs(KArgs K, const uint8_t* __restrict__ recs, int n,
+                                                    float* __restrict__ out) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= n) return;
+  const DRec r = bind_rec((uint8_t*)recs + (int64_t)e * K.L.record_bytes, K.L, K.C);
+  const int t = r.hi[CBEV_HI_TIDX];
+  float* o = out + (int64_t)e * 7;
+  o[0] = (float)r.hd[CBEV_HD_X];
+  o[1] = (float)r.hd[CBEV_HD_Y];
+  o[2] = (float)r.hd[CBEV_HD_YAW];
+  o[3] = (float)r.hd[CBEV_HD_V];
+  o[4] = (float)r.cx[t];
+  o[5] = (float)r.cy[t];
+  o[6] = (float)r.cyaw[t];
+}
+
 // ---------------------------------------------------------------- resize
 // gymnasium ResizeObservation (cv2.resize INTER_AREA, opencv 4.11
 // imgproc/src/resize.cpp ResizeArea_Invoker / resizeAreaFast) of the RGB
@@ -1857,6 +1884,7 @@ struct cbev_ctx {
   int obs_h, obs_w;   // wrapped frame size (ResizeObservation); == size when not resizing
   void* area_dev;     // INTER_AREA tables of cbev_set_obs_size
   AreaTab area;
+  uint8_t* fov_dev;   // cbev_set_fov_mask
 };
 
 // envs per workgroup for a staged kernel: the largest divisor of 64 whose
@@ -1953,6 +1981,7 @@ static KArgs kargs(const cbev_ctx* c) {
   K.L = c->L;
   K.map = c->map_dev;
   K.npitch = c->npitch;
+  K.fov = (const uint32_t*)c->fov_dev;
   return K;
 }
 
@@ -2093,6 +2122,7 @@ void cbev_destroy(cbev_ctx* c) {
   if (c->map_dev) (void)hipFree(c->map_dev);
   if (c->lut_dev) (void)hipFree(c->lut_dev);
   if (c->area_dev) (void)hipFree(c->area_dev);
+  if (c->fov_dev) (void)hipFree(c->fov_dev);
   free(c);
 }
 
@@ -2304,6 +2334,34 @@ static void area_tab(int ssize, int dsize, double scale, std::vector<int32_t>& o
     }
   }
   off[dsize] = (int32_t)si.size();
+}
+
+int cbev_vector_obs(cbev_ctx* c, const void* records, int n, float* out, void* stream) {
+  if (!c || !records || !out) return set_err(CBEV_EINVAL, "null argument");
+  if (n <= 0) return CBEV_OK;
+  hipLaunchKernelGGL(k_vector_obs, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, kargs(c),
+                     (const uint8_t*)records, n, out);
+  HIP_TRY(hipGetLastError());
+  return CBEV_OK;
+}
+
+int cbev_set_fov_mask(cbev_ctx* c, const uint8_t* mask_host) {
+  if (!c) return set_err(CBEV_EINVAL, "null argument");
+  const size_t SS = (size_t)c->P.size * c->P.size;
+  HIP_TRY(hipSetDevice(c->device));
+  if (!mask_host) {
+    if (c->fov_dev) {
+      HIP_TRY(hipDeviceSynchronize());  // queued raster launches may still read it
+      (void)hipFree(c->fov_dev);
+      c->fov_dev = nullptr;
+    }
+    return CBEV_OK;
+  }
+  for (size_t i = 0; i < SS; ++i)
+    if (mask_host[i] != 0 && mask_host[i] != 0xff) return set_err(CBEV_EINVAL, "mask bytes must be 0 or 0xff");
+  if (!c->fov_dev) HIP_TRY(hipMalloc(&c->fov_dev, SS));
+  HIP_TRY(hipMemcpy(c->fov_dev, mask_host, SS, hipMemcpyHostToDevice));
+  return CBEV_OK;
 }
 
 int cbev_set_obs_size(cbev_ctx* c, int h, int w) {

@@ -25,6 +25,7 @@ struct KArgs {
   const uint8_t* map;  // padded class map, nibble-packed: render_h rows x npitch bytes,
                        // texel x of a row in byte x >> 1, high nibble when x is odd
   int npitch;
+  const uint32_t* fov;  // FOV corner mask, S*S bytes (0xff = black), or null (fov_masked off)
 };
 
 // class id of padded-map texel (x, y)

@@ -36,6 +36,7 @@ from .host_reset import HostResetBuilder, route_length_m
 from .scene_gen import SceneGenerator
 from .semantics import gray_lut, rgb_lut, semantic_lut, semantic_mask_channels, PALETTE
 from . import obs_pipeline as OP
+from .fov_mask import fov_corner_mask
 from .spaces import batch_space, make_box, make_discrete
 
 DEFAULT_CAPS = dict(route_cap=128, actor_cap=32, actor_route_cap=64, tl_cap=4)
@@ -58,20 +59,23 @@ class CarlaBEVVectorEnv:
     metadata = {"autoreset_mode": "disabled", "render_modes": ["rgb_array"], "render_fps": 60}
 
     def __init__(self, cfg, *, num_envs: int | None = None, device=None, caps: dict | None = None,
-                 info_mode: str = "full", scene_generator=None):
-        if isinstance(cfg, EnvConfig):
-            run = validate_run_config({"env": cfg})
-        elif isinstance(cfg, RunConfig):
-            run = validate_run_config(cfg)
+                 info_mode: str = "full", scene_generator=None, wrappers: bool = True):
+        """wrappers=False gives the base `CarlaBEV` observation of every env, as a
+        `SyncVectorEnv` of unwrapped `CarlaBEV(cfg)` would: (S, S, 3) uint8 RGB for the
+        BEV modes, float32[7] for obs_mode="vector" (carlabev.py:233-244, spaces.py:54-61).
+        The reference only allows "vector" on the bare env (config/env.py:310-314)."""
+        if isinstance(cfg, RunConfig):
+            raw = cfg
         elif isinstance(cfg, dict) and "env" in cfg:
-            run = validate_run_config(cfg)
+            raw = cfg
         else:
-            run = validate_run_config({"env": cfg})
+            raw = {"env": cfg}
+        run = validate_run_config(raw) if wrappers else (
+            raw if isinstance(raw, RunConfig) else RunConfig.model_validate(dict(raw)))
+        self.wrappers = bool(wrappers)
         self.run_cfg = run
         self.cfg: EnvConfig = run.env
         self.num_envs = int(num_envs if num_envs is not None else run.num_envs)
-        if self.cfg.fov_masked:
-            raise NotImplementedError("fov_masked=True is not implemented on the device yet")
         self.info_mode = info_mode
         if device is None:
             if not torch.cuda.is_available():
@@ -79,7 +83,7 @@ class CarlaBEVVectorEnv:
             device = torch.device("cuda", torch.cuda.current_device())
         self.device = torch.device(device)
         self.S = int(self.cfg.size)
-        self.F = int(self.cfg.frame_stack)
+        self.F = int(self.cfg.frame_stack) if self.wrappers else 1
         self.classes = load_class_map(self.cfg.map_name, self.S)
         self.params: CbevParams = build_params(self.cfg, self.classes)
         self.map_host, pitch = padded_map(self.classes, self.params.pad)
@@ -97,11 +101,14 @@ class CarlaBEVVectorEnv:
                             ctypes.byref(ctx)), "cbev_create")
         self._ctx = ctx
         check(L.cbev_set_map(ctx, self.map_host.ctypes.data_as(ctypes.c_void_p), self.map_host.nbytes), "cbev_set_map")
+        if self.cfg.fov_masked:  # FovRenderSpec(mask_fov=fov_masked), world.py:40-46
+            self.fov_mask = fov_corner_mask(self.cfg.size)
+            check(L.cbev_set_fov_mask(ctx, self.fov_mask.ctypes.data_as(ctypes.c_void_p)), "cbev_set_fov_mask")
         N, S, F = self.num_envs, self.S, self.F
         dev = self.device
         # ResizeObservation(obs_size) (envs/__init__.py:62): frames are rendered at S x S and
         # resized on the device into the (h, w) frame ring
-        self.obs_hw = (int(self.cfg.obs_size[0]), int(self.cfg.obs_size[1]))
+        self.obs_hw = (int(self.cfg.obs_size[0]), int(self.cfg.obs_size[1])) if self.wrappers else (S, S)
         self.resize = self.obs_hw != (S, S)
         if self.resize:
             check(L.cbev_set_obs_size(ctx, self.obs_hw[0], self.obs_hw[1]), "cbev_set_obs_size")
@@ -125,7 +132,14 @@ class CarlaBEVVectorEnv:
         else:
             self.single_action_space = make_box(np.asarray(aspec["low"], np.float32),
                                                 np.asarray(aspec["high"], np.float32), (3,), np.float32)
-        if self.cfg.masked:
+        if not self.wrappers:
+            if self.cfg.obs_mode == "vector":
+                self.single_observation_space = make_box(-np.inf, np.inf, (7,), np.float32)
+                self.obs_buf = torch.zeros((N, 7), dtype=torch.float32, device=dev)
+            else:
+                self.single_observation_space = make_box(0, 255, (S, S, 3), np.uint8)
+                self.obs_buf = torch.zeros((N, S, S, 3), dtype=torch.uint8, device=dev)
+        elif self.cfg.masked:
             self.channels = semantic_mask_channels(self.cfg.semantic_mask_ch)
             C = len(self.channels)
             fusion = self.cfg.temporal_fusion_mode
@@ -308,6 +322,15 @@ class CarlaBEVVectorEnv:
         return obs, rew, term, trunc, infos
 
     def _obs(self):
+        if not self.wrappers:
+            if self.cfg.obs_mode == "vector":
+                check(lib().cbev_vector_obs(self._ctx, _ptr(self.records), self.num_envs, _ptr(self.obs_buf),
+                                            self._stream()), "cbev_vector_obs")
+            else:
+                check(lib().cbev_expand_obs(self._ctx, _ptr(self.frames()[None]), self.num_envs, 1, 0, 2, 3,
+                                            rgb_lut().ctypes.data_as(ctypes.c_void_p), _ptr(self.obs_buf),
+                                            self._stream()), "cbev_expand_obs")
+            return self.obs_buf
         check(lib().cbev_expand_obs(self._ctx, _ptr(self.ring), self.num_envs, self.F, self.head, self._obs_kind,
                                     self._obs_ch, self._obs_lut.ctypes.data_as(ctypes.c_void_p), _ptr(self.obs_buf),
                                     self._stream()), "cbev_expand_obs")

@@ -107,6 +107,18 @@ int cbev_reset_frames(cbev_ctx* ctx, void* records, int n, const void* bank, int
 int cbev_expand_obs(cbev_ctx* ctx, const uint8_t* ring, int n, int n_frames, int head, int kind, int n_channels,
                     const uint32_t* channel_lut_host, void* out, void* stream);
 
+/* obs_mode "vector" (CarlaBEV.render, carlabev.py:237-244): out = float32[n][7],
+ * [x, y, yaw, v] of the hero state + its Stanley set point [cx, cy, cyaw] at
+ * target_idx (stanley_controller.py:140-148), from the records as they are now. */
+int cbev_vector_obs(cbev_ctx* ctx, const void* records, int n, float* out, void* stream);
+
+/* EnvConfig.fov_masked: FovRenderer's static corner mask (envs/fov.py:46-68,96-99)
+ * applied by the raster (step and reset frames) after compose, before the ego
+ * overlay. mask_host = uint8[S][S], 0xff where the output is blacked out, 0
+ * elsewhere (carlabev_env_amd/fov_mask.py builds pygame's polygon fill); NULL
+ * turns the mask off. Not stream-ordered: call it before queuing work. */
+int cbev_set_fov_mask(cbev_ctx* ctx, const uint8_t* mask_host);
+
 /* ResizeObservation(obs_size) (gymnasium; cv2.resize INTER_AREA) between the
  * render and the mask / grayscale wrappers (envs/__init__.py:62-67). Sets the
  * wrapped frame size h x w (<= size; h == w == size turns resizing off) and

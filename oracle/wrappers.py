@@ -191,3 +191,62 @@ def wrap_obs_stack(id_frames: np.ndarray, obs_mode: str, mode: str = "6-class", 
     if fusion == "vehicle_weighted":
         return fuse_weighted_vehicle(stacked, mode)
     return flatten_stacked_frames(stacked)
+
+
+# ---------------------------------------------------------------- FOV corner mask
+def _fillpoly(mask: np.ndarray, px, py) -> None:
+    """pygame 2.6.1 src_c/draw.c draw_fillpoly (scanline fill, clipped to the surface):
+    per scanline, intersections with the non-horizontal edges (y1 <= y < y2, or the
+    last line), floor for even / ceil for odd intersection counts, sorted, filled in
+    pairs; then horizontal border edges strictly between miny and maxy."""
+    H, Wd = mask.shape
+    n = len(px)
+
+    def hline(x1, y, x2):
+        if not 0 <= y < H:
+            return
+        a, b = max(min(x1, x2), 0), min(max(x1, x2), Wd - 1)
+        if a <= b:
+            mask[y, a:b + 1] = True
+
+    miny, maxy = min(py), max(py)
+    if miny == maxy:  # one pixel high: a line from the leftmost to the rightmost point
+        hline(min(px), miny, max(px))
+        return
+    for y in range(miny, maxy + 1):
+        xs = []
+        for i in range(n):
+            ip = i - 1 if i else n - 1
+            y1, y2 = py[ip], py[i]
+            if y1 < y2:
+                x1, x2 = px[ip], px[i]
+            elif y1 > y2:
+                y2, y1 = py[ip], py[i]
+                x2, x1 = px[ip], px[i]
+            else:
+                continue
+            if (y1 <= y < y2) or (y == maxy and y2 == maxy):
+                t = np.float32((y - y1) * (x2 - x1) / np.float32(y2 - y1))
+                t = np.float32(math.floor(t)) if len(xs) % 2 == 0 else np.float32(math.ceil(t))
+                xs.append(int(t) + x1)
+        xs.sort()
+        for k in range(0, len(xs) - 1, 2):
+            hline(xs[k], y, xs[k + 1])
+    for i in range(n):
+        ip = i - 1 if i else n - 1
+        y = py[i]
+        if miny < y < maxy and py[ip] == y:
+            hline(px[i], y, px[ip])
+
+
+def fov_mask(size: int, mask_frac: float = 0.5) -> np.ndarray:
+    """FovRenderer._build_mask_surface (envs/fov.py:46-68): four opaque corner
+    triangles of leg m = int(size * mask_frac); apply_mask (fov.py:96-99) blits
+    them black onto the composed output before the ego is drawn (world.py:137-157).
+    Returns the (size, size) bool mask. Parity unpinned (pygame is not installed)."""
+    S, m = size, int(size * mask_frac)
+    mask = np.zeros((S, S), bool)
+    for pts in ([(0, 0), (m, 0), (0, m)], [(S, 0), (S - m, 0), (S, m)], [(0, S), (0, S - m), (m, S)],
+                [(S, S), (S - m, S), (S, S - m)]):
+        _fillpoly(mask, [p[0] for p in pts], [p[1] for p in pts])
+    return mask

@@ -58,7 +58,7 @@ def compare_records(a: np.ndarray, b: np.ndarray, layout, tag=""):
 
 
 def run_parity(kinds, n_envs, steps, size=128, profile="discrete9_v1", reward="carl_base_v1", seed0=0, anchor_y=0.5,
-               act_seed=1234, edit=None):
+               act_seed=1234, edit=None, fov=False):
     cfg, P, padded, layout, builder = world(size, profile, reward, anchor_y)
     recs, _ = build_records(builder, n_envs, kinds, seed0=seed0)
     if edit is not None:  # hand-made states on top of the seeded scenes
@@ -66,6 +66,13 @@ def run_parity(kinds, n_envs, steps, size=128, profile="discrete9_v1", reward="c
     dw = DevWorld(P, padded, CAPS_FULL)
     L = lib()
     S = P.size
+    omask = None
+    if fov:  # device: the product's mask; oracle: its own restatement, blacked out after the render
+        import wrappers as W
+        from carlabev_env_amd.fov_mask import fov_corner_mask
+        dmask = fov_corner_mask(S)
+        check(L.cbev_set_fov_mask(dw.ctx, dmask.ctypes.data_as(P_)), "fov")
+        omask = W.fov_mask(S)
     d_recs = torch.from_numpy(recs.copy()).cuda()
     d_frames = torch.zeros((n_envs, S, S), dtype=torch.uint8, device="cuda")
     check(L.cbev_reset(dw.ctx, ptr(d_recs), n_envs, None, 0, None, None, 0, ptr(d_frames), 1, None), "reset")
@@ -73,6 +80,8 @@ def run_parity(kinds, n_envs, steps, size=128, profile="discrete9_v1", reward="c
     h_frames = np.zeros((n_envs, S, S), np.uint8)
     for e in range(n_envs):
         orc.reset_obs(recs[e], h_frames[e])
+        if omask is not None:
+            h_frames[e][omask] = 8  # CBEV_PX_BLACK
     torch.cuda.synchronize()
     assert np.array_equal(d_frames.cpu().numpy(), h_frames), "reset frames differ"
     acts = action_stream(P, n_envs, steps, seed=act_seed)
@@ -88,6 +97,8 @@ def run_parity(kinds, n_envs, steps, size=128, profile="discrete9_v1", reward="c
                           ptr(cause), ptr(info), None), "step")
         for e in range(n_envs):
             orc.step_one(recs[e], np.ascontiguousarray(acts[t, e]), h_frames[e])
+            if omask is not None:
+                h_frames[e][omask] = 8  # CBEV_PX_BLACK
         torch.cuda.synchronize()
         df = d_frames.cpu().numpy()
         bad = np.argwhere(df != h_frames)
@@ -117,6 +128,12 @@ def test_parity_continuous_medium_config4():
 
 def test_parity_scenarios_size256_config5():
     run_parity(["mix3"], 24, 100, size=256, seed0=30_000)
+
+
+def test_parity_fov_masked():
+    """EnvConfig.fov_masked: corner triangles blacked out (fov.py:46-68,96-99), step and reset frames."""
+    run_parity(["rt_medium_v1"], 16, 40, seed0=77, fov=True)
+    run_parity(["mix3"], 8, 20, size=256, seed0=30_100, fov=True)
 
 
 def test_parity_shaping_reward_and_offcentre_anchor():

@@ -175,3 +175,34 @@ def test_vector_env_wrapped_obs_match_oracle(obs_mode, fusion, obs_size):
         hist.append(env.frames().cpu().numpy().copy())
         check_obs(obs)
     env.close()
+
+
+@pytest.mark.parametrize("obs_mode", ["vector", "bev_semantic"])
+def test_unwrapped_base_observations(obs_mode):
+    """wrappers=False: the base CarlaBEV observation (carlabev.py:233-244): RGB of the
+    frame, or float32 [x, y, yaw, v, cx, cy, cyaw][target_idx] for obs_mode="vector"."""
+    from carlabev_env_amd import EnvConfig, build_random_navigation_options, RandomNavigationReset
+    from carlabev_env_amd import layout as LY
+    from carlabev_env_amd.vector_env import CarlaBEVVectorEnv
+    cfg = EnvConfig(size=128, obs_size=(96, 96), render_mode="rgb_array", obs_mode=obs_mode, max_vehicles=8)
+    n = 5
+    env = CarlaBEVVectorEnv({"env": cfg, "num_envs": n}, wrappers=False)
+    expect = (7,) if obs_mode == "vector" else (128, 128, 3)
+    assert env.single_observation_space.shape == expect
+    obs, _ = env.reset(seed=4, options=build_random_navigation_options(
+        RandomNavigationReset(difficulty_id="rt_medium_v1")))
+    rng = np.random.default_rng(0)
+    for t in range(5):
+        o = obs.cpu().numpy()
+        if obs_mode == "vector":
+            recs = env.records_host()
+            for e in range(n):
+                v = LY.RecordView(recs[e], env.layout)
+                k = v.i("TIDX")
+                ref = np.array([v.h("X"), v.h("Y"), v.h("YAW"), v.h("V"), v.cx[k], v.cy[k], v.cyaw[k]],
+                               dtype=np.float32)
+                assert np.array_equal(o[e], ref), (t, e)
+        else:
+            assert np.array_equal(o, W.PALETTE[env.frames().cpu().numpy()])
+        obs, *_ = env.step(rng.integers(0, 9, n))
+    env.close()

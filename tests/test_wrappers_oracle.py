@@ -130,3 +130,15 @@ def test_resized_id_encoding_is_lossless_for_the_wrappers():
         m = lut[code]
         got = np.stack([((m >> c) & 1).astype(np.float32) for c in range(len(SM.semantic_mask_channels(mode)))])
         assert np.array_equal(got, W.rgb_to_semantic_mask(rgb, mode)), mode
+
+
+def test_fov_mask_product_matches_oracle_restatement():
+    from carlabev_env_amd.fov_mask import fov_corner_mask
+    for S in (64, 128, 256):
+        m = W.fov_mask(S)
+        assert np.array_equal(fov_corner_mask(S) == 0xFF, m)
+        # the four corners are masked, the ego anchor region is not
+        assert m[0, 0] and m[0, S - 1] and m[S - 1, 0] and m[S - 1, S - 1]
+        assert not m[S // 2 - 4:S // 2 + 4, S // 2 - 4:S // 2 + 4].any()
+        # symmetric under the square's reflections up to pygame's fill rounding: row/column counts agree
+        assert m.sum(axis=1)[:S // 4].tolist() == m.sum(axis=0)[:S // 4].tolist()
