@@ -24,15 +24,19 @@ is also what the GPU and the oracle are compared on.
 """
 from __future__ import annotations
 
+import os
+
 import hashlib
 import random
 from dataclasses import dataclass
 
 import numpy as np
+
 from scipy import ndimage
 from scipy.sparse import csr_matrix
 from scipy.sparse.csgraph import shortest_path
 
+from .authored import load_authored_scene, normalize_scenario_config, read_scene_file, scenario_options_from_config
 from .params import load_class_map
 from .scene_pack import ActorSpec, SceneSpec, TrafficLightSpec
 
@@ -356,6 +360,22 @@ class SceneGenerator:
     # ------------------------------------------------------------ dispatch
     def build_scene(self, options: dict, bundle: RNGBundle) -> SceneSpec:
         scene = options.get("scene", "rdm")
+        config_file = options.get("config_file")
+        if isinstance(scene, str) and scene.endswith(".json") and os.path.exists(scene):
+            config_file = scene
+        if config_file:  # authored scene / scenario config (scene_generator.py:98-138)
+            data = read_scene_file(config_file)
+            if "actors" in data:
+                spec, len_route, ctx = load_authored_scene(data, options)
+                # authored actors are built without np_rng in the reference (fresh-entropy
+                # spawn jitter); here they draw it from the scenario generator
+                spec.hero_rng_state = _rng_state(bundle.route_np_rng)
+                spec.actor_rng_state = _rng_state(bundle.scenario_np_rng)
+                spec.context = dict(ctx, scene=data.get("scenario_id") or data.get("scenario"),
+                                    config_file=config_file, len_route_px=len_route)
+                return spec
+            sub = scenario_options_from_config(normalize_scenario_config(data), options)
+            return self.build_scene(sub, bundle)
         if scene == "rdm":
             spec = self.generate_random(
                 options.get("num_vehicles", self.max_vehicles),
