@@ -316,28 +316,62 @@ __device__ __forceinline__ int d_rect_lo(double w, int pad, int size) { return (
 #define CBEV_RASTER_PHASES 63
 #endif
 
-// LDS image of the crop window, nibble-packed like the map: crop row r starts
-// at dword r * sd and holds the packed map bytes from xa = (xmin >> 1) & ~15 on,
-// so crop pixel (c, r) is nibble shift + c of the row (shift = xmin - 2 xa, 0..31),
-// i.e. "nibble address" r * 8 sd + shift + c: byte >> 1 of it, high nibble when odd.
-// sd = the dwords a row needs (31 + C nibbles), rounded up to odd so that
-// successive crop rows start in different LDS banks and gathers along a rotated
-// row spread over the banks at every angle. Rows are staged as 16-byte chunks
-// (the last one clipped to sd). 182 x 27 dwords = 19.7 KB at S=128: 8 workgroups
-// per CU.
-__host__ __device__ __forceinline__ int raster_stride_dwords(int C) { return ((C + 31 + 7) / 8) | 1; }
-__host__ __device__ __forceinline__ int raster_row_chunks(int C) { return (raster_stride_dwords(C) + 3) / 4; }
-// nibble-level helpers on the LDS image
-__device__ __forceinline__ uint32_t lds_nib(const uint8_t* lds, uint32_t na) {
-  return (lds[na >> 1] >> ((na & 1u) << 2)) & 15u;
+// LDS image of the crop window. Nibble layout (S >= 128), packed like the map:
+// crop row r starts at dword r * sd and holds the packed map bytes from
+// xa = (xmin >> 1) & ~15 on, so crop pixel (c, r) is texel shift + c of the row
+// (shift = xmin - 2 xa, 0..31), i.e. "nibble address" r * 8 sd + shift + c: byte
+// >> 1 of it, high nibble when odd. sd = the dwords a row needs (31 + C
+// nibbles), rounded up to odd so that successive crop rows start in different
+// LDS banks and gathers along a rotated row spread over the banks at every
+// angle. Rows are staged as 16-byte chunks of the packed map (the last one
+// clipped to sd).
+// Byte layout (S <= 64): the staging unpacks the nibbles, one texel per LDS byte,
+// so a gather is an address (row * sb + column, two SDWA ops on the 16.16
+// coordinates) and a byte read, without the nibble select. Texel address
+// = byte address r * 4 sd + shift + c; sd = dwords for 31 + C texels, odd.
+// At S=128 the byte image (182 x 55 dwords = 40 KB) leaves 4 workgroups per CU
+// instead of the nibble image's 8, and measured slower (37 vs 30 us per step
+// raster at 4096 envs) despite half the gather VALU: the raster needs the
+// occupancy to hide latency. S >= 128 keeps the nibble image.
+#ifndef CBEV_RASTER_BYTES_MAX  // largest S with the byte image (experiments: -DCBEV_RASTER_BYTES_MAX=128)
+#define CBEV_RASTER_BYTES_MAX 64
+#endif
+__host__ __device__ __forceinline__ constexpr bool raster_bytes(int S) { return S <= CBEV_RASTER_BYTES_MAX; }
+__host__ __device__ __forceinline__ int raster_stride_dwords(int S, int C) {
+  return raster_bytes(S) ? ((C + 31 + 3) / 4) | 1 : ((C + 31 + 7) / 8) | 1;
 }
-__device__ __forceinline__ void lds_set_nib(uint8_t* lds, uint32_t na, uint32_t col) {
-  uint32_t* w = (uint32_t*)lds + (na >> 3);
-  const uint32_t sh = (na & 7u) << 2;
+// texels per LDS row (the row stride of texel addresses)
+__host__ __device__ __forceinline__ int raster_row_texels(int S, int C) {
+  return (raster_bytes(S) ? 4 : 8) * raster_stride_dwords(S, C);
+}
+// 16-byte chunks of the packed map per staged row (32 texels each)
+__host__ __device__ __forceinline__ int raster_row_chunks(int S, int C) {
+  return raster_bytes(S) ? (C + 31 + 31) / 32 : (raster_stride_dwords(S, C) + 3) / 4;
+}
+// texel-level helpers on the LDS image (texel address ta)
+template <bool BYTES>
+__device__ __forceinline__ uint32_t lds_texel(const uint8_t* lds, uint32_t ta) {
+  if (BYTES) return lds[ta];
+  return (lds[ta >> 1] >> ((ta & 1u) << 2)) & 15u;
+}
+template <bool BYTES>
+__device__ __forceinline__ void lds_set_texel(uint8_t* lds, uint32_t ta, uint32_t col) {
+  if (BYTES) {
+    lds[ta] = (uint8_t)col;
+    return;
+  }
+  uint32_t* w = (uint32_t*)lds + (ta >> 3);
+  const uint32_t sh = (ta & 7u) << 2;
   atomicAnd(w, ~(15u << sh));
   atomicOr(w, col << sh);
 }
-__host__ __device__ __forceinline__ int raster_image_bytes(int C) { return C * raster_stride_dwords(C) * 4; }
+__host__ __device__ __forceinline__ int raster_image_bytes(int S, int C) { return C * raster_stride_dwords(S, C) * 4; }
+// 8 packed texels (one map dword, texel 2k in the low nibble of byte k) -> 8 bytes
+__device__ __forceinline__ void unpack_texels(uint32_t w, uint32_t* o) {
+  const uint32_t lo = w & 0x0F0F0F0Fu, hi = (w >> 4) & 0x0F0F0F0Fu;
+  o[0] = __builtin_amdgcn_perm(hi, lo, 0x05010400u);
+  o[1] = __builtin_amdgcn_perm(hi, lo, 0x07030602u);
+}
 
 // Per-env rotation parameters (pygame transform.rotate, 16.16 fixed point;
 // rotate90 for exact multiples of 90 degrees) and the compose placement.
@@ -346,7 +380,7 @@ struct RotSetup {
   int nx, ny;                  // rotated surface size
   int isin, icos;              // 16.16 sin/cos
   int dx00, dy00;              // source 16.16 coordinates of rotated pixel (0, 0)
-  int a00, ustep, vstep;       // rotate90: LDS nibble address of rotated pixel (0,0) and its steps
+  int a00, ustep, vstep;       // rotate90: LDS texel address of rotated pixel (0,0) and its steps
   int rx0, ry0;                // rotated surface top-left in the output (get_rect(center=anchor))
 };
 
@@ -365,7 +399,7 @@ __device__ __forceinline__ RotSetup rot_setup(const cbev_params& P, float angle,
   if (R.r90) {
     int numturns = ((int)angle / 90) % 4;
     if (numturns < 0) numturns += 4;
-    // rotated pixel (xx, yy) reads LDS nibble a00 + xx*ustep + yy*vstep (rotate90 per turn count)
+    // rotated pixel (xx, yy) reads LDS texel a00 + xx*ustep + yy*vstep (rotate90 per turn count)
     switch (numturns) {
       case 0: R.a00 = 0;                     R.ustep = 1;   R.vstep = sb;  break;
       case 1: R.a00 = C - 1;                 R.ustep = sb;  R.vstep = -1;  break;
@@ -499,7 +533,7 @@ __device__ __forceinline__ bool raster_fast(const cbev_params& P, const RotSetup
 // The render set-up lives in the record's RS_* ints (written by k_hero, read by k_raster).
 __device__ __forceinline__ void d_store_render_setup(const cbev_params& P, int32_t* hi, double x, double y,
                                                      float angle) {
-  const RotSetup R = rot_setup(P, angle, 8 * raster_stride_dwords(P.crop));  // nibble row stride
+  const RotSetup R = rot_setup(P, angle, raster_row_texels(P.size, P.crop));
   int xm, ym;
   d_crop_origin(P, x, y, &xm, &ym);
   hi[CBEV_HI_RS_XMIN] = xm;
@@ -770,6 +804,7 @@ __device__ __forceinline__ void raster_out(const cbev_params& P, const RotSetup&
   constexpr int S = 64 * G;    // == P.size
   constexpr int LPR = S / 4;   // lanes per output row
   constexpr int RPD = 4 / G;   // output rows per dword group
+  constexpr bool BYTES = raster_bytes(S);
   const int C = P.crop;
   const uint32_t vmax = (uint32_t)((C << 16) - 1);
   const int hero_w = P.hero_w;
@@ -791,12 +826,13 @@ __device__ __forceinline__ void raster_out(const cbev_params& P, const RotSetup&
   // lane state at (output row r0 + lrow, column lcol) of this wave's first chunk
   int sx = R.dx00 + xx0 * R.icos - yy0 * R.isin;  // 16.16 source x (general)
   int sy = R.dy00 + xx0 * R.isin + yy0 * R.icos;  // 16.16 source y (general)
-  int sa = R.a00 + shift + xx0 * R.ustep + yy0 * R.vstep;  // LDS nibble address (rotate90)
-  // the crop's nibble offset rides in the integer part of sx, so the LDS byte is
-  // (sy >> 16) * sb + (sx >> 17) and the nibble (sx >> 16) & 1
+  int sa = R.a00 + shift + xx0 * R.ustep + yy0 * R.vstep;  // LDS texel address (rotate90)
+  // the crop's texel offset rides in the integer part of sx, so the LDS byte is
+  // (sy >> 16) * sb + (sx >> 16) (byte image) or (sy >> 16) * sb + (sx >> 17) with
+  // the nibble (sx >> 16) & 1 (nibble image)
   sx += shift << 16;
   const uint8_t* img = lds;
-  const uint32_t sb = 4u * (uint32_t)raster_stride_dwords(C);  // LDS bytes per crop row
+  const uint32_t sb = 4u * (uint32_t)raster_stride_dwords(S, C);  // LDS bytes per crop row
   const int chunk_rows = 4 * RPC;                 // the 4 waves interleave chunks
   const int nchunks = S / RPC;
   // general path: (sx, sy) packed in one 64-bit value, so one 64-bit add steps
@@ -824,23 +860,23 @@ __device__ __forceinline__ void raster_out(const cbev_params& P, const RotSetup&
           const int a = sa + d * RPD * R.vstep + b * R.ustep;
           if (CHECK) {
             const bool ok = ((xok >> b) & 1u) && (unsigned)(r + d * RPD + lrow - R.ry0) < (unsigned)R.ny;
-            v = ok ? lds_nib(img, ok ? a : 0) : (uint32_t)CBEV_PX_BLACK;
+            v = ok ? lds_texel<BYTES>(img, ok ? a : 0) : (uint32_t)CBEV_PX_BLACK;
           } else {
-            v = lds_nib(img, a);
+            v = lds_texel<BYTES>(img, a);
           }
         } else {
           const uint64_t q = b == 0 ? qg : qg + (uint64_t)b * col_step;
           const uint32_t dx = (uint32_t)q, dy = (uint32_t)(q >> 32);
-          const uint32_t byte = __umul24(dy >> 16, sb) + (dx >> 17);
-          const uint32_t nsh = (dx >> 14) & 4u;
+          const uint32_t byte = __umul24(dy >> 16, sb) + (BYTES ? (dx >> 16) : (dx >> 17));
+          const uint32_t nsh = BYTES ? 0u : (dx >> 14) & 4u;
           if (CHECK) {  // bounds on the unshifted source coordinate
             const int ux = (int)dx - (shift << 16);
             const bool ok = ((xok >> b) & 1u) && (unsigned)(r + d * RPD + lrow - R.ry0) < (unsigned)R.ny;
             const bool in = (uint32_t)ux <= vmax && dy <= vmax;
-            const uint32_t s = (img[(in && ok) ? byte : 0u] >> nsh) & 15u;
+            const uint32_t s = BYTES ? img[(in && ok) ? byte : 0u] : (img[(in && ok) ? byte : 0u] >> nsh) & 15u;
             v = !ok ? (uint32_t)CBEV_PX_BLACK : (in ? s : bg);
           } else {
-            v = (img[byte] >> nsh) & 15u;
+            v = BYTES ? img[byte] : (img[byte] >> nsh) & 15u;
           }
         }
         acc |= ((CBEV_RASTER_PHASES & 4) ? v : (uint32_t)(lane + b)) << (8 * b);
@@ -929,7 +965,8 @@ __device__ __forceinline__ PaintPre raster_paint_fetch(const DRec& r) {
 
 // one rect of side sz (rect_from_world_center, transforms.py:46-51) by the 4
 // threads of tid >> 2: thread tq covers columns tq, tq + 4, ...
-__device__ __forceinline__ void paint_rect4(uint8_t* lds, int sb, int shift, int C, int pad, int xmin, int ymin,
+template <bool BYTES>
+__device__ __forceinline__ void paint_rect4(uint8_t* lds, int rt, int shift, int C, int pad, int xmin, int ymin,
                                             double wx, double wy, int sz, int tq, uint32_t col) {
   const int rx = d_rect_lo(wx, pad, sz) - xmin, ry = d_rect_lo(wy, pad, sz) - ymin;
   for (int qy = 0; qy < sz; ++qy) {
@@ -937,36 +974,38 @@ __device__ __forceinline__ void paint_rect4(uint8_t* lds, int sb, int shift, int
     if (py < 0 || py >= C) continue;
     for (int qx = tq; qx < sz; qx += 4) {
       const int px = rx + qx;
-      if (px >= 0 && px < C) lds_set_nib(lds, py * 2 * sb + shift + px, col);
+      if (px >= 0 && px < C) lds_set_texel<BYTES>(lds, py * rt + shift + px, col);
     }
   }
 }
 
+template <bool BYTES>
 __device__ __forceinline__ void raster_paint(const KArgs& K, const DRec& r, const PaintPre& q, int xmin, int ymin,
                                              int shift, uint8_t* __restrict__ lds) {
   const cbev_params& P = K.P;
   const int C = P.crop;
-  const int sb = 4 * raster_stride_dwords(C);
+  const int rt = raster_row_texels(P.size, C);  // texels per LDS row
   const int k = threadIdx.x >> 2, tq = threadIdx.x & 3;
   if (CBEV_RASTER_PHASES & 2) {
     for (int pass = 0; pass < 2; ++pass) {  // vehicles, then pedestrians
       const int a0 = pass == 0 ? 0 : q.nveh, a1 = pass == 0 ? q.nveh : q.nact;
       if (a1 <= a0) continue;
       const uint32_t col = pass == 0 ? CBEV_PX_VEHICLE : CBEV_PX_PEDESTRIAN;
-      if (k >= a0 && k < a1) paint_rect4(lds, sb, shift, C, P.pad, xmin, ymin, q.ax, q.ay, q.asz, tq, col);
+      if (k >= a0 && k < a1) paint_rect4<BYTES>(lds, rt, shift, C, P.pad, xmin, ymin, q.ax, q.ay, q.asz, tq, col);
       for (int a = 64 + k; a < a1; a += 64)  // more than 64 actors: fetched here
         if (a >= a0)
-          paint_rect4(lds, sb, shift, C, P.pad, xmin, ymin, RAD(r, CBEV_AD_X, a), RAD(r, CBEV_AD_Y, a),
-                      RAI(r, CBEV_AI_SIZE, a), tq, col);
+          paint_rect4<BYTES>(lds, rt, shift, C, P.pad, xmin, ymin, RAD(r, CBEV_AD_X, a), RAD(r, CBEV_AD_Y, a),
+                             RAI(r, CBEV_AI_SIZE, a), tq, col);
       __syncthreads();
     }
     const int nt = q.nt;
     // checkpoints 2x2, goal 4x4 (scenes/utils.py:114-122)
-    if (k < nt && q.tvis) paint_rect4(lds, sb, shift, C, P.pad, xmin, ymin, q.tx, q.ty, k < nt - 1 ? 2 : 4, tq,
-                                      CBEV_PX_ROUTE);
+    if (k < nt && q.tvis)
+      paint_rect4<BYTES>(lds, rt, shift, C, P.pad, xmin, ymin, q.tx, q.ty, k < nt - 1 ? 2 : 4, tq, CBEV_PX_ROUTE);
     for (int i = 64 + k; i < nt; i += 64)
       if ((r.vis[i >> 5] >> (i & 31)) & 1u)
-        paint_rect4(lds, sb, shift, C, P.pad, xmin, ymin, r.cx[i], r.cy[i], i < nt - 1 ? 2 : 4, tq, CBEV_PX_ROUTE);
+        paint_rect4<BYTES>(lds, rt, shift, C, P.pad, xmin, ymin, r.cx[i], r.cy[i], i < nt - 1 ? 2 : 4, tq,
+                           CBEV_PX_ROUTE);
     __syncthreads();
     for (int t = 0; t < q.ntl; ++t) {  // traffic lights one at a time (colours may differ)
       const int rx = r.ti[CBEV_TI_RX * r.T + t] - xmin, ry = r.ti[CBEV_TI_RY * r.T + t] - ymin;
@@ -975,7 +1014,7 @@ __device__ __forceinline__ void raster_paint(const KArgs& K, const DRec& r, cons
       for (int qy = threadIdx.x >> 4; qy < rh; qy += 16)
         for (int qx = threadIdx.x & 15; qx < rw; qx += 16) {
           const int px = rx + qx, py = ry + qy;
-          if (px >= 0 && py >= 0 && px < C && py < C) lds_set_nib(lds, py * 2 * sb + shift + px, col);
+          if (px >= 0 && py >= 0 && px < C && py < C) lds_set_texel<BYTES>(lds, py * rt + shift + px, col);
         }
       __syncthreads();
     }
@@ -987,12 +1026,14 @@ __device__ __forceinline__ void raster_env(const KArgs& K, const DRec& r, uint8_
                                            int64_t out_stride, uint8_t* __restrict__ lds) {
   const cbev_params& P = K.P;
   const int C = P.crop;
-  const int sd = raster_stride_dwords(C), sb = 4 * sd;
+  constexpr bool BYTES = raster_bytes(64 * G);
+  const int sd = raster_stride_dwords(64 * G, C);
+  const int rt = raster_row_texels(64 * G, C);
   int xmin, ymin;
   RotSetup R;
   if (RESET) {  // BaseMap.reset: theta 0 -> rotate90 by one turn, crop at the bank record's pose
     d_crop_origin(P, r.hd[CBEV_HD_X], r.hd[CBEV_HD_Y], &xmin, &ymin);
-    R = rot_setup(P, 90.0f, 2 * sb);  // nibble row stride
+    R = rot_setup(P, 90.0f, rt);
   } else if (CBEV_RASTER_PHASES & 16) {  // written by k_hero for this step
     xmin = r.hi[CBEV_HI_RS_XMIN];
     ymin = r.hi[CBEV_HI_RS_YMIN];
@@ -1001,12 +1042,12 @@ __device__ __forceinline__ void raster_env(const KArgs& K, const DRec& r, uint8_
     for (int k = 0; k < CBEV_RS_WORDS; ++k) w[k] = r.hi[CBEV_HI_RS_R90 + k];
   } else {  // (phase experiments only) a fixed pose, no record read
     xmin = ymin = 1000;
-    R = rot_setup(P, 90.0f, 2 * sb);
+    R = rot_setup(P, 90.0f, rt);
   }
   const bool fast = (!RESET && (CBEV_RASTER_PHASES & 16)) ? r.hi[CBEV_HI_RS_FAST] != 0 : raster_fast(P, R);
   PaintPre pq{};
   if (!RESET && (CBEV_RASTER_PHASES & 2)) pq = raster_paint_fetch(r);
-  const int xa = (xmin >> 1) & ~15, shift = xmin - 2 * xa;  // packed byte column, nibble offset
+  const int xa = (xmin >> 1) & ~15, shift = xmin - 2 * xa;  // packed byte column, texel offset (0..31)
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
 
@@ -1014,7 +1055,7 @@ __device__ __forceinline__ void raster_env(const KArgs& K, const DRec& r, uint8_
   // the window's row chunks, all of a batch in flight), then dword LDS stores
   if (CBEV_RASTER_PHASES & 1) {
     constexpr int U = 5;  // chunks in flight per thread (one batch covers size 128)
-    const int nch = raster_row_chunks(C), total = C * nch;
+    const int nch = raster_row_chunks(64 * G, C), total = C * nch;
     const uint8_t* gbase = K.map + (int64_t)ymin * K.npitch + xa;
     const int dr = 256 / nch, dj = 256 - dr * nch;
     int row = threadIdx.x / nch, j = threadIdx.x - row * nch;
@@ -1032,11 +1073,23 @@ __device__ __forceinline__ void raster_env(const KArgs& K, const DRec& r, uint8_
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         if (q0 + 256 * u + (int)threadIdx.x < total) {
-          uint32_t* d = l32 + row * sd + 4 * j;
-          d[0] = v[u].x;
-          d[1] = v[u].y;
-          d[2] = v[u].z;
-          if (4 * j + 3 < sd) d[3] = v[u].w;  // the last chunk of a row may overhang the stride
+          if (BYTES) {  // 32 texels -> 8 dwords; the last chunk of a row may overhang the stride
+            uint32_t* d = l32 + row * sd + 8 * j;
+            uint32_t o[8];
+            unpack_texels(v[u].x, o);
+            unpack_texels(v[u].y, o + 2);
+            unpack_texels(v[u].z, o + 4);
+            unpack_texels(v[u].w, o + 6);
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+              if (8 * j + k < sd) d[k] = o[k];
+          } else {
+            uint32_t* d = l32 + row * sd + 4 * j;
+            d[0] = v[u].x;
+            d[1] = v[u].y;
+            d[2] = v[u].z;
+            if (4 * j + 3 < sd) d[3] = v[u].w;  // the last chunk of a row may overhang the stride
+          }
         }
         row += dr;
         j += dj;
@@ -1048,12 +1101,12 @@ __device__ __forceinline__ void raster_env(const KArgs& K, const DRec& r, uint8_
 
   if (!RESET) {
     CBEV_STAMP(2, 1);
-    raster_paint(K, r, pq, xmin, ymin, shift, lds);
+    raster_paint<BYTES>(K, r, pq, xmin, ymin, shift, lds);
     CBEV_STAMP(2, 2);
   }
 
   // ---- rotate (pygame transform.rotate / rotate90) + compose + ego overlay
-  const uint32_t bg = lds_nib(lds, shift);  // crop top-left pixel after painting
+  const uint32_t bg = lds_texel<BYTES>(lds, shift);  // crop top-left pixel after painting
   if (CBEV_RASTER_PHASES & 32) raster_out_dispatch<G>(P, R, fast, lds, shift, bg, out, nout, out_stride, lane, wave, K.fov);
 }
 
@@ -1995,7 +2048,7 @@ static const void* bank_frames_kernel(int size) {
 static const void* reset_kernel(int size) {
   return size == 64 ? (const void*)k_reset<1> : size == 128 ? (const void*)k_reset<2> : (const void*)k_reset<4>;
 }
-static size_t raster_lds_bytes(const cbev_params& P) { return (size_t)raster_image_bytes(P.crop); }
+static size_t raster_lds_bytes(const cbev_params& P) { return (size_t)raster_image_bytes(P.size, P.crop); }
 
 extern "C" {
 
