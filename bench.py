@@ -105,27 +105,57 @@ def build_env(cfgd, n, rank, device):
 
 
 def cpu_baseline(cfgd, host_recs, env, seconds):
-    """Reference-semantics CPU oracle (single thread) on a bounded sample of the
-    same workload: first 64 envs, same scenes and action streams."""
+    """Reference-semantics CPU oracle on a bounded sample of the same workload
+    (same scenes, same action streams), timed two ways as SURVEY.md §8(d) asks:
+    (i) one thread stepping 64 envs (the reference's SyncVectorEnv model) and
+    (ii) one thread per usable host core (os.sched_getaffinity, capped at 16 =
+    the GPU box's CPU share), each stepping its own 64-env block. ctypes drops
+    the GIL inside orc_step_batch, so the threads run in parallel. `value` is
+    leg (ii); leg (i) is reported beside it."""
+    import threading
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle as O
     P = env.params
-    n = min(64, host_recs.shape[0])
-    recs = host_recs[:n].copy()
-    orc = O.Oracle(P, env.map_host, env.caps.c(), env.rb)
-    frames = np.zeros((n, P.size, P.size), np.uint8)
-    acts = make_actions(P, n, 4000, cfgd["act_seed"], 0)
-    steps = 0
-    t0 = time.perf_counter()
-    t = 0
-    while time.perf_counter() - t0 < seconds and t < acts.shape[0]:
-        orc.step(recs, n, np.ascontiguousarray(acts[t]), frames)
-        steps += n
-        t += 1
-    dt = time.perf_counter() - t0
-    return {"value": steps / dt, "unit": "env-steps/s", "cores": 1, "kind": "port",
-            "sample": f"{n} envs x {t} steps of the same workload ({steps} env-steps, {dt:.1f}s), "
-                      "oracle/cbev_oracle.c single thread, per-step full padded-map restore as in scene.py:93"}
+    blk = min(64, host_recs.shape[0])
+    acts_all = None
+
+    def leg(threads, secs):
+        nonlocal acts_all
+        n_tot = min(blk * threads, host_recs.shape[0])
+        per = n_tot // threads
+        if acts_all is None or acts_all.shape[1] < n_tot:
+            acts_all = make_actions(P, n_tot, 4000, cfgd["act_seed"], 0)
+        counts = [0] * threads
+        stop = time.perf_counter() + secs
+
+        def work(k):
+            lo, hi = k * per, (k + 1) * per
+            recs = host_recs[lo:hi].copy()
+            orc = O.Oracle(P, env.map_host, env.caps.c(), env.rb)
+            frames = np.zeros((hi - lo, P.size, P.size), np.uint8)
+            t = 0
+            while time.perf_counter() < stop and t < acts_all.shape[0]:
+                orc.step(recs, hi - lo, np.ascontiguousarray(acts_all[t, lo:hi]), frames)
+                t += 1
+            counts[k] = t * (hi - lo)
+
+        t0 = time.perf_counter()
+        ths = [threading.Thread(target=work, args=(k,)) for k in range(threads)]
+        for th in ths:
+            th.start()
+        for th in ths:
+            th.join()
+        dt = time.perf_counter() - t0
+        return sum(counts) / dt, sum(counts), dt, per
+
+    v1, s1, d1, _ = leg(1, seconds / 3)
+    cores = max(1, min(16, len(os.sched_getaffinity(0))))
+    vm, sm, dm, per = leg(cores, 2 * seconds / 3) if cores > 1 else (v1, s1, d1, blk)
+    return {"value": vm, "unit": "env-steps/s", "cores": cores, "kind": "port",
+            "single_thread_value": v1,
+            "sample": f"{cores} threads x {per} envs of the same workload ({sm} env-steps in {dm:.1f}s); "
+                      f"single thread: {blk} envs ({s1} env-steps in {d1:.1f}s). oracle/cbev_oracle.c, "
+                      "per-step full padded-map restore as in scene.py:93"}
 
 
 def main():

@@ -34,7 +34,7 @@ int main() {
   hipFuncSetAttribute((const void*)k_spin, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   std::vector<unsigned long long> hs(2 * nwg);
   std::vector<unsigned> hid(nwg);
-  for (int bytes : {16384, 18432, 19456, 19656, 20000, 20224, 20480, 20481, 21504, 23040, 32768}) {
+  for (int bytes : {8192, 10240, 12288, 16384, 17408, 18200, 18432, 19456, 19656, 20000, 20224, 20480, 20481, 21504, 23040, 32768}) {
     int occ = -1;
     hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_spin, 256, bytes);
     hipLaunchKernelGGL(k_spin, dim3(nwg), dim3(256), bytes, 0, st, id, 2000);  // 20 us
