@@ -318,9 +318,9 @@ __device__ __forceinline__ int d_rect_lo(double w, int pad, int size) { return (
 
 // LDS image of the crop window. Nibble layout (S >= 128), packed like the map:
 // crop row r starts at dword r * sd and holds the packed map bytes from
-// xa = (xmin >> 1) & ~15 on, so crop pixel (c, r) is texel shift + c of the row
-// (shift = xmin - 2 xa, 0..31), i.e. "nibble address" r * 8 sd + shift + c: byte
-// >> 1 of it, high nibble when odd. sd = the dwords a row needs (31 + C
+// xa = (xmin >> 1) & ~3 on (dword-aligned), so crop pixel (c, r) is texel shift + c
+// of the row (shift = xmin - 2 xa, 0..7), i.e. "nibble address" r * 8 sd + shift + c:
+// byte >> 1 of it, high nibble when odd. sd = the dwords a row needs (7 + C
 // nibbles), rounded up to odd so that successive crop rows start in different
 // LDS banks and gathers along a rotated row spread over the banks at every
 // angle. Rows are staged as 16-byte chunks of the packed map (the last one
@@ -328,7 +328,11 @@ __device__ __forceinline__ int d_rect_lo(double w, int pad, int size) { return (
 // Byte layout (S <= 64): the staging unpacks the nibbles, one texel per LDS byte,
 // so a gather is an address (row * sb + column, two SDWA ops on the 16.16
 // coordinates) and a byte read, without the nibble select. Texel address
-// = byte address r * 4 sd + shift + c; sd = dwords for 31 + C texels, odd.
+// = byte address r * 4 sd + shift + c; sd = dwords for 7 + C texels, odd.
+// Rows are dword-aligned in the map (16-byte loads at 4-byte alignment), so a
+// row carries at most 7 texels of slack: 182 x 25 dwords = 18.2 KB at S=128,
+// which leaves room for k_step's per-env state within the 20 KB that keeps 8
+// workgroups per CU.
 // At S=128 the byte image (182 x 55 dwords = 40 KB) leaves 4 workgroups per CU
 // instead of the nibble image's 8, and measured slower (37 vs 30 us per step
 // raster at 4096 envs) despite half the gather VALU: the raster needs the
@@ -338,7 +342,7 @@ __device__ __forceinline__ int d_rect_lo(double w, int pad, int size) { return (
 #endif
 __host__ __device__ __forceinline__ constexpr bool raster_bytes(int S) { return S <= CBEV_RASTER_BYTES_MAX; }
 __host__ __device__ __forceinline__ int raster_stride_dwords(int S, int C) {
-  return raster_bytes(S) ? ((C + 31 + 3) / 4) | 1 : ((C + 31 + 7) / 8) | 1;
+  return raster_bytes(S) ? ((C + 7 + 3) / 4) | 1 : ((C + 7 + 7) / 8) | 1;
 }
 // texels per LDS row (the row stride of texel addresses)
 __host__ __device__ __forceinline__ int raster_row_texels(int S, int C) {
@@ -346,7 +350,13 @@ __host__ __device__ __forceinline__ int raster_row_texels(int S, int C) {
 }
 // 16-byte chunks of the packed map per staged row (32 texels each)
 __host__ __device__ __forceinline__ int raster_row_chunks(int S, int C) {
-  return raster_bytes(S) ? (C + 31 + 31) / 32 : (raster_stride_dwords(S, C) + 3) / 4;
+  return raster_bytes(S) ? (C + 7 + 31) / 32 : ((C + 7 + 7) / 8 + 3) / 4;
+}
+// 16 bytes at 4-byte alignment (crop rows start at a dword of the packed map)
+typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
+__device__ __forceinline__ uint4 load16_a4(const uint8_t* p) {
+  const u32x4_a4 t = *(const u32x4_a4*)p;
+  return make_uint4(t.x, t.y, t.z, t.w);
 }
 // texel-level helpers on the LDS image (texel address ta)
 template <bool BYTES>
@@ -583,11 +593,17 @@ struct HeroPre {
 // Ego update, part A (one thread per env): target index update, throttle /
 // brake, State.update, damping (BaseAgent.physics_step, hero.py:88-138).
 __device__ __forceinline__ void hero_env_a(const KArgs& K, DRec r, int e, const void* __restrict__ actions,
-                                           int bi, const HeroPre& hp) {
+                                           int bi, const HeroPre& hp, const float* gsb = nullptr) {
   double* hd = r.hd;
   int32_t* hi = r.hi;
   float g, sa, b;
-  d_decode_action(K, actions, e, &g, &sa, &b);
+  if (gsb) {  // decoded ahead (k_step)
+    g = gsb[0];
+    sa = gsb[1];
+    b = gsb[2];
+  } else {
+    d_decode_action(K, actions, e, &g, &sa, &b);
+  }
   hd[CBEV_HD_T] += CB_DT;  // Scene._t += dt (scene.py:91)
 
   double s[8];
@@ -595,7 +611,7 @@ __device__ __forceinline__ void hero_env_a(const KArgs& K, DRec r, int e, const 
   for (int k = 0; k < 8; ++k) s[k] = hd[CBEV_HD_X + k];
   // stanley_control's target search (bi: first arg-min, reduced by the workgroup);
   // its steering output is unused by the hero
-  hi[CBEV_HI_TIDX] = hi[CBEV_HI_TIDX] >= bi ? hi[CBEV_HI_TIDX] : bi;
+  if (bi >= 0) hi[CBEV_HI_TIDX] = hi[CBEV_HI_TIDX] >= bi ? hi[CBEV_HI_TIDX] : bi;  // bi < 0: k_step's search wave
   const double v = s[3];
   const int scale = K.P.scale;
   // BaseAgent.accelerate / steering / brake (hero.py:140-162)
@@ -679,6 +695,10 @@ __global__ __launch_bounds__(256) void k_hero(KArgs K, uint8_t* __restrict__ rec
   HeroPre* pre = (HeroPre*)(lds + ne * sbytes);  // [ne]
   int* best = (int*)(pre + ne);                   // [ne] Stanley target search result
   CBEV_STAMP(0, 0);
+  // the actions of this workgroup's envs, in flight with the record staging
+  // (wave 0 runs chain A, wave 1 the steering tangent)
+  float ag = 0.f, asa = 0.f, ab = 0.f;
+  if (wave <= 1 && lane < ne_eff) d_decode_action(K, actions, e0 + lane, &ag, &asa, &ab);
   stage_in(lds, recs, e0, ne_eff, rb, sbytes);
   __syncthreads();
   CBEV_STAMP(0, 1);
@@ -690,10 +710,8 @@ __global__ __launch_bounds__(256) void k_hero(KArgs K, uint8_t* __restrict__ rec
       pre[lane].cyaw = cos(hd[CBEV_HD_YAW]);
       pre[lane].syaw = sin(hd[CBEV_HD_YAW]);
     } else if (wave == 1) {
-      float g, sa, b;
-      d_decode_action(K, actions, e0 + lane, &g, &sa, &b);
       const double max_steer = 30.0 * (CB_PI / 180.0);
-      pre[lane].tdelta = tan(d_clip(d_hero_delta(hd[CBEV_HD_V], sa), -max_steer, max_steer));
+      pre[lane].tdelta = tan(d_clip(d_hero_delta(hd[CBEV_HD_V], asa), -max_steer, max_steer));
     }
   }
   __syncthreads();
@@ -752,7 +770,10 @@ __global__ __launch_bounds__(256) void k_hero(KArgs K, uint8_t* __restrict__ rec
   __syncthreads();
   CBEV_STAMP(3, 1);
   // A: the scalar chain, one thread per env
-  if (tid < ne_eff) hero_env_a(K, bind_rec(lds + tid * sbytes, K.L, K.C), e0 + tid, actions, best[tid], pre[tid]);
+  if (tid < ne_eff) {
+    const float gsb[3] = {ag, asa, ab};
+    hero_env_a(K, bind_rec(lds + tid * sbytes, K.L, K.C), e0 + tid, actions, best[tid], pre[tid], gsb);
+  }
   __syncthreads();
   CBEV_STAMP(3, 2);
   // B: comfort + dist2goal (wave 1) beside the render set-up (wave 2)
@@ -770,14 +791,16 @@ __global__ __launch_bounds__(256) void k_hero(KArgs K, uint8_t* __restrict__ rec
 // Scripted actors (ActorManager.step_all, actor_manager.py:111-119): one
 // wavefront per env, one lane per actor (vehicles then pedestrians). Runs after
 // k_hero, so the scene clock hd[T] is already advanced.
-__global__ __launch_bounds__(256) void k_actors(KArgs K, uint8_t* __restrict__ recs, int n) {
+// t_ahead = 1: launched before k_step, which advances the scene clock itself,
+// so the actors take hd[T] + dt (the same float64 sum k_step stores).
+__global__ __launch_bounds__(256) void k_actors(KArgs K, uint8_t* __restrict__ recs, int n, int t_ahead) {
   const int lane = threadIdx.x & 63;
   const int e = xcd_env4_of_wg(blockIdx.x, threadIdx.x >> 6, n);
   if (e >= n) return;
   DRec r = bind_rec(recs + (int64_t)e * K.L.record_bytes, K.L, K.C);
   const int nact = r.hi[CBEV_HI_NACT];
   if (nact == 0) return;
-  const double t = r.hd[CBEV_HD_T];
+  const double t = t_ahead ? r.hd[CBEV_HD_T] + CB_DT : r.hd[CBEV_HD_T];
   for (int a = lane; a < nact; a += 64) d_actor_step(r, a, t);
 }
 
@@ -795,7 +818,7 @@ __global__ __launch_bounds__(256) void k_actors(KArgs K, uint8_t* __restrict__ r
 //   the map is affine) -> no per-pixel tests.
 //   CHECK = true: compose clipping (black outside the rotated surface) and the
 //   rotozoom background test (bg outside the source), per pixel.
-template <int G, bool R90, bool CHECK>
+template <int G, bool R90, bool CHECK, int NW>
 __device__ __forceinline__ void raster_out(const cbev_params& P, const RotSetup& R, const uint8_t* __restrict__ lds,
                                            int shift, uint32_t bg, uint8_t* __restrict__ out, int nout,
                                            int64_t out_stride, int lane, int wave,
@@ -833,7 +856,7 @@ __device__ __forceinline__ void raster_out(const cbev_params& P, const RotSetup&
   sx += shift << 16;
   const uint8_t* img = lds;
   const uint32_t sb = 4u * (uint32_t)raster_stride_dwords(S, C);  // LDS bytes per crop row
-  const int chunk_rows = 4 * RPC;                 // the 4 waves interleave chunks
+  const int chunk_rows = NW * RPC;                // the NW output waves interleave chunks
   const int nchunks = S / RPC;
   // general path: (sx, sy) packed in one 64-bit value, so one 64-bit add steps
   // both coordinates (the low word stays in [0, 2^32): no carry crosses over)
@@ -843,7 +866,7 @@ __device__ __forceinline__ void raster_out(const cbev_params& P, const RotSetup&
   // one output row down: (dx, dy) += (-isin, icos); one column right: += (icos, isin)
   const uint64_t group_step = (uint64_t)(((int64_t)(RPD * R.icos) << 32) + (int64_t)(-RPD * R.isin));
   const uint64_t col_step = (uint64_t)(((int64_t)R.isin << 32) + (int64_t)R.icos);
-  for (int ch = wave, r = r0; ch < nchunks; ch += 4, r += chunk_rows) {
+  for (int ch = wave, r = r0; ch < nchunks; ch += NW, r += chunk_rows) {
     // the frame is written through the uniform base `out` plus a per-lane offset
     const uint32_t vo = (uint32_t)(r * S + 4 * lane);
     const bool hero_rows = (unsigned)(r + RPC - 1 - hy0) < (unsigned)(RPC - 1 + hero_w);  // chunk meets the hero rows
@@ -911,16 +934,16 @@ __device__ __forceinline__ void raster_out(const cbev_params& P, const RotSetup&
   }
 }
 
-template <int G>
+template <int G, int NW = 4>
 __device__ __forceinline__ void raster_out_dispatch(const cbev_params& P, const RotSetup& R, bool fast,
                                                     const uint8_t* lds, int shift, uint32_t bg, uint8_t* out, int nout,
                                                     int64_t out_stride, int lane, int wave, const uint32_t* fov) {
   if (R.r90) {
-    if (fast) raster_out<G, true, false>(P, R, lds, shift, bg, out, nout, out_stride, lane, wave, fov);
-    else      raster_out<G, true, true>(P, R, lds, shift, bg, out, nout, out_stride, lane, wave, fov);
+    if (fast) raster_out<G, true, false, NW>(P, R, lds, shift, bg, out, nout, out_stride, lane, wave, fov);
+    else      raster_out<G, true, true, NW>(P, R, lds, shift, bg, out, nout, out_stride, lane, wave, fov);
   } else {
-    if (fast) raster_out<G, false, false>(P, R, lds, shift, bg, out, nout, out_stride, lane, wave, fov);
-    else      raster_out<G, false, true>(P, R, lds, shift, bg, out, nout, out_stride, lane, wave, fov);
+    if (fast) raster_out<G, false, false, NW>(P, R, lds, shift, bg, out, nout, out_stride, lane, wave, fov);
+    else      raster_out<G, false, true, NW>(P, R, lds, shift, bg, out, nout, out_stride, lane, wave, fov);
   }
 }
 
@@ -1021,9 +1044,17 @@ __device__ __forceinline__ void raster_paint(const KArgs& K, const DRec& r, cons
   }
 }
 
-template <bool RESET, int G>
+struct NoSideWork {
+  __device__ void operator()(int) const {}
+};
+
+// NW < 4: waves NW..3 run `side(lane)` (k_step: the collision / reward pass)
+// while waves 0..NW-1 write the frame; every other LDS access of `side` must
+// stay outside the crop image.
+template <bool RESET, int G, int NW = 4, class Side = NoSideWork>
 __device__ __forceinline__ void raster_env(const KArgs& K, const DRec& r, uint8_t* __restrict__ out, int nout,
-                                           int64_t out_stride, uint8_t* __restrict__ lds) {
+                                           int64_t out_stride, uint8_t* __restrict__ lds,
+                                           const Side& side = Side()) {
   const cbev_params& P = K.P;
   const int C = P.crop;
   constexpr bool BYTES = raster_bytes(64 * G);
@@ -1047,7 +1078,7 @@ __device__ __forceinline__ void raster_env(const KArgs& K, const DRec& r, uint8_
   const bool fast = (!RESET && (CBEV_RASTER_PHASES & 16)) ? r.hi[CBEV_HI_RS_FAST] != 0 : raster_fast(P, R);
   PaintPre pq{};
   if (!RESET && (CBEV_RASTER_PHASES & 2)) pq = raster_paint_fetch(r);
-  const int xa = (xmin >> 1) & ~15, shift = xmin - 2 * xa;  // packed byte column, texel offset (0..31)
+  const int xa = (xmin >> 1) & ~3, shift = xmin - 2 * xa;  // packed byte column (dword), texel offset (0..7)
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
 
@@ -1065,7 +1096,7 @@ __device__ __forceinline__ void raster_env(const KArgs& K, const DRec& r, uint8_
       int r = row, c = j;
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        if (q0 + 256 * u + (int)threadIdx.x < total) v[u] = *(const uint4*)(gbase + (int64_t)r * K.npitch + 16 * c);
+        if (q0 + 256 * u + (int)threadIdx.x < total) v[u] = load16_a4(gbase + (int64_t)r * K.npitch + 16 * c);
         r += dr;
         c += dj;
         if (c >= nch) { c -= nch; ++r; }
@@ -1085,10 +1116,10 @@ __device__ __forceinline__ void raster_env(const KArgs& K, const DRec& r, uint8_
               if (8 * j + k < sd) d[k] = o[k];
           } else {
             uint32_t* d = l32 + row * sd + 4 * j;
-            d[0] = v[u].x;
-            d[1] = v[u].y;
-            d[2] = v[u].z;
-            if (4 * j + 3 < sd) d[3] = v[u].w;  // the last chunk of a row may overhang the stride
+            d[0] = v[u].x;  // the last chunk of a row may overhang the stride
+            if (4 * j + 1 < sd) d[1] = v[u].y;
+            if (4 * j + 2 < sd) d[2] = v[u].z;
+            if (4 * j + 3 < sd) d[3] = v[u].w;
           }
         }
         row += dr;
@@ -1107,7 +1138,11 @@ __device__ __forceinline__ void raster_env(const KArgs& K, const DRec& r, uint8_
 
   // ---- rotate (pygame transform.rotate / rotate90) + compose + ego overlay
   const uint32_t bg = lds_texel<BYTES>(lds, shift);  // crop top-left pixel after painting
-  if (CBEV_RASTER_PHASES & 32) raster_out_dispatch<G>(P, R, fast, lds, shift, bg, out, nout, out_stride, lane, wave, K.fov);
+  if (NW < 4 && wave >= NW) {
+    side(lane);
+  } else if (CBEV_RASTER_PHASES & 32) {
+    raster_out_dispatch<G, NW>(P, R, fast, lds, shift, bg, out, nout, out_stride, lane, wave, K.fov);
+  }
 }
 
 // G = size / 64 (64-pixel gathers per output row)
@@ -1227,24 +1262,44 @@ __device__ __forceinline__ double d_seg_dist2(const DRec& r, int i, double x, do
   return ex * ex + ey * ey;
 }
 
+// CaRL arc position of (x, y) on raw segment i: cumulative length + the clipped
+// projection (carl_reward_fn.py:36-58)
+__device__ __forceinline__ double d_carl_arc(const DRec& r, int i, double x, double y) {
+  const int abx_i = r.raw_x[i + 1] - r.raw_x[i], aby_i = r.raw_y[i + 1] - r.raw_y[i];
+  const double ax = r.raw_x[i], ay = r.raw_y[i];
+  const double tt = d_clip(((x - ax) * abx_i + (y - ay) * aby_i) / ((double)(abx_i * abx_i + aby_i * aby_i) + 1e-9), 0, 1);
+  return r.raw_cum[i] + tt * sqrt((double)(abx_i * abx_i + aby_i * aby_i));
+}
+
 // Loop mask for performance experiments: 1 target loop, 2 route-progress loop.
 #ifndef CBEV_COLLIDE_PHASES
 #define CBEV_COLLIDE_PHASES 3
 #endif
+// signed distance to waypoint segment i (control/utils.py:165-197)
+__device__ __forceinline__ double d_lateral_seg(double px, double py, const double* wx, const double* wy, int i) {
+  double abx = wx[i + 1] - wx[i], aby = wy[i + 1] - wy[i];
+  double apx = px - wx[i], apy = py - wy[i];
+  double tt = (apx * abx + apy * aby) / (abx * abx + aby * aby);
+  tt = d_clip(tt, 0.0, 1.0);
+  double ex = px - (wx[i] + tt * abx), ey = py - (wy[i] + tt * aby);
+  double err = sqrt(ex * ex + ey * ey);
+  double cross = abx * apy - aby * apx;
+  if (cross != 0) err *= (cross > 0) ? 1.0 : ((cross < 0) ? -1.0 : cross);
+  return err;
+}
+// lateral_error: the first segment with the strictly smallest |err|
 __device__ __forceinline__ double d_lateral_error(double px, double py, const double* wx, const double* wy, int n) {
   double min_error = INFINITY;
   for (int i = 0; i < n - 1; ++i) {
-    double abx = wx[i + 1] - wx[i], aby = wy[i + 1] - wy[i];
-    double apx = px - wx[i], apy = py - wy[i];
-    double tt = (apx * abx + apy * aby) / (abx * abx + aby * aby);
-    tt = d_clip(tt, 0.0, 1.0);
-    double ex = px - (wx[i] + tt * abx), ey = py - (wy[i] + tt * aby);
-    double err = sqrt(ex * ex + ey * ey);
-    double cross = abx * apy - aby * apx;
-    if (cross != 0) err *= (cross > 0) ? 1.0 : ((cross < 0) ? -1.0 : cross);
+    const double err = d_lateral_seg(px, py, wx, wy, i);
     if (fabs(err) < fabs(min_error)) min_error = err;
   }
   return min_error;
+}
+// lateral_error's waypoint window: next_wps(5) from the target index (stanley_controller.py:150-152)
+__device__ __forceinline__ int d_next_wps(int tidx, int nt) {
+  const int wend = (tidx + 5 <= nt) ? tidx + 5 : nt - 1;
+  return wend > tidx ? wend - tidx : 0;
 }
 
 // Per-env scratch of k_collide's cooperative pre-pass (LDS, after the staged
@@ -1256,22 +1311,55 @@ struct CollScratchLayout {
 };
 __host__ __device__ __forceinline__ CollScratchLayout coll_scratch_layout(const cbev_caps& C, int vis_words) {
   CollScratchLayout o;
-  o.segd = 0;                                   // double[R]: sqrt(e2) per raw segment
-  o.ttcc = o.segd + 8 * C.route_cap;            // double[A]: compute_ttc_raw per actor (INF if none)
+  o.segd = 0;                                   // double[4]: bdist, s_t, d2r (cooperative reductions)
+  o.ttcc = o.segd + 32;                         // double[A]: compute_ttc_raw per actor (INF if none)
   o.ttcs = o.ttcc + 8 * C.actor_cap;            // double[A]: compute_ttc per actor
   o.ints = o.ttcs + 8 * C.actor_cap;            // int[8]: tgt_last, act_last, nas, hrx, hry, pad...
   o.hitw = o.ints + 32;                         // uint32[vis_words]: visible targets hit
   o.bytes = (o.hitw + 4 * vis_words + 15) & ~15;
   return o;
 }
-enum { CS_TGT_LAST = 0, CS_ACT_LAST = 1, CS_NAS = 2 };
-struct CollPre {  // one env's pre-pass results, as seen by collide_env
-  const double* segd;
-  const double* ttcc;
-  const double* ttcs;
-  const int* ints;
-  const uint32_t* hitw;
+enum { CS_TGT_LAST = 0, CS_ACT_LAST = 1, CS_NAS = 2, CS_BSEG = 5, CS_TILE = 6 };
+struct CollPre {  // one env's reduced pre-pass results, as seen by collide_env
+  int tgt_last, act_last, nas;  // last visible target / actor hit (-1: none), actors_state entries
+  const uint32_t* hitw;         // visible targets hit (cleared from the visibility bits)
+  double ttc_carl, ttc_sh;      // min compute_ttc_raw / compute_ttc over the actors (INF if none)
+  double bdist;                 // first strict minimum of the raw-segment distances (1e9 if none)
+  int bseg;
+  int tile;                     // ego tile class, or -1: looked up by collide_env
+  int have_sd;                  // s_t / d2r below are valid (else collide_env computes them)
+  double s_t;                   // CaRL arc position of the ego on the winning raw segment
+  double d2r;                   // lateral_error over next_wps(5)
 };
+
+// k_collide: reduce one env's scratch arrays in the reference's loop order
+__device__ __forceinline__ CollPre coll_reduce_serial(const uint8_t* sk, const CollScratchLayout& SL, int nact,
+                                                      int nraw) {
+  CollPre p;
+  const int* ints = (const int*)(sk + SL.ints);
+  const double* ttcc = (const double*)(sk + SL.ttcc);
+  const double* ttcs = (const double*)(sk + SL.ttcs);
+  const double* segd = (const double*)(sk + SL.segd);
+  p.tgt_last = ints[CS_TGT_LAST];
+  p.act_last = ints[CS_ACT_LAST];
+  p.nas = ints[CS_NAS];
+  p.hitw = (const uint32_t*)(sk + SL.hitw);
+  p.ttc_carl = p.ttc_sh = INFINITY;
+  for (int a = 0; a < nact; ++a) {
+    p.ttc_carl = ttcc[a] < p.ttc_carl ? ttcc[a] : p.ttc_carl;
+    p.ttc_sh = ttcs[a] < p.ttc_sh ? ttcs[a] : p.ttc_sh;
+  }
+  // reduced by the pre-pass: CaRL's winning raw segment (first strict arg-min,
+  // carl_reward_fn.py:29-58), the ego's arc position on it, lateral_error, ego tile
+  p.bdist = segd[0];
+  p.bseg = ints[CS_BSEG];
+  p.s_t = segd[1];
+  p.d2r = segd[2];
+  p.have_sd = 1;
+  p.tile = ints[CS_TILE];
+  (void)nraw;
+  return p;
+}
 
 // One thread per env for the float64 scalar chain; the element loops come
 // precomputed in `pre`.
@@ -1286,7 +1374,7 @@ __device__ __forceinline__ void collide_env(const KArgs& K, DRec r, int e, const
 
   // ---- ego tile (world.py:159-165)
   int tx = (int)d_clip(rint(x), 0, P.map_w - 1), ty = (int)d_clip(rint(y), 0, P.map_h - 1);
-  const int tile = d_map_texel(K, tx + P.pad, ty + P.pad);
+  const int tile = pre.tile >= 0 ? pre.tile : d_map_texel(K, tx + P.pad, ty + P.pad);
 
   // ---- collisions (scene.py:110-140): hero rect vs vehicles, pedestrians, visible
   // targets; the last hit in iteration order (vehicles, pedestrians, then targets)
@@ -1294,27 +1382,14 @@ __device__ __forceinline__ void collide_env(const KArgs& K, DRec r, int e, const
   CBEV_STAMP(4, 0);
   const int nact = hi[CBEV_HI_NACT];
   const int nt = hi[CBEV_HI_NROUTE];
-  const int tgt_last = pre.ints[CS_TGT_LAST], act_last = pre.ints[CS_ACT_LAST];
-  const int last_hit = tgt_last >= 0 ? nact + tgt_last : act_last;
-  const int nas = pre.ints[CS_NAS];
+  const int last_hit = pre.tgt_last >= 0 ? nact + pre.tgt_last : pre.act_last;
+  const int nas = pre.nas;
   for (int w = 0; w < K.L.vis_words; ++w) r.vis[w] &= ~pre.hitw[w];
-  double ttc_carl = INFINITY, ttc_sh = INFINITY;
-  for (int a = 0; a < nact; ++a) {
-    ttc_carl = pre.ttcc[a] < ttc_carl ? pre.ttcc[a] : ttc_carl;
-    ttc_sh = pre.ttcs[a] < ttc_sh ? pre.ttcs[a] : ttc_sh;
-  }
-
-  // ---- CaRL route progress: first strict arg-min over raw-route segments (carl_reward_fn.py:29-58)
+  const double ttc_carl = pre.ttc_carl, ttc_sh = pre.ttc_sh;
+  // CaRL route progress: the winning raw segment (first strict arg-min, carl_reward_fn.py:29-58)
   const int nraw = hi[CBEV_HI_NRAW];
-  double bdist = 1e9;
-  int bseg = 0;
-  for (int i = 0; (CBEV_COLLIDE_PHASES & 2) && i < nraw - 1; ++i) {
-    const double dist = pre.segd[i];
-    if (dist < bdist) {
-      bdist = dist;
-      bseg = i;
-    }
-  }
+  const double bdist = pre.bdist;
+  const int bseg = pre.bseg;
 
   int result = CBEV_COLL_NONE, coll_id = -1;
   if (last_hit >= 0) {
@@ -1343,8 +1418,7 @@ __device__ __forceinline__ void collide_env(const KArgs& K, DRec r, int e, const
     dist2wp = sqrt(dx * dx + dy * dy);
   }
   hd[CBEV_HD_DIST2WP] = dist2wp;
-  const int wend = (tidx + 5 <= nt) ? tidx + 5 : nt - 1;
-  const int nw = wend > tidx ? wend - tidx : 0;
+  const int nw = d_next_wps(tidx, nt);
   const double al = hd[CBEV_HD_C_AL], alat = hd[CBEV_HD_C_ALAT], yr = hd[CBEV_HD_C_YR];
   const double jl = hd[CBEV_HD_C_JL], jlat = hd[CBEV_HD_C_JLAT], yacc = hd[CBEV_HD_C_YACC];
   const int nviol = (fabs(al) > 2.0) + (fabs(alat) > 2.0) + (fabs(yr) > 20.0) + (fabs(jl) > 3.0) + (fabs(jlat) > 3.0) +
@@ -1372,12 +1446,10 @@ __device__ __forceinline__ void collide_env(const KArgs& K, DRec r, int e, const
       reward = -1.0;
     } else {
       double s_t = 0.0;
-      if (bdist < 1e9) {  // recompute the winning segment's arc position
-        const int i = bseg;
-        const int abx_i = r.raw_x[i + 1] - r.raw_x[i], aby_i = r.raw_y[i + 1] - r.raw_y[i];
-        const double ax = r.raw_x[i], ay = r.raw_y[i];
-        const double tt = d_clip(((x - ax) * abx_i + (y - ay) * aby_i) / ((double)(abx_i * abx_i + aby_i * aby_i) + 1e-9), 0, 1);
-        s_t = r.raw_cum[i] + tt * sqrt((double)(abx_i * abx_i + aby_i * aby_i));
+      if (pre.have_sd) {
+        s_t = pre.s_t;
+      } else if (bdist < 1e9) {  // the winning segment's arc position
+        s_t = d_carl_arc(r, bseg, x, y);
       }
       if (!hi[CBEV_HI_S_PREV_VALID]) {
         hd[CBEV_HD_S_PREV] = s_t;
@@ -1388,7 +1460,7 @@ __device__ __forceinline__ void collide_env(const KArgs& K, DRec r, int e, const
       double total = r.raw_cum[nraw - 1];
       double RC = total > 0 ? rc_raw / total : 0.0;
       RC = d_clip(RC * 100, 0.0, 1.0);
-      double d2r = d_lateral_error(x, y, r.cx + tidx, r.cy + tidx, nw);
+      double d2r = pre.have_sd ? pre.d2r : d_lateral_error(x, y, r.cx + tidx, r.cy + tidx, nw);
       double dist_m = fabs(d2r) * CB_MPP;
       // pow(x, 1.0) is exactly x (IEEE 754 / C99 F.9.4.4); skip the log/exp of the general pow
       const double lx = dist_m / 3.0;
@@ -1455,7 +1527,7 @@ __device__ __forceinline__ void collide_env(const KArgs& K, DRec r, int e, const
         const double yaw1 = hd[CBEV_HD_YAW1], v1 = hd[CBEV_HD_V1];
         double yaw_error = atan2(sin(spyaw - yaw), cos(spyaw - yaw));
         double align = cos(yaw_error);
-        double d2r = d_lateral_error(x, y, r.cx + tidx, r.cy + tidx, nw);
+        double d2r = pre.have_sd ? pre.d2r : d_lateral_error(x, y, r.cx + tidx, r.cy + tidx, nw);
         double ee = d_clip(fabs(d2r), 0.0, P.lat_clip);
         rr -= P.k_lat_quadratic * (ee * ee);
         if (dist2wp > P.route_dev_start) rr -= P.k_route_dev * (dist2wp - P.route_dev_start);
@@ -1535,9 +1607,13 @@ __global__ __launch_bounds__(256) void k_collide(KArgs K, uint8_t* __restrict__ 
   __syncthreads();
   CBEV_STAMP(1, 1);
   const int hw = P.hero_w;
-  // per-env prologue: hero rect, counters
+  // per-env prologue: hero rect, counters; the ego tile's map load
+  // (world.py:159-165) stays in flight through the pre-pass
+  int tile = 0;
   if (tid < ne_eff) {
     const double* hd = (const double*)(lds + tid * sbytes + K.L.hd);
+    const int tx = (int)d_clip(rint(hd[CBEV_HD_X]), 0, P.map_w - 1), ty = (int)d_clip(rint(hd[CBEV_HD_Y]), 0, P.map_h - 1);
+    tile = d_map_texel(K, tx + P.pad, ty + P.pad);
     int* I = (int*)(scr + tid * SL.bytes + SL.ints);
     I[CS_TGT_LAST] = -1;
     I[CS_ACT_LAST] = -1;
@@ -1558,11 +1634,56 @@ __global__ __launch_bounds__(256) void k_collide(KArgs K, uint8_t* __restrict__ 
       DRec r = bind_rec(lds + k * sbytes, K.L, K.C);
       uint8_t* sk = scr + k * SL.bytes;
       const double x = r.hd[CBEV_HD_X], y = r.hd[CBEV_HD_Y];
-      // raw-route segments (carl_reward_fn.py:36-48)
+      // raw-route segments (carl_reward_fn.py:36-48): first strict arg-min over the
+      // env's tpe threads (lane-local in index order, then the (distance, index)
+      // minimum), and lateral_error over next_wps(5) (control/utils.py:165-197):
+      // the first segment with the strictly smallest |err|
       const int nseg = r.hi[CBEV_HI_NRAW] - 1;
-      double* segd = (double*)(sk + SL.segd);
+      double bd = INFINITY;
+      int bi = 0x7fffffff;
 #pragma unroll 4
-      for (int i = sub; i < nseg; i += tpe) segd[i] = sqrt(d_seg_dist2(r, i, x, y));
+      for (int i = sub; (CBEV_COLLIDE_PHASES & 2) && i < nseg; i += tpe) {
+        const double d = sqrt(d_seg_dist2(r, i, x, y));
+        if (d < bd) {  // NaN never wins
+          bd = d;
+          bi = i;
+        }
+      }
+      const int tidx = r.hi[CBEV_HI_TIDX];
+      const int nw = d_next_wps(tidx, r.hi[CBEV_HI_NROUTE]);
+      double lk = INFINITY, le = INFINITY;
+      int li = 0x7fffffff;
+      for (int i = sub; i < nw - 1; i += tpe) {
+        const double err = d_lateral_seg(x, y, r.cx + tidx, r.cy + tidx, i);
+        if (fabs(err) < lk) {
+          lk = fabs(err);
+          le = err;
+          li = i;
+        }
+      }
+      for (int off = tpe >> 1; off > 0; off >>= 1) {
+        const double ob = __shfl_xor(bd, off, 64);
+        const int obi = __shfl_xor(bi, off, 64);
+        if (ob < bd || (ob == bd && obi < bi)) {
+          bd = ob;
+          bi = obi;
+        }
+        const double ok = __shfl_xor(lk, off, 64), oe = __shfl_xor(le, off, 64);
+        const int oli = __shfl_xor(li, off, 64);
+        if (ok < lk || (ok == lk && oli < li)) {
+          lk = ok;
+          le = oe;
+          li = oli;
+        }
+      }
+      if (sub == 0) {
+        double* red = (double*)(sk + SL.segd);
+        const bool any = bd < 1e9;
+        red[0] = any ? bd : 1e9;
+        red[1] = any ? d_carl_arc(r, bi, x, y) : 0.0;
+        red[2] = le;
+        ((int*)(sk + SL.ints))[CS_BSEG] = any ? bi : 0;
+      }
       CBEV_STAMP(5, 1);
       // visible targets vs the hero rect (target.py:37-44)
       int* I = (int*)(sk + SL.ints);
@@ -1623,20 +1744,312 @@ __global__ __launch_bounds__(256) void k_collide(KArgs K, uint8_t* __restrict__ 
       ((double*)(scr + k * SL.bytes + SL.ttcs))[a] = ts;
     }
   }
+  if (tid < ne_eff) ((int*)(scr + tid * SL.bytes + SL.ints))[CS_TILE] = tile;
   __syncthreads();
   CBEV_STAMP(5, 3);
   if (tid < ne_eff) {
-    const uint8_t* sk = scr + tid * SL.bytes;
-    const CollPre pre{(const double*)(sk + SL.segd), (const double*)(sk + SL.ttcc), (const double*)(sk + SL.ttcs),
-                      (const int*)(sk + SL.ints), (const uint32_t*)(sk + SL.hitw)};
-    collide_env(K, bind_rec(lds + tid * sbytes, K.L, K.C), e0 + tid, pre, reward_out, term_out, trunc_out, cause_out,
-                info_out);
+    const DRec rr = bind_rec(lds + tid * sbytes, K.L, K.C);
+    const CollPre pre = coll_reduce_serial(scr + tid * SL.bytes, SL, rr.hi[CBEV_HI_NACT], rr.hi[CBEV_HI_NRAW]);
+    collide_env(K, rr, e0 + tid, pre, reward_out, term_out, trunc_out, cause_out, info_out);
   }
   CBEV_STAMP(1, 2);
   __syncthreads();
   stage_out(lds, recs, e0, ne_eff, rb, sbytes, 0, (int)K.L.cx);                                // HD + HI
   stage_out(lds, recs, e0, ne_eff, rb, sbytes, (int)K.L.vis, (4 * K.L.vis_words + 15) & ~15);  // target visibility
   CBEV_STAMP(1, 3);
+}
+
+// ============================================================== k_step (fused step)
+// One 256-thread workgroup runs the whole CarlaBEV.step() of NE envs (after
+// the scripted actors: k_actors is launched before it when the record has
+// actor slots): ego updates, render set-ups, each env's crop staging + paint +
+// frame, and the collision / reward pass.
+//
+// A float64 scalar chain costs a wavefront instruction per step whether one
+// lane or 64 run it, so the chains of the NE envs run side by side in lanes
+// 0..NE-1 (ego) and in lane groups of 64/NE (collision), and with NE = 2 the
+// 2048 workgroups of 4096 envs are all resident at once (8 per CU), so each
+// workgroup's chain latency overlaps the other seven's staging and stores.
+//   S0  HD + HI of the NE records -> LDS (the chains read and write there);
+//       actions prefetched
+//   S1  cos(yaw) (wave 0) | tan(clip(delta)) (wave 1) | sin(yaw) (wave 2)
+//   S2  ego chain A (wave 0) | Stanley target search (wave 1, 64/NE lanes per
+//       env over the route points, first arg-min by group reduction)
+//   S3  render set-up (wave 0) | comfort + dist2goal (wave 1)
+//   S4  per env: raster_env (crop staging, paint, output); for the last env the
+//       output runs on waves 0-2 beside collide_group for all NE envs (wave 3)
+//   S5  HD + HI back to the records
+// Reference: Scene._scene_step (scene.py:90-98), hero.py:88-187,
+// world.py:137-165, fov.py:70-99, scene.py:110-140, carl_reward_fn.py:149-341,
+// reward.py:80-278, stats.py:30-56, carlabev.py:177-185.
+#ifndef CBEV_STEP_NE
+#define CBEV_STEP_NE 2
+#endif
+
+// LDS of k_step: crop image | NE x (HD + HI) | NE x 8 doubles of ego pre-computation | NE x hit words
+__host__ __device__ __forceinline__ int step_img_bytes(int S, int C) { return (raster_image_bytes(S, C) + 15) & ~15; }
+__host__ __device__ __forceinline__ int step_hw_bytes(const cbev_layout& L) { return (4 * L.vis_words + 15) & ~15; }
+__host__ __device__ __forceinline__ int step_lds_bytes(int S, int C, const cbev_layout& L, int ne) {
+  return step_img_bytes(S, C) + ne * ((int)(L.cx - L.hd) + 64 + step_hw_bytes(L));
+}
+
+// Scene.collision_check + the CaRL / shaping reward pass of one env on a group
+// of W lanes (sub = lane within the group): element loops over the lanes
+// (raw-route segments, visible targets, actors), reduced with the reference's
+// order semantics (first strict arg-min, last hit in draw order, minimum TTC),
+// then collide_env's scalar chain on the group's first lane.
+template <int W>
+__device__ __forceinline__ void collide_group(const KArgs& K, const DRec& r, int e, int sub, uint32_t* hitw,
+                                              double* __restrict__ reward_out, uint8_t* __restrict__ term_out,
+                                              uint8_t* __restrict__ trunc_out, int32_t* __restrict__ cause_out,
+                                              float* __restrict__ info_out) {
+  const cbev_params& P = K.P;
+  const int hw = P.hero_w;
+  const int gshift = (threadIdx.x & 63) & ~(W - 1);  // this group's first lane
+  const double x = r.hd[CBEV_HD_X], y = r.hd[CBEV_HD_Y], yaw = r.hd[CBEV_HD_YAW], v = r.hd[CBEV_HD_V];
+  const int hrx = d_rect_lo(x, P.pad, hw), hry = d_rect_lo(y, P.pad, hw);
+  // raw-route segments (carl_reward_fn.py:36-48): lane-local first strict minimum
+  // in increasing index order, then the lexicographic (distance, index) minimum
+  const int nseg = r.hi[CBEV_HI_NRAW] - 1;
+  double bd = INFINITY;
+  int bi = 0x7fffffff;
+  for (int i = sub; (CBEV_COLLIDE_PHASES & 2) && i < nseg; i += W) {
+    const double d = sqrt(d_seg_dist2(r, i, x, y));
+    if (d < bd) {  // NaN never wins, as in the serial loop
+      bd = d;
+      bi = i;
+    }
+  }
+  group_argmin<W>(bd, bi);
+  // visible targets vs the hero rect (target.py:37-44); every hit is consumed
+  for (int w = sub; w < K.L.vis_words; w += W) hitw[w] = 0u;
+  const int nt = r.hi[CBEV_HI_NROUTE];
+  int tgt_last = -1;
+  for (int b0 = 0; b0 < nt; b0 += W) {
+    const int i = b0 + sub;
+    bool hit = false;
+    if (i < nt && ((r.vis[i >> 5] >> (i & 31)) & 1u)) {
+      const int sz = (i < nt - 1) ? 2 : 4;
+      const int trx = d_rect_lo(r.cx[i], P.pad, sz), try_ = d_rect_lo(r.cy[i], P.pad, sz);
+      hit = hrx < trx + sz && hry < try_ + sz && hrx + hw > trx && hry + hw > try_;
+    }
+    uint64_t m = __ballot(hit) >> gshift;  // this group's W bits: target b0 + b at bit b
+    if (W < 64) m &= (1ull << W) - 1;
+    if (sub == 0) {
+      if (W == 64) {
+        hitw[b0 >> 5] = (uint32_t)m;
+        if ((b0 >> 5) + 1 < K.L.vis_words) hitw[(b0 >> 5) + 1] = (uint32_t)(m >> 32);
+      } else {
+        hitw[b0 >> 5] |= (uint32_t)m << (b0 & 31);
+      }
+    }
+    if (m) tgt_last = b0 + 63 - __builtin_clzll(m);
+  }
+  // vehicles / pedestrians: rect hit, actors_state entry and both TTCs
+  // (scene.py:110-140, reward_signals.py:15-94)
+  const int nact = r.hi[CBEV_HI_NACT];
+  int act_last = -1, nas = 0;
+  double tcm = INFINITY, tsm = INFINITY;
+  for (int a = sub; a < nact; a += W) {
+    const int sz = RAI(r, CBEV_AI_SIZE, a);
+    const double ax = RAD(r, CBEV_AD_X, a), ay = RAD(r, CBEV_AD_Y, a);
+    const int arx = d_rect_lo(ax, P.pad, sz), ary = d_rect_lo(ay, P.pad, sz);
+    if (hw > 0 && sz > 0 && hrx < arx + sz && hry < ary + sz && hrx + hw > arx && hry + hw > ary) act_last = a;
+    const int ddx = (hrx + hw / 2) - (arx + sz / 2), ddy = (hry + hw / 2) - (ary + sz / 2);
+    const double dist = hypot((double)ddx, (double)ddy);
+    if (fabs(dist) < P.collide_min_dist) {
+      ++nas;
+      const double hx_m = x * CB_MPP, hy_m = y * CB_MPP, hv_m = v * CB_MPP;
+      const double hvx_m = hv_m * cos(yaw), hvy_m = hv_m * sin(yaw);
+      const double hvx = v * cos(yaw), hvy = v * sin(yaw);
+      const double av = RAD(r, CBEV_AD_V, a), ayaw = RAD(r, CBEV_AD_YAW, a);
+      const double avx = av * cos(ayaw), avy = av * sin(ayaw);
+      {  // compute_ttc_raw (reward_signals.py:46-94)
+        double rx_ = ax * CB_MPP - hx_m, ry_ = ay * CB_MPP - hy_m;
+        double rvx = avx * CB_MPP - hvx_m, rvy = avy * CB_MPP - hvy_m;
+        double nrm = sqrt(rx_ * rx_ + ry_ * ry_);
+        double rel = (rvx * rx_ + rvy * ry_) / (nrm + 1e-6);
+        if (!(rel >= 0)) {
+          const double tc = fabs(nrm / rel);
+          tcm = tc < tcm ? tc : tcm;
+        }
+      }
+      {  // compute_ttc (reward_signals.py:15-42)
+        double rx_ = ax - x, ry_ = ay - y;
+        double rvx = avx - hvx, rvy = avy - hvy;
+        double nrm = sqrt(rx_ * rx_ + ry_ * ry_);
+        double rel = (rvx * rx_ + rvy * ry_) / (nrm + 1e-6);
+        if (!(rel >= 0)) {
+          const double ts = fabs(nrm / rel);
+          tsm = ts < tsm ? ts : tsm;
+        }
+      }
+    }
+  }
+  act_last = group_max_i<W>(act_last);
+  nas = group_sum_i<W>(nas);
+  tcm = group_min<W>(tcm);
+  tsm = group_min<W>(tsm);
+  if (sub == 0) {
+    CollPre p;
+    p.tgt_last = tgt_last;
+    p.act_last = act_last;
+    p.nas = nas;
+    p.hitw = hitw;
+    p.ttc_carl = tcm;
+    p.ttc_sh = tsm;
+    p.bdist = bd < 1e9 ? bd : 1e9;
+    p.bseg = bd < 1e9 ? bi : 0;
+    p.tile = -1;
+    p.have_sd = 0;
+    p.s_t = p.d2r = 0.0;
+    collide_env(K, r, e, p, reward_out, term_out, trunc_out, cause_out, info_out);
+  }
+}
+
+// waves per SIMD the register allocation must allow (8: every workgroup the
+// LDS admits can be resident)
+#ifndef CBEV_STEP_WAVES
+#define CBEV_STEP_WAVES 8
+#endif
+template <int G, int NE>
+__global__ __launch_bounds__(256, CBEV_STEP_WAVES) void k_step(KArgs K, uint8_t* __restrict__ recs, int n,
+                                                                const void* __restrict__ actions,
+                                                                uint8_t* __restrict__ frames,
+                                                                double* __restrict__ reward_out,
+                                                                uint8_t* __restrict__ term_out,
+                                                                uint8_t* __restrict__ trunc_out,
+                                                                int32_t* __restrict__ cause_out,
+                                                                float* __restrict__ info_out) {
+  extern __shared__ __align__(16) uint8_t lds[];
+  constexpr int W = 64 / NE;  // collision lanes per env
+  const int npairs = (n + NE - 1) / NE;
+  const int e0 = NE * xcd_env_of_wg(blockIdx.x, npairs);
+  if (e0 >= n) return;
+  const int ne = min(NE, n - e0);
+  const int hh = (int)(K.L.cx - K.L.hd);  // HD + HI bytes (64-byte aligned groups)
+  const int hwb = step_hw_bytes(K.L);
+  uint8_t* lhh = lds + step_img_bytes(64 * G, K.P.crop);  // [NE][hh]
+  double* misc = (double*)(lhh + NE * hh);               // [NE][8]: cos yaw, sin yaw, tan delta, front axle x, y
+  uint8_t* hitb = (uint8_t*)(misc + 8 * NE);             // [NE][hwb]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int64_t rb = K.L.record_bytes;
+  auto rec_of = [&](int k) {
+    DRec r = bind_rec(recs + (int64_t)(e0 + k) * rb, K.L, K.C);
+    r.hd = (double*)(lhh + k * hh);
+    r.hi = (int32_t*)(lhh + k * hh + (K.L.hi - K.L.hd));
+    return r;
+  };
+  CBEV_STAMP(2, 0);
+  // S0
+  float g = 0.f, sa = 0.f, b = 0.f;
+  if (wave <= 1 && lane < ne) d_decode_action(K, actions, e0 + lane, &g, &sa, &b);  // in flight during S0
+  {
+    const int q16 = hh / 16;
+    for (int q = tid; q < ne * q16; q += 256) {
+      const int k = q / q16, c = q - k * q16;
+      ((uint4*)(lhh + k * hh))[c] = ((const uint4*)(recs + (int64_t)(e0 + k) * rb + K.L.hd))[c];
+    }
+  }
+  __syncthreads();
+  CBEV_STAMP(3, 0);
+  // S1: the pre-update trig of State.update and the front axle of calc_target_index
+  if (lane < ne) {
+    const DRec r = rec_of(lane);
+    double* m = misc + 8 * lane;
+    if (wave == 0) {
+      const double c = cos(r.hd[CBEV_HD_YAW]);
+      m[0] = c;
+      m[3] = r.hd[CBEV_HD_X] + CB_WHEELBASE * c;
+    } else if (wave == 1) {
+      const double max_steer = 30.0 * (CB_PI / 180.0);
+      m[2] = tan(d_clip(d_hero_delta(r.hd[CBEV_HD_V], sa), -max_steer, max_steer));
+    } else if (wave == 2) {
+      const double sn = sin(r.hd[CBEV_HD_YAW]);
+      m[1] = sn;
+      m[4] = r.hd[CBEV_HD_Y] + CB_WHEELBASE * sn;
+    }
+  }
+  __syncthreads();
+  CBEV_STAMP(3, 1);
+  // S2
+  if (wave == 0) {
+    if (lane < ne) {
+      const double* m = misc + 8 * lane;
+      HeroPre hp;
+      hp.cyaw = m[0];
+      hp.syaw = m[1];
+      hp.tdelta = m[2];
+      const float gsb[3] = {g, sa, b};
+      hero_env_a(K, rec_of(lane), e0 + lane, actions, -1, hp, gsb);
+    }
+  } else if (wave == 1) {
+    // Controller.calc_target_index (stanley_controller.py:51-62), first arg-min of
+    // hypot: squared-distance pre-filter within (1 + 1e-14) of the minimum, as k_hero
+    const int k = lane / W, sub = lane - k * W;
+    const bool act = k < ne;
+    const DRec r = rec_of(act ? k : 0);
+    const double fx = misc[8 * k + 3], fy = misc[8 * k + 4];
+    const int nr = act ? r.hi[CBEV_HI_NROUTE] : 0;
+    double m2 = INFINITY;
+    for (int i = sub; i < nr; i += W) {
+      const double dx = fx - r.cx[i], dy = fy - r.cy[i];
+      const double d2 = dx * dx + dy * dy;
+      m2 = d2 < m2 ? d2 : m2;
+    }
+    m2 = group_min<W>(m2);
+    const double lim = m2 * (1.0 + 1e-14);
+    double bd = INFINITY;
+    int bi = 0x7fffffff;
+    for (int i = sub; i < nr; i += W) {
+      const double dx = fx - r.cx[i], dy = fy - r.cy[i];
+      if (dx * dx + dy * dy <= lim) {
+        const double h = hypot(dx, dy);
+        if (h < bd) {
+          bd = h;
+          bi = i;
+        }
+      }
+    }
+    group_argmin<W>(bd, bi);
+    if (act && sub == 0) {
+      bi = bi == 0x7fffffff ? 0 : bi;
+      r.hi[CBEV_HI_TIDX] = r.hi[CBEV_HI_TIDX] >= bi ? r.hi[CBEV_HI_TIDX] : bi;
+    }
+  }
+  __syncthreads();
+  CBEV_STAMP(3, 2);
+  // S3
+  if (lane < ne) {
+    if (wave == 0) hero_env_render_setup(K, rec_of(lane));
+    else if (wave == 1) hero_env_comfort(rec_of(lane));
+  }
+  __syncthreads();
+  CBEV_STAMP(3, 3);
+  // S4
+  const int64_t SS = (int64_t)K.P.size * K.P.size;
+  for (int k = 0; k < ne - 1; ++k) {
+    raster_env<false, G>(K, rec_of(k), frames + (e0 + k) * SS, 1, 0, lds);
+    __syncthreads();  // the next env's staging overwrites the crop image
+  }
+  auto side = [&](int ln) {
+    const int k = ln / W;
+    if (k < ne)
+      collide_group<W>(K, rec_of(k), e0 + k, ln - k * W, (uint32_t*)(hitb + k * hwb), reward_out, term_out,
+                       trunc_out, cause_out, info_out);
+  };
+  raster_env<false, G, 3>(K, rec_of(ne - 1), frames + (e0 + ne - 1) * SS, 1, 0, lds, side);
+  __syncthreads();
+  // S5
+  {
+    const int q16 = hh / 16;
+    for (int q = tid; q < ne * q16; q += 256) {
+      const int k = q / q16, c = q - k * q16;
+      ((uint4*)(recs + (int64_t)(e0 + k) * rb + K.L.hd))[c] = ((const uint4*)(lhh + k * hh))[c];
+    }
+  }
+  CBEV_STAMP(2, 3);
 }
 
 // ============================================================== reset / ring / expansion
@@ -1938,6 +2351,8 @@ struct cbev_ctx {
   void* area_dev;     // INTER_AREA tables of cbev_set_obs_size
   AreaTab area;
   uint8_t* fov_dev;   // cbev_set_fov_mask
+  int step_mode;      // CBEV_STEP_FUSED (k_step) or CBEV_STEP_SPLIT (k_hero, k_raster, k_collide)
+  int step_lb;        // k_step dynamic LDS bytes
 };
 
 // envs per workgroup for a staged kernel: the largest divisor of 64 whose
@@ -2041,6 +2456,11 @@ static KArgs kargs(const cbev_ctx* c) {
 static const void* raster_kernel(int size) {
   return size == 64 ? (const void*)k_raster<1> : size == 128 ? (const void*)k_raster<2> : (const void*)k_raster<4>;
 }
+static const void* step_kernel(int size) {
+  return size == 64    ? (const void*)k_step<1, CBEV_STEP_NE>
+         : size == 128 ? (const void*)k_step<2, CBEV_STEP_NE>
+                       : (const void*)k_step<4, CBEV_STEP_NE>;
+}
 static const void* bank_frames_kernel(int size) {
   return size == 64 ? (const void*)k_bank_frames<1> : size == 128 ? (const void*)k_bank_frames<2>
                                                                    : (const void*)k_bank_frames<4>;
@@ -2125,6 +2545,14 @@ int cbev_create(const cbev_params* params, const cbev_caps* caps, int device, cb
     e = hipFuncSetAttribute(raster_kernel(P.size), hipFuncAttributeMaxDynamicSharedMemorySize, (int)raster_lds_bytes(P));
   if (e == hipSuccess)
     e = hipFuncSetAttribute(reset_kernel(P.size), hipFuncAttributeMaxDynamicSharedMemorySize, (int)raster_lds_bytes(P));
+  c->step_lb = step_lds_bytes(P.size, P.crop, c->L, CBEV_STEP_NE);
+  {
+    // default: the split step (measured faster); CBEV_STEP_MODE=fused selects k_step
+    const char* m = getenv("CBEV_STEP_MODE");
+    c->step_mode = (m && strcmp(m, "fused") == 0) && c->step_lb <= 160 * 1024 ? CBEV_STEP_FUSED : CBEV_STEP_SPLIT;
+  }
+  if (e == hipSuccess && c->step_lb <= 160 * 1024)
+    e = hipFuncSetAttribute(step_kernel(P.size), hipFuncAttributeMaxDynamicSharedMemorySize, c->step_lb);
   if (e == hipSuccess)
     e = hipFuncSetAttribute(bank_frames_kernel(P.size), hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)raster_lds_bytes(P));
@@ -2135,6 +2563,17 @@ int cbev_create(const cbev_params* params, const cbev_caps* caps, int device, cb
   *out = c;
   return CBEV_OK;
 }
+
+int cbev_set_step_mode(cbev_ctx* c, int mode) {
+  if (!c) return set_err(CBEV_EINVAL, "null argument");
+  if (mode != CBEV_STEP_FUSED && mode != CBEV_STEP_SPLIT) return set_err(CBEV_EINVAL, "bad step mode %d", mode);
+  if (mode == CBEV_STEP_FUSED && c->step_lb > 160 * 1024)
+    return set_err(CBEV_EINVAL, "k_step needs %d bytes of LDS", c->step_lb);
+  c->step_mode = mode;
+  return CBEV_OK;
+}
+
+int cbev_step_mode(const cbev_ctx* c) { return c ? c->step_mode : -1; }
 
 int cbev_profile(cbev_ctx* c, int enable) {
   if (!c) return set_err(CBEV_EINVAL, "null argument");
@@ -2217,10 +2656,30 @@ int cbev_step(cbev_ctx* c, void* records, int n, const void* actions, uint8_t* f
   hipEvent_t* ev = nullptr;
   if (c->prof_on && c->prof_n < CBEV_PROF_MAX) ev = c->prof_ev + 4 * c->prof_n++;
   if (ev) HIP_TRY(hipEventRecord(ev[0], s));
+  if (c->step_mode == CBEV_STEP_FUSED) {
+    // k_actors (clock look-ahead: k_step advances hd[T]) + one fused launch
+    if (c->C.actor_cap > 0) hipLaunchKernelGGL(k_actors, dim3(wg4), dim3(256), 0, s, K, (uint8_t*)records, n, 1);
+    if (ev) HIP_TRY(hipEventRecord(ev[1], s));
+    const dim3 grid((n + CBEV_STEP_NE - 1) / CBEV_STEP_NE);
+    switch (c->P.size) {
+      case 64: hipLaunchKernelGGL((k_step<1, CBEV_STEP_NE>), grid, dim3(256), c->step_lb, s, K, (uint8_t*)records, n,
+                                  actions, frames, reward, term, trunc, cause, info); break;
+      case 128: hipLaunchKernelGGL((k_step<2, CBEV_STEP_NE>), grid, dim3(256), c->step_lb, s, K, (uint8_t*)records, n,
+                                   actions, frames, reward, term, trunc, cause, info); break;
+      default: hipLaunchKernelGGL((k_step<4, CBEV_STEP_NE>), grid, dim3(256), c->step_lb, s, K, (uint8_t*)records, n,
+                                  actions, frames, reward, term, trunc, cause, info); break;
+    }
+    if (ev) {
+      HIP_TRY(hipEventRecord(ev[2], s));
+      HIP_TRY(hipEventRecord(ev[3], s));
+    }
+    HIP_TRY(hipGetLastError());
+    return CBEV_OK;
+  }
   hipLaunchKernelGGL(k_hero, dim3((n + c->hero_ne - 1) / c->hero_ne), dim3(256),
                      (size_t)c->hero_ne * (c->hero_sb + 32), s, K,
                      (uint8_t*)records, n, actions, c->hero_ne, c->hero_sb);
-  if (c->C.actor_cap > 0) hipLaunchKernelGGL(k_actors, dim3(wg4), dim3(256), 0, s, K, (uint8_t*)records, n);
+  if (c->C.actor_cap > 0) hipLaunchKernelGGL(k_actors, dim3(wg4), dim3(256), 0, s, K, (uint8_t*)records, n, 0);
   if (ev) HIP_TRY(hipEventRecord(ev[1], s));
   {
     const size_t lb = raster_lds_bytes(c->P);

@@ -144,6 +144,45 @@ __device__ __forceinline__ int wave_sum_i(int v) {
   return v;
 }
 
+// the same reductions within aligned groups of W lanes (W divides 64): each
+// group reduces on its own (xor offsets below W never leave the group)
+template <int W>
+__device__ __forceinline__ void group_argmin(double& v, int& i) {
+#pragma unroll
+  for (int off = W / 2; off > 0; off >>= 1) {
+    double ov = __shfl_xor(v, off, 64);
+    int oi = __shfl_xor(i, off, 64);
+    if (ov < v || (ov == v && oi < i)) {
+      v = ov;
+      i = oi;
+    }
+  }
+}
+template <int W>
+__device__ __forceinline__ double group_min(double v) {
+#pragma unroll
+  for (int off = W / 2; off > 0; off >>= 1) {
+    double o = __shfl_xor(v, off, 64);
+    v = o < v ? o : v;
+  }
+  return v;
+}
+template <int W>
+__device__ __forceinline__ int group_max_i(int v) {
+#pragma unroll
+  for (int off = W / 2; off > 0; off >>= 1) {
+    int o = __shfl_xor(v, off, 64);
+    v = o > v ? o : v;
+  }
+  return v;
+}
+template <int W>
+__device__ __forceinline__ int group_sum_i(int v) {
+#pragma unroll
+  for (int off = W / 2; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
 // ---------------------------------------------------------------- kinematics
 // State.update (src/control/state.py:29-51); s = x,y,yaw,v,x1,y1,yaw1,v1
 __device__ __forceinline__ void d_state_update(double* s, double acc, double delta, double ts) {

@@ -62,6 +62,18 @@ int cbev_set_map(cbev_ctx* ctx, const uint8_t* padded_map_host, int64_t bytes);
 int cbev_step(cbev_ctx* ctx, void* records, int n, const void* actions, uint8_t* frames, double* reward,
               uint8_t* term, uint8_t* trunc, int32_t* cause, float* info, void* stream);
 
+/* How cbev_step runs on the device (results are identical):
+ *   CBEV_STEP_SPLIT  k_hero, k_actors, k_raster, k_collide (default)
+ *   CBEV_STEP_FUSED  k_actors (when the record has actor slots) + k_step, one
+ *                    workgroup per 2 envs for ego update, raster and collision /
+ *                    reward (the environment variable CBEV_STEP_MODE=fused
+ *                    selects it at cbev_create)
+ * Not stream-ordered: call it between steps. */
+#define CBEV_STEP_FUSED 0
+#define CBEV_STEP_SPLIT 1
+int cbev_set_step_mode(cbev_ctx* ctx, int mode);
+int cbev_step_mode(const cbev_ctx* ctx);
+
 /* Reset the envs selected by mask (uint8[n], NULL = all):
  *   if bank != NULL: records[i] = bank[b] with b = bank_idx[i], or, when
  *   bank_idx == NULL, b = (i + bank_offset) % n_bank (device-side scene bank);
@@ -137,10 +149,11 @@ int cbev_resize_obs(cbev_ctx* ctx, const uint8_t* frames, int n, const uint8_t* 
                     int n_out, int64_t out_stride, void* stream);
 
 /* Kernel timing with HIP events recorded on the step's own stream around each
- * of the three step kernels (used by bench.py for the roofline figure).
- * cbev_profile(ctx, 1) resets the counters and starts recording (up to 8192
- * steps); cbev_profile_read synchronises on the last event and returns the
- * summed milliseconds of [k_hero + k_actors, k_raster, k_collide] and the step count. */
+ * step kernel (used by bench.py for the roofline figure). cbev_profile(ctx, 1)
+ * resets the counters and starts recording (up to 8192 steps);
+ * cbev_profile_read synchronises on the last event and returns the summed
+ * milliseconds of [k_hero + k_actors, k_raster, k_collide] (split step) or
+ * [k_actors, k_step, 0] (fused step) and the step count. */
 int cbev_profile(cbev_ctx* ctx, int enable);
 int cbev_profile_read(cbev_ctx* ctx, double* ms3, int64_t* steps);
 

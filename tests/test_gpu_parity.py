@@ -58,13 +58,16 @@ def compare_records(a: np.ndarray, b: np.ndarray, layout, tag=""):
 
 
 def run_parity(kinds, n_envs, steps, size=128, profile="discrete9_v1", reward="carl_base_v1", seed0=0, anchor_y=0.5,
-               act_seed=1234, edit=None, fov=False):
+               act_seed=1234, edit=None, fov=False, mode=None):
     cfg, P, padded, layout, builder = world(size, profile, reward, anchor_y)
     recs, _ = build_records(builder, n_envs, kinds, seed0=seed0)
     if edit is not None:  # hand-made states on top of the seeded scenes
         edit(recs, layout, P)
     dw = DevWorld(P, padded, CAPS_FULL)
     L = lib()
+    if mode is not None:  # cbev_set_step_mode: the fused k_step must give the same results
+        check(L.cbev_set_step_mode(dw.ctx, mode), "step mode")
+        assert L.cbev_step_mode(dw.ctx) == mode
     S = P.size
     omask = None
     if fov:  # device: the product's mask; oracle: its own restatement, blacked out after the render
@@ -165,6 +168,19 @@ def test_parity_edge_states_shaping_and_truncation():
         _edge_states(recs, layout, P)
         LY.RecordView(recs[0], layout).hi[LY.HI["KSTEPS"]] = P.max_actions - 2  # truncation on step 2
     run_parity(["rt_easy_v1"], 10, 4, reward="shaping_base_v1", seed0=4242, edit=edit)
+
+
+def test_parity_fused_step():
+    """CBEV_STEP_FUSED (k_step: two envs per workgroup, ego + raster + collision in one
+    launch) against the oracle on every config; odd env counts leave a half-full
+    last workgroup."""
+    from carlabev_env_amd._lib import STEP_FUSED
+    run_parity(["rt_no_traffic_v1"], 47, 60, seed0=10_000, mode=STEP_FUSED)
+    run_parity(["rt_hard_v1"], 31, 60, seed0=20_000, act_seed=7, mode=STEP_FUSED)
+    run_parity(["rt_medium_v1"], 12, 40, profile="continuous_gsb_v1", seed0=40_000, act_seed=99, mode=STEP_FUSED)
+    run_parity(["mix3"], 13, 40, size=256, seed0=30_000, mode=STEP_FUSED)
+    run_parity(["rt_easy_v1", "jaywalk"], 9, 40, reward="shaping_base_v1", anchor_y=0.2, seed0=5, mode=STEP_FUSED)
+    run_parity(["rt_medium_v1"], 10, 6, seed0=777, edit=_edge_states, mode=STEP_FUSED)
 
 
 def test_bank_reset_and_wrapper_expansion():
