@@ -462,10 +462,11 @@ __device__ __forceinline__ int xcd_env4_of_wg(int w, int wave, int n) {
 // ---- in-kernel phase stamps (timing builds only, -DCBEV_TIMING): thread 0 of
 // each workgroup records s_memtime at phase boundaries; read by cbev_debug_times.
 #ifdef CBEV_TIMING
-__device__ unsigned long long g_stamps[6][4096][4];
-__device__ unsigned long long g_rtstamps[6][4096][4];  // s_memrealtime (constant 100 MHz)
-__device__ unsigned g_xcc[6][4096];                    // XCC (XCD) the workgroup ran on
-__device__ unsigned g_hwid[6][4096];                   // HW_ID (SE / SH / CU / SIMD) of its wave 0
+#define CBEV_NSTAMP 7
+__device__ unsigned long long g_stamps[CBEV_NSTAMP][4096][4];
+__device__ unsigned long long g_rtstamps[CBEV_NSTAMP][4096][4];  // s_memrealtime (constant 100 MHz)
+__device__ unsigned g_xcc[CBEV_NSTAMP][4096];                    // XCC (XCD) the workgroup ran on
+__device__ unsigned g_hwid[CBEV_NSTAMP][4096];                   // HW_ID (SE / SH / CU / SIMD) of its wave 0
 #define CBEV_STAMP(kern, slot)                                                  \
   if (threadIdx.x == 0 && blockIdx.x < 4096) {                                  \
     g_stamps[kern][blockIdx.x][slot] = __builtin_amdgcn_s_memtime();            \
@@ -793,6 +794,19 @@ __global__ __launch_bounds__(256) void k_hero(KArgs K, uint8_t* __restrict__ rec
 // k_hero, so the scene clock hd[T] is already advanced.
 // t_ahead = 1: launched before k_step, which advances the scene clock itself,
 // so the actors take hd[T] + dt (the same float64 sum k_step stores).
+//
+// Up to 64 actors: Actor.step in three passes over the wave.
+//   1. lane per actor: behaviour, target speed, the frozen-at-route-end test,
+//      the front axle of calc_target_index;
+//   2. calc_target_index for AG actors at a time, AW lanes per actor over its
+//      route points (coalesced reads of the actor's contiguous route instead of
+//      one strided gather per lane and point): squared-distance minimum, then
+//      hypot over the candidates within (1 + 1e-14) of it, first arg-min by
+//      group reduction (d_target_index_serial's semantics);
+//   3. lane per actor: the rest of stanley_control, PID, State.update.
+// More than 64 actors: d_actor_step per lane.
+#define AW 8
+#define AG (64 / AW)
 __global__ __launch_bounds__(256) void k_actors(KArgs K, uint8_t* __restrict__ recs, int n, int t_ahead) {
   const int lane = threadIdx.x & 63;
   const int e = xcd_env4_of_wg(blockIdx.x, threadIdx.x >> 6, n);
@@ -801,8 +815,104 @@ __global__ __launch_bounds__(256) void k_actors(KArgs K, uint8_t* __restrict__ r
   const int nact = r.hi[CBEV_HI_NACT];
   if (nact == 0) return;
   const double t = t_ahead ? r.hd[CBEV_HD_T] + CB_DT : r.hd[CBEV_HD_T];
-  for (int a = lane; a < nact; a += 64) d_actor_step(r, a, t);
+  if (nact > 64) {
+    for (int a = lane; a < nact; a += 64) d_actor_step(r, a, t);
+    return;
+  }
+  const int RA = r.RA;
+  CBEV_STAMP(6, 0);
+  // ---- 1
+  const int a = lane;
+  bool live = false;
+  int nrt = 0, tid0 = 0;
+  double s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  double fx = 0.0, fy = 0.0, ts = 0.0;
+  if (a < nact) {
+    d_behavior(r, a, t);
+    ts = RAD(r, CBEV_AD_T_SPEED, a);
+    RAD(r, CBEV_AD_CT_SPEED, a) = ts;
+    nrt = RAI(r, CBEV_AI_NROUTE, a);
+    tid0 = RAI(r, CBEV_AI_TIDX, a);
+    if (tid0 >= nrt - 1) {
+      RAD(r, CBEV_AD_CT_SPEED, a) = 0.0;  // frozen at route end
+    } else {
+      live = true;
+      s[0] = RAD(r, CBEV_AD_X, a);
+      s[1] = RAD(r, CBEV_AD_Y, a);
+      s[2] = RAD(r, CBEV_AD_YAW, a);
+      s[3] = RAD(r, CBEV_AD_V, a);
+      fx = s[0] + CB_WHEELBASE * cos(s[2]);
+      fy = s[1] + CB_WHEELBASE * sin(s[2]);
+    }
+  }
+  CBEV_STAMP(6, 1);
+  // ---- 2
+  const uint64_t livem = __ballot(live);
+  const int g = lane / AW, sub = lane - g * AW;
+  int best = 0;
+  for (int r0 = 0; r0 < nact; r0 += AG) {
+    const int aa = r0 + g;  // this group's actor
+    const double gfx = __shfl(fx, aa & 63), gfy = __shfl(fy, aa & 63);
+    const int gn = __shfl(nrt, aa & 63);
+    const bool glive = aa < nact && ((livem >> (aa & 63)) & 1ull);
+    const double* cx = r.acx + (int64_t)(aa & 63) * RA;
+    const double* cy = r.acy + (int64_t)(aa & 63) * RA;
+    double m2 = INFINITY;
+    if (glive) {
+#pragma unroll 4
+      for (int i = sub; i < gn; i += AW) {
+        const double dx = gfx - cx[i], dy = gfy - cy[i];
+        const double d2 = dx * dx + dy * dy;
+        m2 = d2 < m2 ? d2 : m2;
+      }
+    }
+    m2 = group_min<AW>(m2);
+    const double lim = m2 * (1.0 + 1e-14);
+    double bd = INFINITY;
+    int bi = 0x7fffffff;
+    if (glive) {
+      for (int i = sub; i < gn; i += AW) {
+        const double dx = gfx - cx[i], dy = gfy - cy[i];
+        if (!(dx * dx + dy * dy <= lim)) continue;
+        const double h = hypot(dx, dy);
+        if (bi == 0x7fffffff || h < bd) {  // the first candidate is taken as is (serial `first`)
+          bd = h;
+          bi = i;
+        }
+      }
+    }
+    group_argmin<AW>(bd, bi);
+    // the owner lane of actor r0 + k takes group k's result
+    const int got = __shfl(bi, ((lane - r0) & (AG - 1)) * AW);
+    if (lane >= r0 && lane < r0 + AG) best = got == 0x7fffffff ? 0 : got;
+  }
+  CBEV_STAMP(6, 2);
+  // ---- 3: stanley_control (stanley_controller.py:64-89), pid_control, State.update
+  if (live) {
+    const double* cx = r.acx + (int64_t)a * RA;
+    const double* cy = r.acy + (int64_t)a * RA;
+    const double* cyaw = r.acyaw + (int64_t)a * RA;
+    const double yaw = s[2];
+    const double fa0 = -cos(yaw + CB_PI / 2.0), fa1 = -sin(yaw + CB_PI / 2.0);
+    const double err = (fx - cx[best]) * fa0 + (fy - cy[best]) * fa1;
+    const int cur = tid0 >= best ? tid0 : best;
+    const double theta_e = d_angle_mod(cyaw[cur] - yaw);
+    const double theta_d = atan2(2.0 * err, d_pymax(s[3], 1e-3));
+    const double max_steer = 30.0 * (CB_PI / 180.0);
+    const double di = d_clip(theta_e + theta_d, -max_steer, max_steer);
+    RAI(r, CBEV_AI_TIDX, a) = cur;
+    const double ai = 1.0 * (ts - s[3]);
+    d_state_update(s, ai, di, ts);
+    RAD(r, CBEV_AD_X, a) = s[0];
+    RAD(r, CBEV_AD_Y, a) = s[1];
+    RAD(r, CBEV_AD_YAW, a) = s[2];
+    RAD(r, CBEV_AD_V, a) = s[3];
+    RAD(r, CBEV_AD_TIME, a) += CB_DT;
+  }
+  CBEV_STAMP(6, 3);
 }
+#undef AW
+#undef AG
 
 // Output pass over one wave's chunks of 1024 output pixels (16 / G rows). A
 // chunk is four 256-pixel dword groups: in group d lane l owns the 4
@@ -1145,16 +1255,27 @@ __device__ __forceinline__ void raster_env(const KArgs& K, const DRec& r, uint8_
   }
 }
 
-// G = size / 64 (64-pixel gathers per output row)
+// G = size / 64 (64-pixel gathers per output row). CBEV_RASTER_NE envs per
+// workgroup, rendered one after the other through the same LDS image.
+#ifndef CBEV_RASTER_NE
+#define CBEV_RASTER_NE 1
+#endif
 template <int G>
 __global__ __launch_bounds__(256) void k_raster(KArgs K, uint8_t* __restrict__ recs, int n,
                                                 uint8_t* __restrict__ frames) {
   extern __shared__ __align__(16) uint8_t lds[];
-  const int e = xcd_env_of_wg(blockIdx.x, n);
-  if (e >= n) return;
+  const int ng = (n + CBEV_RASTER_NE - 1) / CBEV_RASTER_NE;
+  const int g = xcd_env_of_wg(blockIdx.x, ng);
+  if (g >= ng) return;
   CBEV_STAMP(2, 0);
-  DRec r = bind_rec(recs + (int64_t)e * K.L.record_bytes, K.L, K.C);
-  raster_env<false, G>(K, r, frames + (int64_t)e * K.P.size * K.P.size, 1, 0, lds);
+#pragma unroll 1
+  for (int k = 0; k < CBEV_RASTER_NE; ++k) {
+    const int e = CBEV_RASTER_NE == 1 ? g : g + k * ng;  // env blocks keep their XCD
+    if (e >= n) break;
+    if (k > 0) __syncthreads();  // the next env's staging overwrites the crop image
+    DRec r = bind_rec(recs + (int64_t)e * K.L.record_bytes, K.L, K.C);
+    raster_env<false, G>(K, r, frames + (int64_t)e * K.P.size * K.P.size, 1, 0, lds);
+  }
   CBEV_STAMP(2, 3);
 }
 
@@ -2683,10 +2804,11 @@ int cbev_step(cbev_ctx* c, void* records, int n, const void* actions, uint8_t* f
   if (ev) HIP_TRY(hipEventRecord(ev[1], s));
   {
     const size_t lb = raster_lds_bytes(c->P);
+    const int rg = (n + CBEV_RASTER_NE - 1) / CBEV_RASTER_NE;
     switch (c->P.size) {
-      case 64: hipLaunchKernelGGL(k_raster<1>, dim3(n), dim3(256), lb, s, K, (uint8_t*)records, n, frames); break;
-      case 128: hipLaunchKernelGGL(k_raster<2>, dim3(n), dim3(256), lb, s, K, (uint8_t*)records, n, frames); break;
-      default: hipLaunchKernelGGL(k_raster<4>, dim3(n), dim3(256), lb, s, K, (uint8_t*)records, n, frames); break;
+      case 64: hipLaunchKernelGGL(k_raster<1>, dim3(rg), dim3(256), lb, s, K, (uint8_t*)records, n, frames); break;
+      case 128: hipLaunchKernelGGL(k_raster<2>, dim3(rg), dim3(256), lb, s, K, (uint8_t*)records, n, frames); break;
+      default: hipLaunchKernelGGL(k_raster<4>, dim3(rg), dim3(256), lb, s, K, (uint8_t*)records, n, frames); break;
     }
   }
   if (ev) HIP_TRY(hipEventRecord(ev[2], s));
@@ -2951,13 +3073,15 @@ int cbev_resize_obs(cbev_ctx* c, const uint8_t* frames, int n, const uint8_t* ma
 // timing builds only: copy the phase stamps [6][4096][4] (u64 s_memtime ticks), realtime stamps,
 // XCC ids | HW_ID << 32
 int cbev_debug_times(unsigned long long* out_host) {
+  // [2][CBEV_NSTAMP][4096][4] s_memtime / s_memrealtime stamps, then [CBEV_NSTAMP][4096] xcc | hwid << 32
+  const int NS = CBEV_NSTAMP;
   if (hipMemcpyFromSymbol(out_host, HIP_SYMBOL(g_stamps), sizeof(g_stamps)) != hipSuccess) return -1;
-  if (hipMemcpyFromSymbol(out_host + 6 * 4096 * 4, HIP_SYMBOL(g_rtstamps), sizeof(g_rtstamps)) != hipSuccess) return -1;
-  static unsigned x[6 * 4096];
+  if (hipMemcpyFromSymbol(out_host + NS * 4096 * 4, HIP_SYMBOL(g_rtstamps), sizeof(g_rtstamps)) != hipSuccess) return -1;
+  static unsigned x[CBEV_NSTAMP * 4096];
   if (hipMemcpyFromSymbol(x, HIP_SYMBOL(g_xcc), sizeof(x)) != hipSuccess) return -1;
-  static unsigned h[6 * 4096];
+  static unsigned h[CBEV_NSTAMP * 4096];
   if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_hwid), sizeof(h)) != hipSuccess) return -1;
-  for (int i = 0; i < 6 * 4096; ++i) out_host[12 * 4096 * 4 + i] = x[i] | ((unsigned long long)h[i] << 32);
+  for (int i = 0; i < NS * 4096; ++i) out_host[2 * NS * 4096 * 4 + i] = x[i] | ((unsigned long long)h[i] << 32);
   return 0;
 }
 

@@ -44,13 +44,14 @@ for b in (19656, 20480, 20481):
 for t in range(a.steps):
     env.step_async_only(acts[t])
 torch.cuda.synchronize()
-buf = np.zeros(2 * 6 * 4096 * 4 + 6 * 4096, np.uint64)
+NS = 7
+buf = np.zeros(2 * NS * 4096 * 4 + NS * 4096, np.uint64)
 assert L.cbev_debug_times(buf.ctypes.data_as(ctypes.c_void_p)) == 0
-xcc = buf[2 * 6 * 4096 * 4:].reshape(6, 4096).astype(np.int64)
+xcc = buf[2 * NS * 4096 * 4:].reshape(NS, 4096).astype(np.int64)
 hwid = xcc >> 32
 xcc = xcc & 0xFFFFFFFF
-buf = buf[:2 * 6 * 4096 * 4].reshape(2, 6, 4096, 4)
-for k, name in enumerate(("k_hero", "k_collide", "k_raster", "k_hero after P1 / P2 / A / B (slots 0-3)", "collide_env(thread0)", "k_collide pre-pass: segs/targets/actors+sync")):
+buf = buf[:2 * NS * 4096 * 4].reshape(2, NS, 4096, 4)
+for k, name in enumerate(("k_hero", "k_collide", "k_raster", "k_hero after P1 / P2 / A / B (slots 0-3)", "collide_env(thread0)", "k_collide pre-pass: segs/targets/actors+sync", "k_actors: behaviour / search / stanley+update (wave 0 of each WG)")):
     if not (buf[0, k, :, 0] > 0).any():
         continue
     st = buf[0, k].astype(np.int64)
