@@ -161,7 +161,7 @@ __device__ int d_smooth_route(DRec& r, int a) {
 
 // BaseJaywalkBehavior._start_retreat (jaywalk.py:43-54) + Actor.set_route_surface
 // (actor.py:139-149) + Controller.set_route(jitter_start=False).
-__device__ void d_start_retreat(DRec& r, int a) {
+__device__ __noinline__ void d_start_retreat(DRec& r, int a) {
   const int RA = r.RA;
   int nrx = RAI(r, CBEV_AI_NRX, a);
   int cur = RAI(r, CBEV_AI_TIDX, a);
@@ -798,16 +798,67 @@ __global__ __launch_bounds__(256) void k_hero(KArgs K, uint8_t* __restrict__ rec
 // Up to 64 actors: Actor.step in three passes over the wave.
 //   1. lane per actor: behaviour, target speed, the frozen-at-route-end test,
 //      the front axle of calc_target_index;
-//   2. calc_target_index for AG actors at a time, AW lanes per actor over its
-//      route points (coalesced reads of the actor's contiguous route instead of
-//      one strided gather per lane and point): squared-distance minimum, then
+//   2. calc_target_index with 64 / nact (rounded down to a power of two) lanes
+//      per actor over its route points, all actors in one round (coalesced
+//      reads of each actor's contiguous route instead of one strided gather
+//      per lane and point): squared-distance minimum, then
 //      hypot over the candidates within (1 + 1e-14) of it, first arg-min by
 //      group reduction (d_target_index_serial's semantics);
 //   3. lane per actor: the rest of stanley_control, PID, State.update.
 // More than 64 actors: d_actor_step per lane.
-#define AW 8
-#define AG (64 / AW)
-__global__ __launch_bounds__(256) void k_actors(KArgs K, uint8_t* __restrict__ recs, int n, int t_ahead) {
+// calc_target_index of every live actor of one env (nact <= 64): AW lanes per
+// actor, 64 / AW actors per round; returns lane a's result for actor a
+template <int AW>
+__device__ __forceinline__ int actor_search(const DRec& r, int nact, uint64_t livem, double fx, double fy, int nrt,
+                                            int lane) {
+  constexpr int AG = 64 / AW;
+  const int RA = r.RA;
+  const int g = lane / AW, sub = lane - g * AW;
+  int best = 0;
+  for (int r0 = 0; r0 < nact; r0 += AG) {
+    const int aa = r0 + g;  // this group's actor
+    const double gfx = __shfl(fx, aa & 63), gfy = __shfl(fy, aa & 63);
+    const int gn = __shfl(nrt, aa & 63);
+    const bool glive = aa < nact && ((livem >> (aa & 63)) & 1ull);
+    const double* cx = r.acx + (int64_t)(aa & 63) * RA;
+    const double* cy = r.acy + (int64_t)(aa & 63) * RA;
+    double m2 = INFINITY;
+    if (glive) {
+#pragma unroll 8
+      for (int i = sub; i < gn; i += AW) {
+        const double dx = gfx - cx[i], dy = gfy - cy[i];
+        const double d2 = dx * dx + dy * dy;
+        m2 = d2 < m2 ? d2 : m2;
+      }
+    }
+    m2 = group_min<AW>(m2);
+    const double lim = m2 * (1.0 + 1e-14);
+    double bd = INFINITY;
+    int bi = 0x7fffffff;
+    if (glive) {
+      for (int i = sub; i < gn; i += AW) {
+        const double dx = gfx - cx[i], dy = gfy - cy[i];
+        if (!(dx * dx + dy * dy <= lim)) continue;
+        const double h = hypot(dx, dy);
+        if (bi == 0x7fffffff || h < bd) {  // the first candidate is taken as is (serial `first`)
+          bd = h;
+          bi = i;
+        }
+      }
+    }
+    group_argmin<AW>(bd, bi);
+    // the owner lane of actor r0 + k takes group k's result
+    const int got = __shfl(bi, ((lane - r0) & (AG - 1)) * AW);
+    if (lane >= r0 && lane < r0 + AG) best = got == 0x7fffffff ? 0 : got;
+  }
+  return best;
+}
+
+// waves per SIMD the register allocation must allow (occupancy vs spills)
+#ifndef CBEV_ACTORS_WAVES
+#define CBEV_ACTORS_WAVES 1
+#endif
+__global__ __launch_bounds__(256, CBEV_ACTORS_WAVES) void k_actors(KArgs K, uint8_t* __restrict__ recs, int n, int t_ahead) {
   const int lane = threadIdx.x & 63;
   const int e = xcd_env4_of_wg(blockIdx.x, threadIdx.x >> 6, n);
   if (e >= n) return;
@@ -848,43 +899,17 @@ __global__ __launch_bounds__(256) void k_actors(KArgs K, uint8_t* __restrict__ r
   CBEV_STAMP(6, 1);
   // ---- 2
   const uint64_t livem = __ballot(live);
-  const int g = lane / AW, sub = lane - g * AW;
-  int best = 0;
-  for (int r0 = 0; r0 < nact; r0 += AG) {
-    const int aa = r0 + g;  // this group's actor
-    const double gfx = __shfl(fx, aa & 63), gfy = __shfl(fy, aa & 63);
-    const int gn = __shfl(nrt, aa & 63);
-    const bool glive = aa < nact && ((livem >> (aa & 63)) & 1ull);
-    const double* cx = r.acx + (int64_t)(aa & 63) * RA;
-    const double* cy = r.acy + (int64_t)(aa & 63) * RA;
-    double m2 = INFINITY;
-    if (glive) {
-#pragma unroll 4
-      for (int i = sub; i < gn; i += AW) {
-        const double dx = gfx - cx[i], dy = gfy - cy[i];
-        const double d2 = dx * dx + dy * dy;
-        m2 = d2 < m2 ? d2 : m2;
-      }
-    }
-    m2 = group_min<AW>(m2);
-    const double lim = m2 * (1.0 + 1e-14);
-    double bd = INFINITY;
-    int bi = 0x7fffffff;
-    if (glive) {
-      for (int i = sub; i < gn; i += AW) {
-        const double dx = gfx - cx[i], dy = gfy - cy[i];
-        if (!(dx * dx + dy * dy <= lim)) continue;
-        const double h = hypot(dx, dy);
-        if (bi == 0x7fffffff || h < bd) {  // the first candidate is taken as is (serial `first`)
-          bd = h;
-          bi = i;
-        }
-      }
-    }
-    group_argmin<AW>(bd, bi);
-    // the owner lane of actor r0 + k takes group k's result
-    const int got = __shfl(bi, ((lane - r0) & (AG - 1)) * AW);
-    if (lane >= r0 && lane < r0 + AG) best = got == 0x7fffffff ? 0 : got;
+  // lanes per actor: the widest group that still takes every actor in one round
+  const int aw = nact <= 1 ? 64 : nact <= 2 ? 32 : nact <= 4 ? 16 : nact <= 8 ? 8 : nact <= 16 ? 4 : nact <= 32 ? 2 : 1;
+  int best;
+  switch (aw) {
+    case 64: best = actor_search<64>(r, nact, livem, fx, fy, nrt, lane); break;
+    case 32: best = actor_search<32>(r, nact, livem, fx, fy, nrt, lane); break;
+    case 16: best = actor_search<16>(r, nact, livem, fx, fy, nrt, lane); break;
+    case 8: best = actor_search<8>(r, nact, livem, fx, fy, nrt, lane); break;
+    case 4: best = actor_search<4>(r, nact, livem, fx, fy, nrt, lane); break;
+    case 2: best = actor_search<2>(r, nact, livem, fx, fy, nrt, lane); break;
+    default: best = actor_search<1>(r, nact, livem, fx, fy, nrt, lane); break;
   }
   CBEV_STAMP(6, 2);
   // ---- 3: stanley_control (stanley_controller.py:64-89), pid_control, State.update
@@ -911,8 +936,7 @@ __global__ __launch_bounds__(256) void k_actors(KArgs K, uint8_t* __restrict__ r
   }
   CBEV_STAMP(6, 3);
 }
-#undef AW
-#undef AG
+
 
 // Output pass over one wave's chunks of 1024 output pixels (16 / G rows). A
 // chunk is four 256-pixel dword groups: in group d lane l owns the 4

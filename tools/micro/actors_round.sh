@@ -3,4 +3,4 @@ set -u
 mkdir -p gpurun_out
 timeout -k 10 600 python -u -m pytest tests -x -q -m gpu --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 || { echo pytest failed; tail -30 gpurun_out/pytest_gpu.log; exit 1; }
 tail -1 gpurun_out/pytest_gpu.log
-CONFIGS="${CONFIGS:-3 5}" bash tools/micro/configs.sh
+CFGS="${CFGS:-3 5}" bash tools/micro/step_variants.sh
