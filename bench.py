@@ -168,6 +168,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-wire", action="store_true")
+    ap.add_argument("--raster-reps", type=int, default=50, help="back-to-back k_raster launches timed for the roofline")
     args = ap.parse_args()
 
     import torch
@@ -253,6 +254,17 @@ def main():
         reseed()
         el_prof, ms3, _ = timed(False, True)  # same workload with HIP events around each kernel (roofline)
         value = world * n * args.steps / el
+        burst_ms = None
+        if lib().cbev_step_mode(env._ctx) == 1 and hasattr(lib(), "cbev_profile_raster"):
+            # k_raster's own launch duration: one more step (no reset, so every
+            # record holds this step's render set-up), then a burst of raster
+            # launches over it between two events (cbev_profile_raster); the
+            # per-kernel events above also count each launch's dispatch gap
+            env.step_async_only(acts[total_steps - 1])
+            bm = ctypes.c_double()
+            check(lib().cbev_profile_raster(env._ctx, env.records.data_ptr(), n, env.frames().data_ptr(),
+                                            args.raster_reps, env._stream(), ctypes.byref(bm)), "profile_raster")
+            burst_ms = bm.value
         wire_value = None
         if not args.no_wire:
             reseed()
@@ -270,7 +282,7 @@ def main():
         from carlabev_env_amd import layout as LY
         hi = LY.batch_views(np.ascontiguousarray(host_recs).reshape(-1), env.layout, host_recs.shape[0])["hi"]
         algo_bytes += int(round(16 * (mode == 0) * hi[:, LY.HI["NROUTE"]].mean() + 16 * hi[:, LY.HI["NRAW"]].mean()))
-    raster_ms = ms3[1]
+    raster_ms = burst_ms if burst_ms is not None else ms3[1]
     achieved = n * algo_bytes / (raster_ms * 1e-3) / 1e9
     traffic = None
     pmc_path = os.path.join(REPO, "profiles", f"pmc_raster_config{args.config}.json")
@@ -304,6 +316,7 @@ def main():
             "step_mode": ("fused", "split", "raster_collide")[mode],
             "kernel_ms": ({("k_hero+k_actors" if mode == 2 else "k_actors"): round(ms3[0], 5), "k_step": round(ms3[1], 5)} if fused else
                           {"k_hero+k_actors": round(ms3[0], 5), "k_raster": round(ms3[1], 5), "k_collide": round(ms3[2], 5)}),
+            "raster_ms_per_launch": None if burst_ms is None else round(burst_ms, 5),
             "roofline": {"bound": "hbm", "kernel": "k_step" if fused else "k_raster", "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic, "algorithmic_bytes_per_env": algo_bytes},

@@ -939,14 +939,21 @@ __global__ __launch_bounds__(256, CBEV_ACTORS_WAVES) void k_actors(KArgs K, uint
 
 
 // Output pass over one wave's chunks of 1024 output pixels (16 / G rows). A
-// chunk is four 256-pixel dword groups: in group d lane l owns the 4
-// consecutive output pixels 256 d + 4 l .. + 3 of the chunk (row r + d (4 / G)
-// + l / (16 G), columns 4 (l % (16 G)) .. + 3), gathers them one column step
-// apart and packs them into one dword, so each group is ONE 256-byte dword
-// store. Source coordinates are stepped, not recomputed (pygame's rotozoom is
-// affine in the output pixel): per gather one 64-bit add, a 24-bit
-// multiply-add for the LDS byte address, the LDS read, the nibble extract and
-// the pack.
+// chunk is four dword groups; group d covers columns [d S/4, (d+1) S/4) of
+// every row of the chunk: lane l owns the 4 consecutive pixels from column
+// d S/4 + 4 (l % 4G) of row l / 4G, gathers them (one LDS read per pixel, b =
+// 0..3) and stores them as one dword. A gather instruction therefore samples
+// 16 / G rows x 4G pixel blocks rather than one or two whole rows: whatever the
+// rotation, the 32 lanes of an LDS lane group then spread over the banks (the
+// rows of a block land in one dword of the odd-stride image, the blocks of a
+// row step 4 texels along the rotated row); with whole rows per instruction a
+// vertical source direction stepped 4 image rows per lane, i.e. 4 sd = 0 mod 4
+// dwords: 4-way conflicts. Each store instruction writes 4G-dword runs of
+// 16 / G rows; the wave's four groups complete every row of the chunk.
+// Source coordinates are stepped, not recomputed (pygame's rotozoom is affine
+// in the output pixel): per gather one 64-bit add, a 24-bit multiply-add for the
+// LDS byte address, the LDS read, the nibble extract and the pack; rotate90
+// steps an LDS texel address.
 //   CHECK = false: the rotated surface covers the whole output and every output
 //   pixel samples inside the crop (checked once per env at the four corners;
 //   the map is affine) -> no per-pixel tests.
@@ -959,25 +966,15 @@ __device__ __forceinline__ void raster_out(const cbev_params& P, const RotSetup&
                                            const uint32_t* __restrict__ fov) {
   constexpr int RPC = 16 / G;  // output rows per chunk
   constexpr int S = 64 * G;    // == P.size
-  constexpr int LPR = S / 4;   // lanes per output row
-  constexpr int RPD = 4 / G;   // output rows per dword group
+  constexpr int LPR = 4 * G;   // lanes per output row in one dword group
+  constexpr int GC = S / 4;    // columns per dword group
   constexpr bool BYTES = raster_bytes(S);
   const int C = P.crop;
   const uint32_t vmax = (uint32_t)((C << 16) - 1);
   const int hero_w = P.hero_w;
   const int hx0 = P.anchor_x - hero_w / 2, hy0 = P.anchor_y - hero_w / 2;
   const int lrow = lane / LPR, lcol = 4 * (lane % LPR);
-  // this lane's columns: hero byte mask (Hero.draw: black w x w rect at the
-  // anchor, hero.py:26-32) and the compose-clip column test
-  uint32_t hmask = 0, xok = 0;
-#pragma unroll
-  for (int b = 0; b < 4; ++b) {
-    const int u = lcol + b;
-    if (u >= hx0 && u < hx0 + hero_w) hmask |= 0xffu << (8 * b);
-    const int xx = u - R.rx0;
-    if (xx >= 0 && xx < R.nx) xok |= 1u << b;
-  }
-  const uint32_t hblack = hmask & (CBEV_PX_BLACK * 0x01010101u);
+  const uint32_t hblack = CBEV_PX_BLACK * 0x01010101u;
   const int r0 = wave * RPC;
   const int xx0 = lcol - R.rx0, yy0 = r0 + lrow - R.ry0;
   // lane state at (output row r0 + lrow, column lcol) of this wave's first chunk
@@ -998,25 +995,29 @@ __device__ __forceinline__ void raster_out(const cbev_params& P, const RotSetup&
   const uint64_t chunk_step =
       (uint64_t)(((int64_t)(chunk_rows * R.icos) << 32) + (int64_t)(-chunk_rows * R.isin));
   // one output row down: (dx, dy) += (-isin, icos); one column right: += (icos, isin)
-  const uint64_t group_step = (uint64_t)(((int64_t)(RPD * R.icos) << 32) + (int64_t)(-RPD * R.isin));
+  const uint64_t group_step = (uint64_t)(((int64_t)(GC * R.isin) << 32) + (int64_t)(GC * R.icos));
   const uint64_t col_step = (uint64_t)(((int64_t)R.isin << 32) + (int64_t)R.icos);
   for (int ch = wave, r = r0; ch < nchunks; ch += NW, r += chunk_rows) {
+    const int row = r + lrow;  // this lane's output row
     // the frame is written through the uniform base `out` plus a per-lane offset
-    const uint32_t vo = (uint32_t)(r * S + 4 * lane);
+    const uint32_t vo = (uint32_t)(row * S + lcol);
     const bool hero_rows = (unsigned)(r + RPC - 1 - hy0) < (unsigned)(RPC - 1 + hero_w);  // chunk meets the hero rows
+    const bool row_ok = !CHECK || (unsigned)(row - R.ry0) < (unsigned)R.ny;  // compose clip (rows)
     asm volatile("" : "+v"(pxy), "+v"(sa));  // keep the per-gather offsets as scalar adds
     uint32_t w[4];
-    uint64_t qg = pxy;  // general path: source coordinates of (row r + d RPD + lrow, column lcol)
+    uint64_t qg = pxy;  // general path: source coordinates of (row, column d GC + lcol)
 #pragma unroll
     for (int d = 0; d < 4; ++d) {
       uint32_t acc = 0;
 #pragma unroll
       for (int b = 0; b < 4; ++b) {
         uint32_t v;
+        // compose clip (columns): rotated-surface column of this pixel
+        const bool col_ok = !CHECK || (unsigned)(lcol + d * GC + b - R.rx0) < (unsigned)R.nx;
         if (R90) {
-          const int a = sa + d * RPD * R.vstep + b * R.ustep;
+          const int a = sa + (d * GC + b) * R.ustep;
           if (CHECK) {
-            const bool ok = ((xok >> b) & 1u) && (unsigned)(r + d * RPD + lrow - R.ry0) < (unsigned)R.ny;
+            const bool ok = col_ok && row_ok;
             v = ok ? lds_texel<BYTES>(img, ok ? a : 0) : (uint32_t)CBEV_PX_BLACK;
           } else {
             v = lds_texel<BYTES>(img, a);
@@ -1028,7 +1029,7 @@ __device__ __forceinline__ void raster_out(const cbev_params& P, const RotSetup&
           const uint32_t nsh = BYTES ? 0u : (dx >> 14) & 4u;
           if (CHECK) {  // bounds on the unshifted source coordinate
             const int ux = (int)dx - (shift << 16);
-            const bool ok = ((xok >> b) & 1u) && (unsigned)(r + d * RPD + lrow - R.ry0) < (unsigned)R.ny;
+            const bool ok = col_ok && row_ok;
             const bool in = (uint32_t)ux <= vmax && dy <= vmax;
             const uint32_t s = BYTES ? img[(in && ok) ? byte : 0u] : (img[(in && ok) ? byte : 0u] >> nsh) & 15u;
             v = !ok ? (uint32_t)CBEV_PX_BLACK : (in ? s : bg);
@@ -1041,16 +1042,21 @@ __device__ __forceinline__ void raster_out(const cbev_params& P, const RotSetup&
       w[d] = acc;
       if (!R90) qg += group_step;
     }
-    if (hero_rows) {
+    if (hero_rows && (unsigned)(row - hy0) < (unsigned)hero_w) {  // Hero.draw: black w x w rect at the anchor (hero.py:26-32)
 #pragma unroll
-      for (int d = 0; d < 4; ++d)
-        if ((unsigned)(r + d * RPD + lrow - hy0) < (unsigned)hero_w) w[d] = (w[d] & ~hmask) | hblack;
+      for (int d = 0; d < 4; ++d) {
+        uint32_t hm = 0;
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+          if ((unsigned)(lcol + d * GC + b - hx0) < (unsigned)hero_w) hm |= 0xffu << (8 * b);
+        w[d] = (w[d] & ~hm) | (hm & hblack);
+      }
     }
     if (fov) {  // FovRenderer.apply_mask (fov.py:96-99): black corner triangles (uniform branch)
 #pragma unroll
       for (int d = 0; d < 4; ++d) {
-        const uint32_t fm = fov[(vo >> 2) + 64 * d];
-        w[d] = (w[d] & ~fm) | (fm & (CBEV_PX_BLACK * 0x01010101u));
+        const uint32_t fm = fov[(vo + (uint32_t)(d * GC)) >> 2];
+        w[d] = (w[d] & ~fm) | (fm & hblack);
       }
     }
     if (CBEV_RASTER_PHASES & 8) {
@@ -1058,7 +1064,7 @@ __device__ __forceinline__ void raster_out(const cbev_params& P, const RotSetup&
         uint8_t* ob = out + (int64_t)k * out_stride;
 #pragma unroll
         for (int d = 0; d < 4; ++d)  // streamed out: keep the L2 for the map and the records
-          __builtin_nontemporal_store(w[d], (uint32_t*)(ob + (vo + (uint32_t)(256 * d))));
+          __builtin_nontemporal_store(w[d], (uint32_t*)(ob + (vo + (uint32_t)(d * GC))));
       }
     } else {
       if ((w[0] ^ w[1] ^ w[2] ^ w[3]) == 0x7fffffffu) out[vo] = 1;  // keeps the gathers live
@@ -1182,123 +1188,227 @@ struct NoSideWork {
   __device__ void operator()(int) const {}
 };
 
+// One env's render set-up: crop origin, rotation, fast-path flag and the paint
+// inputs. RESET: BaseMap.reset's frame (theta = 0, no actors drawn,
+// world.py:92-100) at the record's pose; otherwise the RS_* ints k_hero wrote.
+struct RasterJob {
+  int xmin, ymin, shift, xa;  // crop origin, its texel offset in the dword-aligned LDS row, packed byte column
+  RotSetup R;
+  bool fast;
+  PaintPre pq;
+};
+
+template <bool RESET, int G>
+__device__ __forceinline__ void raster_origin(const KArgs& K, const DRec& r, RasterJob& J) {
+  if (RESET) {
+    d_crop_origin(K.P, r.hd[CBEV_HD_X], r.hd[CBEV_HD_Y], &J.xmin, &J.ymin);
+  } else if (CBEV_RASTER_PHASES & 16) {
+    J.xmin = r.hi[CBEV_HI_RS_XMIN];
+    J.ymin = r.hi[CBEV_HI_RS_YMIN];
+  } else {  // (phase experiments only) a fixed pose, no record read
+    J.xmin = J.ymin = 1000;
+  }
+  J.xa = (J.xmin >> 1) & ~3;  // packed byte column (dword aligned)
+  J.shift = J.xmin - 2 * J.xa;  // texel offset (0..7)
+}
+
+template <bool RESET, int G>
+__device__ __forceinline__ void raster_rot(const KArgs& K, const DRec& r, RasterJob& J) {
+  const cbev_params& P = K.P;
+  const int rt = raster_row_texels(64 * G, P.crop);
+  if (RESET || !(CBEV_RASTER_PHASES & 16)) {  // BaseMap.reset: theta 0 -> rotate90 by one turn
+    J.R = rot_setup(P, 90.0f, rt);
+  } else {  // written by k_hero for this step
+    int32_t* w = (int32_t*)&J.R;
+#pragma unroll
+    for (int k = 0; k < CBEV_RS_WORDS; ++k) w[k] = r.hi[CBEV_HI_RS_R90 + k];
+  }
+  J.fast = (!RESET && (CBEV_RASTER_PHASES & 16)) ? r.hi[CBEV_HI_RS_FAST] != 0 : raster_fast(P, J.R);
+}
+
+// Crop staging: 16-byte global loads of the nibble-packed map, lane-linear over
+// the window's row chunks (STAGE_U per thread in flight), then dword LDS stores.
+// Split in an issue half (loads into registers) and a commit half (LDS stores)
+// so k_raster can hold the next env's loads in flight across an output pass.
+#define STAGE_U 5
+struct StageBuf {
+  uint4 v[STAGE_U];
+};
+template <int G>
+__device__ __forceinline__ int stage_total(const cbev_params& P) {
+  return P.crop * raster_row_chunks(64 * G, P.crop);
+}
+template <int G>
+__device__ __forceinline__ void stage_issue(const KArgs& K, const RasterJob& J, int q0, StageBuf& b) {
+  const int C = K.P.crop;
+  const int nch = raster_row_chunks(64 * G, C), total = C * nch;
+  const uint8_t* gbase = K.map + (int64_t)J.ymin * K.npitch + J.xa;
+  const int dr = 256 / nch, dj = 256 - dr * nch;
+  const int q = q0 + (int)threadIdx.x;
+  int r = q / nch, c = q - r * nch;
+#pragma unroll
+  for (int u = 0; u < STAGE_U; ++u) {
+    if (q + 256 * u < total) b.v[u] = load16_a4(gbase + (int64_t)r * K.npitch + 16 * c);
+    r += dr;
+    c += dj;
+    if (c >= nch) { c -= nch; ++r; }
+  }
+}
+template <int G>
+__device__ __forceinline__ void stage_commit(const KArgs& K, int q0, const StageBuf& b, uint8_t* __restrict__ lds) {
+  constexpr bool BYTES = raster_bytes(64 * G);
+  const int C = K.P.crop;
+  const int sd = raster_stride_dwords(64 * G, C);
+  const int nch = raster_row_chunks(64 * G, C), total = C * nch;
+  const int dr = 256 / nch, dj = 256 - dr * nch;
+  const int q = q0 + (int)threadIdx.x;
+  int row = q / nch, j = q - row * nch;
+  uint32_t* l32 = (uint32_t*)lds;
+#pragma unroll
+  for (int u = 0; u < STAGE_U; ++u) {
+    if (q + 256 * u < total) {
+      if (BYTES) {  // 32 texels -> 8 dwords; the last chunk of a row may overhang the stride
+        uint32_t* d = l32 + row * sd + 8 * j;
+        uint32_t o[8];
+        unpack_texels(b.v[u].x, o);
+        unpack_texels(b.v[u].y, o + 2);
+        unpack_texels(b.v[u].z, o + 4);
+        unpack_texels(b.v[u].w, o + 6);
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+          if (8 * j + k < sd) d[k] = o[k];
+      } else {
+        uint32_t* d = l32 + row * sd + 4 * j;
+        d[0] = b.v[u].x;  // the last chunk of a row may overhang the stride
+        if (4 * j + 1 < sd) d[1] = b.v[u].y;
+        if (4 * j + 2 < sd) d[2] = b.v[u].z;
+        if (4 * j + 3 < sd) d[3] = b.v[u].w;
+      }
+    }
+    row += dr;
+    j += dj;
+    if (j >= nch) { j -= nch; ++row; }
+  }
+}
+template <int G>
+__device__ __forceinline__ void stage_all(const KArgs& K, const RasterJob& J, uint8_t* __restrict__ lds) {
+  if (CBEV_RASTER_PHASES & 1) {
+    const int total = stage_total<G>(K.P);
+    for (int q0 = 0; q0 < total; q0 += 256 * STAGE_U) {
+      StageBuf b;
+      stage_issue<G>(K, J, q0, b);
+      stage_commit<G>(K, q0, b, lds);
+    }
+  }
+}
+
 // NW < 4: waves NW..3 run `side(lane)` (k_step: the collision / reward pass)
 // while waves 0..NW-1 write the frame; every other LDS access of `side` must
 // stay outside the crop image.
+template <int G, int NW = 4, class Side = NoSideWork>
+__device__ __forceinline__ void raster_emit(const KArgs& K, const RasterJob& J, uint8_t* __restrict__ out, int nout,
+                                            int64_t out_stride, const uint8_t* __restrict__ lds,
+                                            const Side& side = Side()) {
+  constexpr bool BYTES = raster_bytes(64 * G);
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  // ---- rotate (pygame transform.rotate / rotate90) + compose + ego overlay
+  const uint32_t bg = lds_texel<BYTES>(lds, J.shift);  // crop top-left pixel after painting
+  if (NW < 4 && wave >= NW) {
+    side(lane);
+  } else if (CBEV_RASTER_PHASES & 32) {
+    raster_out_dispatch<G, NW>(K.P, J.R, J.fast, lds, J.shift, bg, out, nout, out_stride, lane, wave, K.fov);
+  }
+}
+
+// Render one env's observation (whole 256-thread workgroup). The frame is
+// written to `nout` destinations out + k*out_stride (the frame-stack ring on reset).
 template <bool RESET, int G, int NW = 4, class Side = NoSideWork>
 __device__ __forceinline__ void raster_env(const KArgs& K, const DRec& r, uint8_t* __restrict__ out, int nout,
                                            int64_t out_stride, uint8_t* __restrict__ lds,
                                            const Side& side = Side()) {
-  const cbev_params& P = K.P;
-  const int C = P.crop;
   constexpr bool BYTES = raster_bytes(64 * G);
-  const int sd = raster_stride_dwords(64 * G, C);
-  const int rt = raster_row_texels(64 * G, C);
-  int xmin, ymin;
-  RotSetup R;
-  if (RESET) {  // BaseMap.reset: theta 0 -> rotate90 by one turn, crop at the bank record's pose
-    d_crop_origin(P, r.hd[CBEV_HD_X], r.hd[CBEV_HD_Y], &xmin, &ymin);
-    R = rot_setup(P, 90.0f, rt);
-  } else if (CBEV_RASTER_PHASES & 16) {  // written by k_hero for this step
-    xmin = r.hi[CBEV_HI_RS_XMIN];
-    ymin = r.hi[CBEV_HI_RS_YMIN];
-    int32_t* w = (int32_t*)&R;
-#pragma unroll
-    for (int k = 0; k < CBEV_RS_WORDS; ++k) w[k] = r.hi[CBEV_HI_RS_R90 + k];
-  } else {  // (phase experiments only) a fixed pose, no record read
-    xmin = ymin = 1000;
-    R = rot_setup(P, 90.0f, rt);
-  }
-  const bool fast = (!RESET && (CBEV_RASTER_PHASES & 16)) ? r.hi[CBEV_HI_RS_FAST] != 0 : raster_fast(P, R);
-  PaintPre pq{};
-  if (!RESET && (CBEV_RASTER_PHASES & 2)) pq = raster_paint_fetch(r);
-  const int xa = (xmin >> 1) & ~3, shift = xmin - 2 * xa;  // packed byte column (dword), texel offset (0..7)
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-
-  // ---- stage the crop window into LDS: 16-byte global loads (lane-linear over
-  // the window's row chunks, all of a batch in flight), then dword LDS stores
-  if (CBEV_RASTER_PHASES & 1) {
-    constexpr int U = 5;  // chunks in flight per thread (one batch covers size 128)
-    const int nch = raster_row_chunks(64 * G, C), total = C * nch;
-    const uint8_t* gbase = K.map + (int64_t)ymin * K.npitch + xa;
-    const int dr = 256 / nch, dj = 256 - dr * nch;
-    int row = threadIdx.x / nch, j = threadIdx.x - row * nch;
-    uint32_t* l32 = (uint32_t*)lds;
-    for (int q0 = 0; q0 < total; q0 += 256 * U) {
-      uint4 v[U];
-      int r = row, c = j;
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        if (q0 + 256 * u + (int)threadIdx.x < total) v[u] = load16_a4(gbase + (int64_t)r * K.npitch + 16 * c);
-        r += dr;
-        c += dj;
-        if (c >= nch) { c -= nch; ++r; }
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        if (q0 + 256 * u + (int)threadIdx.x < total) {
-          if (BYTES) {  // 32 texels -> 8 dwords; the last chunk of a row may overhang the stride
-            uint32_t* d = l32 + row * sd + 8 * j;
-            uint32_t o[8];
-            unpack_texels(v[u].x, o);
-            unpack_texels(v[u].y, o + 2);
-            unpack_texels(v[u].z, o + 4);
-            unpack_texels(v[u].w, o + 6);
-#pragma unroll
-            for (int k = 0; k < 8; ++k)
-              if (8 * j + k < sd) d[k] = o[k];
-          } else {
-            uint32_t* d = l32 + row * sd + 4 * j;
-            d[0] = v[u].x;  // the last chunk of a row may overhang the stride
-            if (4 * j + 1 < sd) d[1] = v[u].y;
-            if (4 * j + 2 < sd) d[2] = v[u].z;
-            if (4 * j + 3 < sd) d[3] = v[u].w;
-          }
-        }
-        row += dr;
-        j += dj;
-        if (j >= nch) { j -= nch; ++row; }
-      }
-    }
-  }
+  RasterJob J;
+  raster_origin<RESET, G>(K, r, J);
+  raster_rot<RESET, G>(K, r, J);
+  J.pq = PaintPre{};
+  if (!RESET && (CBEV_RASTER_PHASES & 2)) J.pq = raster_paint_fetch(r);
+  stage_all<G>(K, J, lds);
   __syncthreads();
-
   if (!RESET) {
     CBEV_STAMP(2, 1);
-    raster_paint<BYTES>(K, r, pq, xmin, ymin, shift, lds);
+    raster_paint<BYTES>(K, r, J.pq, J.xmin, J.ymin, J.shift, lds);
     CBEV_STAMP(2, 2);
   }
-
-  // ---- rotate (pygame transform.rotate / rotate90) + compose + ego overlay
-  const uint32_t bg = lds_texel<BYTES>(lds, shift);  // crop top-left pixel after painting
-  if (NW < 4 && wave >= NW) {
-    side(lane);
-  } else if (CBEV_RASTER_PHASES & 32) {
-    raster_out_dispatch<G, NW>(P, R, fast, lds, shift, bg, out, nout, out_stride, lane, wave, K.fov);
-  }
+  raster_emit<G, NW>(K, J, out, nout, out_stride, lds, side);
 }
 
 // G = size / 64 (64-pixel gathers per output row). CBEV_RASTER_NE envs per
-// workgroup, rendered one after the other through the same LDS image.
+// workgroup (envs g, g + ng, ... of env group g, so env blocks keep their XCD),
+// software-pipelined through one LDS image: the next env's crop loads are
+// issued into registers before this env's output pass and committed to LDS
+// after it, so their L2 latency hides under the frame stores. With 2 envs per
+// workgroup a 4096-env step is one dispatch round of 8 workgroups per CU.
 #ifndef CBEV_RASTER_NE
 #define CBEV_RASTER_NE 1
 #endif
+#ifndef CBEV_RASTER_PREFETCH  // hold the next env's crop loads in registers across the output pass
+#define CBEV_RASTER_PREFETCH 1
+#endif
+#ifndef CBEV_RASTER_WAVES
+#define CBEV_RASTER_WAVES 8
+#endif
 template <int G>
-__global__ __launch_bounds__(256) void k_raster(KArgs K, uint8_t* __restrict__ recs, int n,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CBEV_RASTER_WAVES))) void k_raster(KArgs K, uint8_t* __restrict__ recs, int n,
                                                 uint8_t* __restrict__ frames) {
   extern __shared__ __align__(16) uint8_t lds[];
+  constexpr bool BYTES = raster_bytes(64 * G);
   const int ng = (n + CBEV_RASTER_NE - 1) / CBEV_RASTER_NE;
   const int g = xcd_env_of_wg(blockIdx.x, ng);
   if (g >= ng) return;
   CBEV_STAMP(2, 0);
-#pragma unroll 1
+  const int64_t SS = (int64_t)K.P.size * K.P.size;
+  const bool one_batch = CBEV_RASTER_PREFETCH && stage_total<G>(K.P) <= 256 * STAGE_U;
+  int e = g;
+  DRec r = bind_rec(recs + (int64_t)e * K.L.record_bytes, K.L, K.C);
+  RasterJob J;
+  raster_origin<false, G>(K, r, J);
+  raster_rot<false, G>(K, r, J);
+  J.pq = PaintPre{};
+  if (CBEV_RASTER_PHASES & 2) J.pq = raster_paint_fetch(r);
+  stage_all<G>(K, J, lds);
+  __syncthreads();
+  CBEV_STAMP(2, 1);
+  raster_paint<BYTES>(K, r, J.pq, J.xmin, J.ymin, J.shift, lds);
+  CBEV_STAMP(2, 2);
+#pragma unroll
   for (int k = 0; k < CBEV_RASTER_NE; ++k) {
-    const int e = CBEV_RASTER_NE == 1 ? g : g + k * ng;  // env blocks keep their XCD
-    if (e >= n) break;
-    if (k > 0) __syncthreads();  // the next env's staging overwrites the crop image
-    DRec r = bind_rec(recs + (int64_t)e * K.L.record_bytes, K.L, K.C);
-    raster_env<false, G>(K, r, frames + (int64_t)e * K.P.size * K.P.size, 1, 0, lds);
+    const int en = e + ng;
+    const bool more = CBEV_RASTER_NE > 1 && k + 1 < CBEV_RASTER_NE && en < n;
+    DRec rn;
+    RasterJob Jn;
+    StageBuf b;
+    if (more) {  // the next env's crop loads, in flight across this output pass
+      rn = bind_rec(recs + (int64_t)en * K.L.record_bytes, K.L, K.C);
+      raster_origin<false, G>(K, rn, Jn);
+      if (one_batch && (CBEV_RASTER_PHASES & 1)) stage_issue<G>(K, Jn, 0, b);
+    }
+    raster_emit<G>(K, J, frames + (int64_t)e * SS, 1, 0, lds);
+    if (!more) break;
+    raster_rot<false, G>(K, rn, Jn);
+    Jn.pq = PaintPre{};
+    if (CBEV_RASTER_PHASES & 2) Jn.pq = raster_paint_fetch(rn);
+    __syncthreads();  // every wave is done reading this env's image
+    if (one_batch) {
+      if (CBEV_RASTER_PHASES & 1) stage_commit<G>(K, 0, b, lds);
+    } else {
+      stage_all<G>(K, Jn, lds);
+    }
+    __syncthreads();
+    raster_paint<BYTES>(K, rn, Jn.pq, Jn.xmin, Jn.ymin, Jn.shift, lds);
+    e = en;
+    r = rn;
+    J = Jn;
   }
   CBEV_STAMP(2, 3);
 }
@@ -2746,6 +2856,38 @@ int cbev_profile_read(cbev_ctx* c, double* ms3, int64_t* steps) {
       ms3[k] += ms;
     }
   }
+  return CBEV_OK;
+}
+
+int cbev_profile_raster(cbev_ctx* c, void* records, int n, uint8_t* frames, int reps, void* stream, double* ms) {
+  if (!c || !records || !frames || !ms) return set_err(CBEV_EINVAL, "null argument");
+  if (!c->map_dev) return set_err(CBEV_ESTATE, "cbev_set_map not called");
+  if (c->step_mode != CBEV_STEP_SPLIT) return set_err(CBEV_ESTATE, "the render set-up is written by the split step");
+  if (n <= 0 || reps <= 0) return set_err(CBEV_EINVAL, "n and reps must be positive");
+  HIP_TRY(hipSetDevice(c->device));
+  hipStream_t s = (hipStream_t)stream;
+  const KArgs K = kargs(c);
+  const size_t lb = raster_lds_bytes(c->P);
+  const int rg = (n + CBEV_RASTER_NE - 1) / CBEV_RASTER_NE;
+  hipEvent_t ev[2];
+  HIP_TRY(hipEventCreate(&ev[0]));
+  HIP_TRY(hipEventCreate(&ev[1]));
+  HIP_TRY(hipEventRecord(ev[0], s));
+  for (int i = 0; i < reps; ++i) {
+    switch (c->P.size) {
+      case 64: hipLaunchKernelGGL(k_raster<1>, dim3(rg), dim3(256), lb, s, K, (uint8_t*)records, n, frames); break;
+      case 128: hipLaunchKernelGGL(k_raster<2>, dim3(rg), dim3(256), lb, s, K, (uint8_t*)records, n, frames); break;
+      default: hipLaunchKernelGGL(k_raster<4>, dim3(rg), dim3(256), lb, s, K, (uint8_t*)records, n, frames); break;
+    }
+  }
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipEventRecord(ev[1], s));
+  HIP_TRY(hipEventSynchronize(ev[1]));
+  float t = 0.f;
+  HIP_TRY(hipEventElapsedTime(&t, ev[0], ev[1]));
+  (void)hipEventDestroy(ev[0]);
+  (void)hipEventDestroy(ev[1]);
+  *ms = (double)t / reps;
   return CBEV_OK;
 }
 

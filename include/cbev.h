@@ -157,6 +157,16 @@ int cbev_resize_obs(cbev_ctx* ctx, const uint8_t* frames, int n, const uint8_t* 
 int cbev_profile(cbev_ctx* ctx, int enable);
 int cbev_profile_read(cbev_ctx* ctx, double* ms3, int64_t* steps);
 
+/* Average duration of one k_raster launch over `reps` back-to-back launches on
+ * `stream`, timed with two HIP events around the burst (bench.py's roofline
+ * figure: the per-kernel events of cbev_profile also count each launch's
+ * dispatch gap). It re-renders the observation of the current records, so
+ * call it right after a split-mode cbev_step (which writes the render set-up)
+ * and before any reset: `frames` then receives the bytes that step wrote, less
+ * the checkpoint targets that step's collision pass consumed after its render.
+ * Synchronises; writes the milliseconds per launch to *ms. */
+int cbev_profile_raster(cbev_ctx* ctx, void* records, int n, uint8_t* frames, int reps, void* stream, double* ms);
+
 #ifdef __cplusplus
 }
 #endif

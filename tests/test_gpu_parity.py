@@ -300,3 +300,43 @@ def test_vector_env_surface_and_partial_reset():
     assert len(rgb) == 8 and rgb[0].shape == (128, 128, 3)
     assert saw_term
     env.close()
+
+
+def test_profile_raster_rerenders_the_step():
+    """cbev_profile_raster (bench.py's burst-timed roofline) re-renders the frames
+    the preceding split step wrote, for traffic scenes at both sizes."""
+    for size, kinds in ((128, ["rt_hard_v1"]), (256, ["mix3"])):
+        cfg, P, padded, layout, builder = world(size, "discrete9_v1", "carl_base_v1", 0.5)
+        n = 48
+        recs, _ = build_records(builder, n, kinds, seed0=7)
+        dw = DevWorld(P, padded, CAPS_FULL)
+        L = lib()
+        S = P.size
+        d_recs = torch.from_numpy(recs.copy()).cuda()
+        d_frames = torch.zeros((n, S, S), dtype=torch.uint8, device="cuda")
+        check(L.cbev_reset(dw.ctx, ptr(d_recs), n, None, 0, None, None, 0, ptr(d_frames), 1, None), "reset")
+        acts = action_stream(P, n, 3, seed=5)
+        rew = torch.zeros(n, dtype=torch.float64, device="cuda")
+        term = torch.zeros(n, dtype=torch.uint8, device="cuda")
+        trunc = torch.zeros_like(term)
+        cause = torch.zeros(n, dtype=torch.int32, device="cuda")
+        for t in range(3):
+            a = torch.from_numpy(np.ascontiguousarray(acts[t])).cuda()
+            check(L.cbev_step(dw.ctx, ptr(d_recs), n, ptr(a), ptr(d_frames), ptr(rew), ptr(term), ptr(trunc),
+                              ptr(cause), None, None), "step")
+        torch.cuda.synchronize()
+        want = d_frames.cpu().numpy()
+        again = torch.full_like(d_frames, 0xAA)
+        ms = ctypes.c_double()
+        check(L.cbev_profile_raster(dw.ctx, ptr(d_recs), n, ptr(again), 3, None, ctypes.byref(ms)), "profile_raster")
+        assert ms.value > 0
+        got = again.cpu().numpy()
+        # k_collide consumes the checkpoint targets the ego hit after the step's
+        # render (scene.py:110-140), so only their route pixels may be gone
+        diff = got != want
+        assert np.all(want[diff] == 5), (size, np.unique(want[diff]))  # CBEV_PX_ROUTE
+        assert diff.sum() <= 16 * 16 * n, size
+        assert np.array_equal(got[~diff], want[~diff]), size
+        # the fused step writes no render set-up: refused, not a wrong render
+        check(L.cbev_set_step_mode(dw.ctx, 0), "mode")
+        assert L.cbev_profile_raster(dw.ctx, ptr(d_recs), n, ptr(again), 1, None, ctypes.byref(ms)) != 0
