@@ -1290,7 +1290,7 @@ __device__ __forceinline__ void paint_rect4(uint8_t* lds, int rt, int shift, int
   }
 }
 
-template <bool BYTES>
+template <bool BYTES, int NT = 256>
 __device__ __forceinline__ void raster_paint(const KArgs& K, const DRec& r, const PaintPre& q, int xmin, int ymin,
                                              int shift, uint8_t* __restrict__ lds) {
   const cbev_params& P = K.P;
@@ -1303,7 +1303,7 @@ __device__ __forceinline__ void raster_paint(const KArgs& K, const DRec& r, cons
       if (a1 <= a0) continue;
       const uint32_t col = pass == 0 ? CBEV_PX_VEHICLE : CBEV_PX_PEDESTRIAN;
       if (k >= a0 && k < a1) paint_rect4<BYTES>(lds, rt, shift, C, P.pad, xmin, ymin, q.ax, q.ay, q.asz, tq, col);
-      for (int a = 64 + k; a < a1; a += 64)  // more than 64 actors: fetched here
+      for (int a = NT / 4 + k; a < a1; a += NT / 4)  // more than NT / 4 actors: fetched here
         if (a >= a0)
           paint_rect4<BYTES>(lds, rt, shift, C, P.pad, xmin, ymin, RAD(r, CBEV_AD_X, a), RAD(r, CBEV_AD_Y, a),
                              RAI(r, CBEV_AI_SIZE, a), tq, col);
@@ -1313,7 +1313,7 @@ __device__ __forceinline__ void raster_paint(const KArgs& K, const DRec& r, cons
     // checkpoints 2x2, goal 4x4 (scenes/utils.py:114-122)
     if (k < nt && q.tvis)
       paint_rect4<BYTES>(lds, rt, shift, C, P.pad, xmin, ymin, q.tx, q.ty, k < nt - 1 ? 2 : 4, tq, CBEV_PX_ROUTE);
-    for (int i = 64 + k; i < nt; i += 64)
+    for (int i = NT / 4 + k; i < nt; i += NT / 4)
       if ((r.vis[i >> 5] >> (i & 31)) & 1u)
         paint_rect4<BYTES>(lds, rt, shift, C, P.pad, xmin, ymin, r.cx[i], r.cy[i], i < nt - 1 ? 2 : 4, tq,
                            CBEV_PX_ROUTE);
@@ -1322,7 +1322,7 @@ __device__ __forceinline__ void raster_paint(const KArgs& K, const DRec& r, cons
       const int rx = r.ti[CBEV_TI_RX * r.T + t] - xmin, ry = r.ti[CBEV_TI_RY * r.T + t] - ymin;
       const int rw = r.ti[CBEV_TI_RW * r.T + t], rh = r.ti[CBEV_TI_RH * r.T + t];
       const uint8_t col = (uint8_t)r.ti[CBEV_TI_COLOR * r.T + t];
-      for (int qy = threadIdx.x >> 4; qy < rh; qy += 16)
+      for (int qy = threadIdx.x >> 4; qy < rh; qy += NT / 16)
         for (int qx = threadIdx.x & 15; qx < rw; qx += 16) {
           const int px = rx + qx, py = ry + qy;
           if (px >= 0 && py >= 0 && px < C && py < C) lds_set_texel<BYTES>(lds, py * rt + shift + px, col);
@@ -1386,35 +1386,35 @@ template <int G>
 __device__ __forceinline__ int stage_total(const cbev_params& P) {
   return P.crop * raster_row_chunks(64 * G, P.crop);
 }
-template <int G>
+template <int G, int NT = 256>
 __device__ __forceinline__ void stage_issue(const KArgs& K, const RasterJob& J, int q0, StageBuf& b) {
   const int C = K.P.crop;
   const int nch = raster_row_chunks(64 * G, C), total = C * nch;
   const uint8_t* gbase = K.map + (int64_t)J.ymin * K.npitch + J.xa;
-  const int dr = 256 / nch, dj = 256 - dr * nch;
+  const int dr = NT / nch, dj = NT - dr * nch;
   const int q = q0 + (int)threadIdx.x;
   int r = q / nch, c = q - r * nch;
 #pragma unroll
   for (int u = 0; u < STAGE_U; ++u) {
-    if (q + 256 * u < total) b.v[u] = load16_a4(gbase + (int64_t)r * K.npitch + 16 * c);
+    if (q + NT * u < total) b.v[u] = load16_a4(gbase + (int64_t)r * K.npitch + 16 * c);
     r += dr;
     c += dj;
     if (c >= nch) { c -= nch; ++r; }
   }
 }
-template <int G>
+template <int G, int NT = 256>
 __device__ __forceinline__ void stage_commit(const KArgs& K, int q0, const StageBuf& b, uint8_t* __restrict__ lds) {
   constexpr bool BYTES = raster_bytes(64 * G);
   const int C = K.P.crop;
   const int sd = raster_stride_dwords(64 * G, C);
   const int nch = raster_row_chunks(64 * G, C), total = C * nch;
-  const int dr = 256 / nch, dj = 256 - dr * nch;
+  const int dr = NT / nch, dj = NT - dr * nch;
   const int q = q0 + (int)threadIdx.x;
   int row = q / nch, j = q - row * nch;
   uint32_t* l32 = (uint32_t*)lds;
 #pragma unroll
   for (int u = 0; u < STAGE_U; ++u) {
-    if (q + 256 * u < total) {
+    if (q + NT * u < total) {
       if (BYTES) {  // 32 texels -> 8 dwords; the last chunk of a row may overhang the stride
         uint32_t* d = l32 + row * sd + 8 * j;
         uint32_t o[8];
@@ -1438,22 +1438,22 @@ __device__ __forceinline__ void stage_commit(const KArgs& K, int q0, const Stage
     if (j >= nch) { j -= nch; ++row; }
   }
 }
-template <int G>
+template <int G, int NT = 256>
 __device__ __forceinline__ void stage_all(const KArgs& K, const RasterJob& J, uint8_t* __restrict__ lds) {
   if (CBEV_RASTER_PHASES & 1) {
     const int total = stage_total<G>(K.P);
-    for (int q0 = 0; q0 < total; q0 += 256 * STAGE_U) {
+    for (int q0 = 0; q0 < total; q0 += NT * STAGE_U) {
       StageBuf b;
-      stage_issue<G>(K, J, q0, b);
-      stage_commit<G>(K, q0, b, lds);
+      stage_issue<G, NT>(K, J, q0, b);
+      stage_commit<G, NT>(K, q0, b, lds);
     }
   }
 }
 
-// NW < 4: waves NW..3 run `side(lane)` (k_step: the collision / reward pass)
-// while waves 0..NW-1 write the frame; every other LDS access of `side` must
-// stay outside the crop image.
-template <int G, int NW = 4, class Side = NoSideWork>
+// NW < NT / 64: waves NW.. run `side(lane)` (k_step: the collision / reward
+// pass) while waves 0..NW-1 write the frame; every other LDS access of `side`
+// must stay outside the crop image.
+template <int G, int NW = 4, class Side = NoSideWork, int NT = 256>
 __device__ __forceinline__ void raster_emit(const KArgs& K, const RasterJob& J, uint8_t* __restrict__ out, int nout,
                                             int64_t out_stride, const uint8_t* __restrict__ lds,
                                             const Side& side = Side()) {
@@ -1462,7 +1462,7 @@ __device__ __forceinline__ void raster_emit(const KArgs& K, const RasterJob& J, 
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   // ---- rotate (pygame transform.rotate / rotate90) + compose + ego overlay
   const uint32_t bg = lds_texel<BYTES>(lds, J.shift);  // crop top-left pixel after painting
-  if (NW < 4 && wave >= NW) {
+  if (NW < NT / 64 && wave >= NW) {
     side(lane);
   } else if (CBEV_RASTER_PHASES & 32) {
     raster_out_dispatch<G, NW>(K.P, J.R, J.fast, lds, J.shift, bg, out, nout, out_stride, lane, wave, K.fov);
@@ -1506,17 +1506,26 @@ __device__ __forceinline__ void raster_env(const KArgs& K, const DRec& r, uint8_
 #ifndef CBEV_RASTER_WAVES
 #define CBEV_RASTER_WAVES 8
 #endif
+// Threads per k_raster workgroup: 8 waves at S=256, where the 68 KB crop image
+// leaves 2 workgroups per CU (4 waves each would leave the SIMDs half empty);
+// 4 waves below, where 8 workgroups share a CU.
+#ifndef CBEV_RASTER_NT256
+#define CBEV_RASTER_NT256 512
+#endif
+__host__ __device__ constexpr int raster_threads(int S) { return S >= 256 ? CBEV_RASTER_NT256 : 256; }
+
 template <int G>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CBEV_RASTER_WAVES))) void k_raster(KArgs K, uint8_t* __restrict__ recs, int n,
-                                                uint8_t* __restrict__ frames) {
+__global__ __launch_bounds__(raster_threads(64 * G)) __attribute__((amdgpu_waves_per_eu(CBEV_RASTER_WAVES))) void k_raster(
+    KArgs K, uint8_t* __restrict__ recs, int n, uint8_t* __restrict__ frames) {
   extern __shared__ __align__(16) uint8_t lds[];
   constexpr bool BYTES = raster_bytes(64 * G);
+  constexpr int NT = raster_threads(64 * G), NW = NT / 64;
   const int ng = (n + CBEV_RASTER_NE - 1) / CBEV_RASTER_NE;
   const int g = xcd_env_of_wg(blockIdx.x, ng);
   if (g >= ng) return;
   CBEV_STAMP(2, 0);
   const int64_t SS = (int64_t)K.P.size * K.P.size;
-  const bool one_batch = CBEV_RASTER_PREFETCH && stage_total<G>(K.P) <= 256 * STAGE_U;
+  const bool one_batch = CBEV_RASTER_PREFETCH && stage_total<G>(K.P) <= NT * STAGE_U;
   int e = g;
   DRec r = bind_rec(recs + (int64_t)e * K.L.record_bytes, K.L, K.C);
   RasterJob J;
@@ -1524,10 +1533,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CBEV_RASTER
   raster_rot<false, G>(K, r, J);
   J.pq = PaintPre{};
   if (CBEV_RASTER_PHASES & 2) J.pq = raster_paint_fetch(r);
-  stage_all<G>(K, J, lds);
+  stage_all<G, NT>(K, J, lds);
   __syncthreads();
   CBEV_STAMP(2, 1);
-  raster_paint<BYTES>(K, r, J.pq, J.xmin, J.ymin, J.shift, lds);
+  raster_paint<BYTES, NT>(K, r, J.pq, J.xmin, J.ymin, J.shift, lds);
   CBEV_STAMP(2, 2);
 #pragma unroll
   for (int k = 0; k < CBEV_RASTER_NE; ++k) {
@@ -1539,21 +1548,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CBEV_RASTER
     if (more) {  // the next env's crop loads, in flight across this output pass
       rn = bind_rec(recs + (int64_t)en * K.L.record_bytes, K.L, K.C);
       raster_origin<false, G>(K, rn, Jn);
-      if (one_batch && (CBEV_RASTER_PHASES & 1)) stage_issue<G>(K, Jn, 0, b);
+      if (one_batch && (CBEV_RASTER_PHASES & 1)) stage_issue<G, NT>(K, Jn, 0, b);
     }
-    raster_emit<G>(K, J, frames + (int64_t)e * SS, 1, 0, lds);
+    raster_emit<G, NW, NoSideWork, NT>(K, J, frames + (int64_t)e * SS, 1, 0, lds);
     if (!more) break;
     raster_rot<false, G>(K, rn, Jn);
     Jn.pq = PaintPre{};
     if (CBEV_RASTER_PHASES & 2) Jn.pq = raster_paint_fetch(rn);
     __syncthreads();  // every wave is done reading this env's image
     if (one_batch) {
-      if (CBEV_RASTER_PHASES & 1) stage_commit<G>(K, 0, b, lds);
+      if (CBEV_RASTER_PHASES & 1) stage_commit<G, NT>(K, 0, b, lds);
     } else {
-      stage_all<G>(K, Jn, lds);
+      stage_all<G, NT>(K, Jn, lds);
     }
     __syncthreads();
-    raster_paint<BYTES>(K, rn, Jn.pq, Jn.xmin, Jn.ymin, Jn.shift, lds);
+    raster_paint<BYTES, NT>(K, rn, Jn.pq, Jn.xmin, Jn.ymin, Jn.shift, lds);
     e = en;
     r = rn;
     J = Jn;
@@ -3023,9 +3032,9 @@ int cbev_profile_raster(cbev_ctx* c, void* records, int n, uint8_t* frames, int 
   HIP_TRY(hipEventRecord(ev[0], s));
   for (int i = 0; i < reps; ++i) {
     switch (c->P.size) {
-      case 64: hipLaunchKernelGGL(k_raster<1>, dim3(rg), dim3(256), lb, s, K, (uint8_t*)records, n, frames); break;
-      case 128: hipLaunchKernelGGL(k_raster<2>, dim3(rg), dim3(256), lb, s, K, (uint8_t*)records, n, frames); break;
-      default: hipLaunchKernelGGL(k_raster<4>, dim3(rg), dim3(256), lb, s, K, (uint8_t*)records, n, frames); break;
+      case 64: hipLaunchKernelGGL(k_raster<1>, dim3(rg), dim3(raster_threads(64)), lb, s, K, (uint8_t*)records, n, frames); break;
+      case 128: hipLaunchKernelGGL(k_raster<2>, dim3(rg), dim3(raster_threads(128)), lb, s, K, (uint8_t*)records, n, frames); break;
+      default: hipLaunchKernelGGL(k_raster<4>, dim3(rg), dim3(raster_threads(256)), lb, s, K, (uint8_t*)records, n, frames); break;
     }
   }
   HIP_TRY(hipGetLastError());
@@ -3120,9 +3129,9 @@ int cbev_step(cbev_ctx* c, void* records, int n, const void* actions, uint8_t* f
     const size_t lb = raster_lds_bytes(c->P);
     const int rg = (n + CBEV_RASTER_NE - 1) / CBEV_RASTER_NE;
     switch (c->P.size) {
-      case 64: hipLaunchKernelGGL(k_raster<1>, dim3(rg), dim3(256), lb, s, K, (uint8_t*)records, n, frames); break;
-      case 128: hipLaunchKernelGGL(k_raster<2>, dim3(rg), dim3(256), lb, s, K, (uint8_t*)records, n, frames); break;
-      default: hipLaunchKernelGGL(k_raster<4>, dim3(rg), dim3(256), lb, s, K, (uint8_t*)records, n, frames); break;
+      case 64: hipLaunchKernelGGL(k_raster<1>, dim3(rg), dim3(raster_threads(64)), lb, s, K, (uint8_t*)records, n, frames); break;
+      case 128: hipLaunchKernelGGL(k_raster<2>, dim3(rg), dim3(raster_threads(128)), lb, s, K, (uint8_t*)records, n, frames); break;
+      default: hipLaunchKernelGGL(k_raster<4>, dim3(rg), dim3(raster_threads(256)), lb, s, K, (uint8_t*)records, n, frames); break;
     }
   }
   if (ev) HIP_TRY(hipEventRecord(ev[2], s));
