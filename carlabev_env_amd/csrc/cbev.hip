@@ -1631,7 +1631,17 @@ __global__ __launch_bounds__(256) void k_bank_frames(KArgs K, const uint8_t* __r
 
 // Partial reset from a bank with cached reset frames: records[e] <- bank[b] and
 // bank_frames[b] into every frame-stack slot of env e, for the envs selected by
-// mask. Pure copies (16-byte), strided over a RESET_WGS grid like k_reset.
+// mask. Pure 16-byte copies, split into 4 KB pieces (one per 256-thread pass):
+// RESET_PIECE_F frame pieces (each written to every ring slot) and
+// RESET_PIECE_R record pieces per env. The pieces of the selected envs are
+// dealt round-robin over the workgroups of the env's XCD (env block e / 64 ->
+// XCD (e / 64) % 8, as in the step kernels; workgroup w runs on XCD w % 8), so a
+// reset's copies spread over many CUs instead of one workgroup per env: every
+// workgroup ballots the masks of its XCD's env blocks and counts the selected
+// envs' pieces in env order, taking every WPX-th.
+__host__ __device__ __forceinline__ int reset_pieces_frame(int64_t SS) { return (int)((SS + 4095) / 4096); }
+__host__ __device__ __forceinline__ int reset_pieces_rec(int64_t rb) { return (int)((rb + 4095) / 4096); }
+
 __global__ __launch_bounds__(256) void k_reset_copy(KArgs K, uint8_t* __restrict__ recs, int n,
                                                     const uint8_t* __restrict__ bank, int n_bank,
                                                     const uint8_t* __restrict__ mask,
@@ -1641,24 +1651,43 @@ __global__ __launch_bounds__(256) void k_reset_copy(KArgs K, uint8_t* __restrict
   const int64_t rb = K.L.record_bytes;
   const int64_t SS = (int64_t)K.P.size * K.P.size;
   const int lane = threadIdx.x & 63;
-  for (int p0 = blockIdx.x; p0 < n; p0 += 64 * gridDim.x) {
-    const int pl = p0 + lane * gridDim.x;
-    const bool sel = pl < n && (mask == nullptr || mask[xcd_env_of_wg(pl, n)] != 0);
-    uint64_t todo = __ballot(sel);
+  const int pf = reset_pieces_frame(SS), ppe = pf + reset_pieces_rec(rb);
+  const int myx = blockIdx.x & 7, wpx = gridDim.x >> 3, wk = blockIdx.x >> 3;  // gridDim.x % 8 == 0
+  int t = 0;  // pieces of this XCD's selected envs counted so far (uniform)
+  for (int base0 = 64 * myx; base0 < n; base0 += 8 * 512) {  // this XCD's env blocks, 8 mask loads in flight
+    bool sel[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int p = base0 + 512 * k + lane;
+      sel[k] = p < n && (mask == nullptr || mask[p] != 0);
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+    const int base = base0 + 512 * k;
+    uint64_t todo = __ballot(sel[k]);
     while (todo) {
-      const int k = __builtin_ctzll(todo);
+      const int e = base + __builtin_ctzll(todo);
       todo &= todo - 1;
-      const int e = xcd_env_of_wg(p0 + k * gridDim.x, n);
+      // this workgroup's pieces of env e: c = first, first + wpx, ...
+      int first = wk - t % wpx;
+      if (first < 0) first += wpx;
+      t += ppe;
+      if (first >= ppe) continue;
       int b = bank_idx ? bank_idx[e] : (int)(((int64_t)e + bank_offset) % n_bank);
       b = b < 0 ? 0 : (b >= n_bank ? n_bank - 1 : b);
-      const uint4* s4 = (const uint4*)(bank + (int64_t)b * rb);
-      uint4* d4 = (uint4*)(recs + (int64_t)e * rb);
-      for (int64_t i = threadIdx.x; i < rb / 16; i += 256) d4[i] = s4[i];
-      const uint4* f4 = (const uint4*)(bank_frames + (int64_t)b * SS);
-      for (int64_t i = threadIdx.x; i < SS / 16; i += 256) {
-        const uint4 v = f4[i];
-        for (int f = 0; f < n_frames; ++f) ((uint4*)(ring + ((int64_t)f * n + e) * SS))[i] = v;
+      for (int c = first; c < ppe; c += wpx) {
+        if (c < pf) {
+          const int64_t i = (int64_t)c * 256 + threadIdx.x;  // uint4 index in the frame
+          if (i < SS / 16) {
+            const uint4 v = ((const uint4*)(bank_frames + (int64_t)b * SS))[i];
+            for (int f = 0; f < n_frames; ++f) ((uint4*)(ring + ((int64_t)f * n + e) * SS))[i] = v;
+          }
+        } else {
+          const int64_t i = (int64_t)(c - pf) * 256 + threadIdx.x;  // uint4 index in the record
+          if (i < rb / 16) ((uint4*)(recs + (int64_t)e * rb))[i] = ((const uint4*)(bank + (int64_t)b * rb))[i];
+        }
       }
+    }
     }
   }
 }
@@ -3192,7 +3221,10 @@ int cbev_reset_frames(cbev_ctx* c, void* records, int n, const void* bank, int n
   if (n_frames < 1) return set_err(CBEV_EINVAL, "n_frames < 1");
   if (n <= 0) return CBEV_OK;
   KArgs K = kargs(c);
-  const int grid = n < RESET_WGS ? n : RESET_WGS;
+  // 8 .. RESET_WGS workgroups, a multiple of 8 (k_reset_copy's per-XCD dealing)
+  const int64_t pieces = (int64_t)n * (reset_pieces_frame((int64_t)c->P.size * c->P.size) +
+                                       reset_pieces_rec(c->L.record_bytes));
+  const int grid = pieces >= RESET_WGS ? RESET_WGS : (int)((pieces + 7) & ~7);
   hipLaunchKernelGGL(k_reset_copy, dim3(grid), dim3(256), 0, (hipStream_t)stream, K, (uint8_t*)records, n,
                      (const uint8_t*)bank, n_bank, mask, bank_idx, bank_offset, bank_frames, frames, n_frames);
   HIP_TRY(hipGetLastError());
