@@ -198,15 +198,190 @@ __device__ __noinline__ void d_start_retreat(DRec& r, int a) {
   d_bset(r, a, CBEV_BST_RETREATING, RAD(r, CBEV_AD_CRUISE_MPS, a));
 }
 
-// Behaviour.apply (lead_brake.py:10-15, jaywalk.py:56-138)
-__device__ void d_behavior(DRec& r, int a, double t) {
+// j-th (0-based) set bit of m (m has more than j set bits)
+__device__ __forceinline__ int nth_set_bit(uint64_t m, int j) {
+  int p = 0;
+#pragma unroll
+  for (int w = 32; w > 0; w >>= 1) {
+    const int c = __popcll((m >> p) & ((1ull << w) - 1));
+    if (c <= j) {
+      j -= c;
+      p += w;
+    }
+  }
+  return p;
+}
+
+// d_start_retreat by the whole wave for actor a when its route fits the lanes
+// (RA <= 64: lane i holds route point i). Every per-point expression of
+// d_smooth_route is evaluated as there, one point per lane; the two serial sums
+// (arc lengths, np.unwrap corrections) are accumulated in index order through
+// shuffles and the target search reduces the same candidates, so the result is
+// the serial one bit for bit. Retreats are rare but each serial rebuild costs a
+// lane ~50 k cycles, which the whole k_actors launch then waits for.
+__device__ __noinline__ void wave_start_retreat(DRec& r, int a, int lane) {
+  __threadfence();  // the owner lane's behaviour stores come first
+  const int RA = r.RA;
+  const int nrx = RAI(r, CBEV_AI_NRX, a);
+  int cur = RAI(r, CBEV_AI_TIDX, a);
+  if (cur > nrx - 1) cur = nrx - 1;
+  if (cur < 0) cur = 0;
+  int n = cur + 2;
+  if (n > RA) n = RA;
+  const double* ix = r.aix + (int64_t)a * RA;
+  const double* iy = r.aiy + (int64_t)a * RA;
+  // raw route [pos] + initial_route[:cur + 1][::-1] (jaywalk.py:43-54)
+  double px = RAD(r, CBEV_AD_X, a), py = RAD(r, CBEV_AD_Y, a);
+  if (lane >= 1 && lane < n) {
+    px = ix[cur - (lane - 1)];
+    py = iy[cur - (lane - 1)];
+  }
+  // ---- smooth_and_compute (control/utils.py:200-269)
+  // consecutive duplicates (vs the raw predecessor) dropped
+  const double ppx = __shfl(px, lane > 0 ? lane - 1 : 0), ppy = __shfl(py, lane > 0 ? lane - 1 : 0);
+  const bool keep = lane < n && (lane == 0 || hypot(px - ppx, py - ppy) > 1e-9);
+  const uint64_t km = __ballot(keep);
+  int nd = __popcll(km);
+  const int src = lane < nd ? nth_set_bit(km, lane) : 0;
+  double qx = __shfl(px, src), qy = __shfl(py, src);  // deduplicated point `lane`
+  if (nd < 2) {
+    const double x0 = __shfl(qx, 0), y0 = __shfl(qy, 0);
+    qx = lane == 1 ? x0 + 1e-3 : x0;
+    qy = y0;
+    nd = 2;
+  }
+  int w = 11;
+  if (w > nd) w = (nd % 2 == 1) ? nd : nd - 1;
+  if (w < 3) w = 3;
+  const int h = w / 2, ti = w / 2;
+  double cxv = qx, cyv = qy;
+  if (nd >= w) {  // Savitzky-Golay (mode='interp'): y first, then x, as the serial pass
+    const int i = lane;
+    double accy = 0.0, accx = 0.0;
+    for (int j = 0; j < w; ++j) {
+      int idx;
+      double c;
+      if (i < h) {
+        idx = j;
+        c = c_sg.left[ti][i][j];
+      } else if (i >= nd - h) {
+        idx = nd - w + j;
+        c = c_sg.right[ti][i >= nd ? 0 : i - (nd - h)][j];
+      } else {
+        idx = i - h + j;
+        c = c_sg.conv[ti][j];
+      }
+      const double vy = __shfl(qy, idx & 63), vx = __shfl(qx, idx & 63);
+      accy += c * vy;
+      accx += c * vx;
+    }
+    cxv = accx;
+    cyv = accy;
+  }
+  // arc length: segment lengths in parallel, their running sum in index order
+  const double pcx = __shfl(cxv, lane > 0 ? lane - 1 : 0), pcy = __shfl(cyv, lane > 0 ? lane - 1 : 0);
+  const double seg = lane > 0 ? hypot(cxv - pcx, cyv - pcy) : 0.0;
+  double total = 0.0, sv = 0.0;
+  for (int k = 1; k < nd; ++k) {
+    total += __shfl(seg, k);
+    if (lane == k) sv = total;
+  }
+  double yawv = 0.0;
+  if (total > 1e-9) {
+    const double s_prev = __shfl(sv, lane > 0 ? lane - 1 : 0), s_next = __shfl(sv, lane + 1 < 64 ? lane + 1 : 63);
+    const double ncx = __shfl(cxv, lane + 1 < 64 ? lane + 1 : 63), ncy = __shfl(cyv, lane + 1 < 64 ? lane + 1 : 63);
+    double gx, gy;
+    if (lane == 0) {
+      gx = (ncx - cxv) / (s_next - sv);
+      gy = (ncy - cyv) / (s_next - sv);
+    } else if (lane == nd - 1) {
+      gx = (cxv - pcx) / (sv - s_prev);
+      gy = (cyv - pcy) / (sv - s_prev);
+    } else {
+      const double dx1 = sv - s_prev, dx2 = s_next - sv;
+      const double ca = -(dx2) / (dx1 * (dx1 + dx2));
+      const double cb = (dx2 - dx1) / (dx1 * dx2);
+      const double cc = dx1 / (dx2 * (dx1 + dx2));
+      gx = ca * pcx + cb * cxv + cc * ncx;
+      gy = ca * pcy + cb * cyv + cc * ncy;
+    }
+    const double raw = lane < nd ? atan2(gy, gx) : 0.0;
+    const double praw = __shfl(raw, lane > 0 ? lane - 1 : 0);
+    double corr = 0.0;
+    if (lane > 0) {  // np.unwrap
+      const double dd = raw - praw;
+      double ddmod = d_remainder(dd + CB_PI, 2.0 * CB_PI) - CB_PI;
+      if (ddmod == -CB_PI && dd > 0) ddmod = CB_PI;
+      corr = ddmod - dd;
+      if (fabs(dd) < CB_PI) corr = 0.0;
+    }
+    double acc = 0.0, av = 0.0;
+    for (int k = 1; k < nd; ++k) {
+      acc += __shfl(corr, k);
+      if (lane == k) av = acc;
+    }
+    yawv = raw + av;
+  }
+  double* ax = r.arx + (int64_t)a * RA;
+  double* ay = r.ary + (int64_t)a * RA;
+  double* cx = r.acx + (int64_t)a * RA;
+  double* cy = r.acy + (int64_t)a * RA;
+  double* cyaw = r.acyaw + (int64_t)a * RA;
+  const double gx0 = ix[0], gy0 = iy[0];
+  if (lane < n) {
+    ax[lane] = px;
+    ay[lane] = py;
+  }
+  if (lane < nd) {
+    cx[lane] = cxv;
+    cy[lane] = cyv;
+    cyaw[lane] = yawv;
+  }
+  // ---- Actor.set_route_surface / Controller.set_route(jitter_start=False): pose at the
+  // smoothed start, target index from there (calc_target_index), heading cyaw[idx]
+  const int m = nd;
+  const double x0 = __shfl(cxv, 0), y0 = __shfl(cyv, 0);
+  const double yaw_old = RAD(r, CBEV_AD_YAW, a);
+  const double fx = x0 + CB_WHEELBASE * cos(yaw_old), fy = y0 + CB_WHEELBASE * sin(yaw_old);
+  const double dxl = fx - cxv, dyl = fy - cyv;
+  const double d2 = lane < m ? dxl * dxl + dyl * dyl : INFINITY;
+  const double lim = group_min<64>(d2) * (1.0 + 1e-14);
+  double bd = INFINITY;
+  int bi = 0x7fffffff;
+  if (lane < m && d2 <= lim) {
+    bd = hypot(dxl, dyl);
+    bi = lane;
+  }
+  group_argmin<64>(bd, bi);
+  const int tidx = bi == 0x7fffffff ? 0 : bi;
+  const double yaw_new = __shfl(yawv, tidx);
+  if (lane == 0) {
+    RAD(r, CBEV_AD_GOAL_X, a) = gx0;
+    RAD(r, CBEV_AD_GOAL_Y, a) = gy0;
+    RAI(r, CBEV_AI_HAS_GOAL, a) = 1;
+    RAI(r, CBEV_AI_NRX, a) = n;
+    RAI(r, CBEV_AI_NROUTE, a) = m;
+    RAD(r, CBEV_AD_X, a) = x0;
+    RAD(r, CBEV_AD_Y, a) = y0;
+    RAI(r, CBEV_AI_TIDX, a) = tidx;
+    RAD(r, CBEV_AD_YAW, a) = yaw_new;
+    d_bset(r, a, CBEV_BST_RETREATING, RAD(r, CBEV_AD_CRUISE_MPS, a));
+  }
+  __threadfence();  // the other lanes read these record fields next
+}
+
+// Behaviour.apply (lead_brake.py:10-15, jaywalk.py:56-138). DEFER: a due
+// retreat (the last action of its branch) is returned instead of run, for the
+// caller to rebuild the route with the whole wave (wave_start_retreat).
+template <bool DEFER = false>
+__device__ bool d_behavior(DRec& r, int a, double t) {
   const int beh = RAI(r, CBEV_AI_BEH, a);
-  if (beh == CBEV_BEH_NONE) return;
+  if (beh == CBEV_BEH_NONE) return false;
   if (beh == CBEV_BEH_LEAD_BRAKE) {
     if (t >= RAD(r, CBEV_AD_P0, a)) RAI(r, CBEV_AI_BRAKING, a) = 1;
     if (RAI(r, CBEV_AI_BRAKING, a))
       d_set_target_speed_mps(r, a, RAD(r, CBEV_AD_T_SPEED_MPS, a) - RAD(r, CBEV_AD_P1, a) * CB_DT);
-    return;
+    return false;
   }
   RAD(r, CBEV_AD_ELAPSED, a) += CB_DT;
   RAD(r, CBEV_AD_STATE_ELAPSED, a) += CB_DT;
@@ -225,7 +400,7 @@ __device__ void d_behavior(DRec& r, int a, double t) {
     } else if (st == CBEV_BST_CLEARED) {
       d_set_target_speed_mps(r, a, 0.0);
     }
-    return;
+    return false;
   }
   const double trigger = (beh == CBEV_BEH_STOP_MID) ? 0.5 : 1.0 / 3.0;
   const bool retreat = (beh == CBEV_BEH_YIELD_RETURN);
@@ -244,7 +419,10 @@ __device__ void d_behavior(DRec& r, int a, double t) {
     }
   } else if (st == CBEV_BST_YIELDING) {
     d_set_target_speed_mps(r, a, 0.0);
-    if (retreat && RAD(r, CBEV_AD_STATE_ELAPSED, a) >= RAD(r, CBEV_AD_P1, a)) d_start_retreat(r, a);
+    if (retreat && RAD(r, CBEV_AD_STATE_ELAPSED, a) >= RAD(r, CBEV_AD_P1, a)) {
+      if (DEFER) return true;
+      d_start_retreat(r, a);
+    }
   } else if (st == CBEV_BST_CROSSING) {
     d_set_target_speed_mps(r, a, cruise);
     if (done) d_bset(r, a, CBEV_BST_CLEARED, 0.0);
@@ -262,6 +440,7 @@ __device__ void d_behavior(DRec& r, int a, double t) {
   } else if (st == CBEV_BST_CLEARED || st == CBEV_BST_RETREATED) {
     d_set_target_speed_mps(r, a, 0.0);
   }
+  return false;
 }
 
 // Actor.step (actor.py:110-119) + Controller.control_step (stanley_controller.py:51-62)
@@ -477,8 +656,21 @@ __device__ unsigned g_hwid[CBEV_NSTAMP][4096];                   // HW_ID (SE / 
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(xcc_));          \
     g_hwid[kern][blockIdx.x] = xcc_;                                            \
   }
+// per wave (lane 0; entry 4 * workgroup + wave): kernels with a wave per env
+#define CBEV_STAMPW(kern, slot)                                                                  \
+  if ((threadIdx.x & 63) == 0 && 4 * blockIdx.x + (threadIdx.x >> 6) < 4096) {                  \
+    const int w_ = 4 * blockIdx.x + (threadIdx.x >> 6);                                          \
+    g_stamps[kern][w_][slot] = __builtin_amdgcn_s_memtime();                                     \
+    g_rtstamps[kern][w_][slot] = __builtin_amdgcn_s_memrealtime();                               \
+    unsigned xcc_;                                                                               \
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc_));                          \
+    g_xcc[kern][w_] = xcc_;                                                                      \
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(xcc_));                           \
+    g_hwid[kern][w_] = xcc_;                                                                     \
+  }
 #else
 #define CBEV_STAMP(kern, slot)
+#define CBEV_STAMPW(kern, slot)
 #endif
 
 // ---- record staging for the thread-per-env kernels. A workgroup owns `ne`
@@ -871,15 +1063,29 @@ __global__ __launch_bounds__(256, CBEV_ACTORS_WAVES) void k_actors(KArgs K, uint
     return;
   }
   const int RA = r.RA;
-  CBEV_STAMP(6, 0);
+  CBEV_STAMPW(6, 0);
   // ---- 1
   const int a = lane;
   bool live = false;
   int nrt = 0, tid0 = 0;
   double s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   double fx = 0.0, fy = 0.0, ts = 0.0;
+  // behaviours; a due retreat rebuilds the actor's route with the whole wave
+  const bool retreat = a < nact && d_behavior<true>(r, a, t);
+  uint64_t rm = __ballot(retreat);
+  if (rm) {
+    if (RA <= 64) {
+      while (rm) {
+        const int k = __builtin_ctzll(rm);
+        rm &= rm - 1;
+        wave_start_retreat(r, k, lane);
+      }
+    } else if (retreat) {
+      d_start_retreat(r, a);
+      __threadfence();
+    }
+  }
   if (a < nact) {
-    d_behavior(r, a, t);
     ts = RAD(r, CBEV_AD_T_SPEED, a);
     RAD(r, CBEV_AD_CT_SPEED, a) = ts;
     nrt = RAI(r, CBEV_AI_NROUTE, a);
@@ -896,7 +1102,7 @@ __global__ __launch_bounds__(256, CBEV_ACTORS_WAVES) void k_actors(KArgs K, uint
       fy = s[1] + CB_WHEELBASE * sin(s[2]);
     }
   }
-  CBEV_STAMP(6, 1);
+  CBEV_STAMPW(6, 1);
   // ---- 2
   const uint64_t livem = __ballot(live);
   // lanes per actor: the widest group that still takes every actor in one round
@@ -911,7 +1117,7 @@ __global__ __launch_bounds__(256, CBEV_ACTORS_WAVES) void k_actors(KArgs K, uint
     case 2: best = actor_search<2>(r, nact, livem, fx, fy, nrt, lane); break;
     default: best = actor_search<1>(r, nact, livem, fx, fy, nrt, lane); break;
   }
-  CBEV_STAMP(6, 2);
+  CBEV_STAMPW(6, 2);
   // ---- 3: stanley_control (stanley_controller.py:64-89), pid_control, State.update
   if (live) {
     const double* cx = r.acx + (int64_t)a * RA;
@@ -934,7 +1140,7 @@ __global__ __launch_bounds__(256, CBEV_ACTORS_WAVES) void k_actors(KArgs K, uint
     RAD(r, CBEV_AD_V, a) = s[3];
     RAD(r, CBEV_AD_TIME, a) += CB_DT;
   }
-  CBEV_STAMP(6, 3);
+  CBEV_STAMPW(6, 3);
 }
 
 

@@ -19,6 +19,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--config", type=int, default=2)
 ap.add_argument("--steps", type=int, default=10)
 ap.add_argument("--defs", default="")
+ap.add_argument("--reset", action="store_true", help="canonical loop: reset the terminated envs from the bank each step")
 a = ap.parse_args()
 so = os.path.join(REPO, "gpurun_out", "libcbev_timing.so")
 os.makedirs(os.path.dirname(so), exist_ok=True)
@@ -41,8 +42,11 @@ L.cbev_debug_times.argtypes = [ctypes.c_void_p]
 L.cbev_debug_occupancy.argtypes = [ctypes.c_int, ctypes.c_int]
 for b in (19656, 20480, 20481):
     print(f"raster occupancy API (size {cfgd['size']}, {b} B LDS): {L.cbev_debug_occupancy(cfgd['size'], b)} WGs/CU")
+env.auto_obs = False
 for t in range(a.steps):
     env.step_async_only(acts[t])
+    if a.reset:
+        env.reset_from_bank(mask=env.term)
 torch.cuda.synchronize()
 NS = 7
 buf = np.zeros(2 * NS * 4096 * 4 + NS * 4096, np.uint64)
@@ -51,7 +55,7 @@ xcc = buf[2 * NS * 4096 * 4:].reshape(NS, 4096).astype(np.int64)
 hwid = xcc >> 32
 xcc = xcc & 0xFFFFFFFF
 buf = buf[:2 * NS * 4096 * 4].reshape(2, NS, 4096, 4)
-for k, name in enumerate(("k_hero", "k_collide", "k_raster", "k_hero after P1 / P2 / A / B (slots 0-3)", "collide_env(thread0)", "k_collide pre-pass: segs/targets/actors+sync", "k_actors: behaviour / search / stanley+update (wave 0 of each WG)")):
+for k, name in enumerate(("k_hero", "k_collide", "k_raster", "k_hero after P1 / P2 / A / B (slots 0-3)", "collide_env(thread0)", "k_collide pre-pass: segs/targets/actors+sync", "k_actors: behaviour / search / stanley+update (per wave)")):
     if not (buf[0, k, :, 0] > 0).any():
         continue
     st = buf[0, k].astype(np.int64)
@@ -62,7 +66,7 @@ for k, name in enumerate(("k_hero", "k_collide", "k_raster", "k_hero after P1 / 
           f"WG mean {(rt[:, 3] - rt[:, 0]).mean() / 100:.2f} us, first start->last start "
           f"{(rt[:, 0].max() - rt[:, 0].min()) / 100:.2f} us; clock {((st[:, 3] - st[:, 0]).sum() / max((rt[:, 3] - rt[:, 0]).sum(), 1)) / 100:.2f} GHz")
     d = np.diff(st, axis=1)
-    print(f"{name}: {used.sum()} WGs; cycles mean phase1 {d[:, 0].mean():.0f}  phase2 {d[:, 1].mean():.0f} "
+    print(f"{name}: {used.sum()} WGs; cycles mean phase1 {d[:, 0].mean():.0f} (max {d[:, 0].max():.0f})  phase2 {d[:, 1].mean():.0f} "
           f"(max {d[:, 1].max():.0f})  phase3 {d[:, 2].mean():.0f}; WG total mean {(st[:, 3] - st[:, 0]).mean():.0f}; "
           )
     idx = np.flatnonzero(used)
