@@ -212,6 +212,13 @@ __device__ __forceinline__ int nth_set_bit(uint64_t m, int j) {
   return p;
 }
 
+// lane k's double (k wave-uniform): two v_readlane, no LDS round trip
+__device__ __forceinline__ double lane_value(double v, int k) {
+  const uint64_t b = __double_as_longlong(v);
+  const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)b, k), hi = __builtin_amdgcn_readlane((uint32_t)(b >> 32), k);
+  return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+
 // d_start_retreat by the whole wave for actor a when its route fits the lanes
 // (RA <= 64: lane i holds route point i). Every per-point expression of
 // d_smooth_route is evaluated as there, one point per lane; the two serial sums
@@ -219,8 +226,12 @@ __device__ __forceinline__ int nth_set_bit(uint64_t m, int j) {
 // shuffles and the target search reduces the same candidates, so the result is
 // the serial one bit for bit. Retreats are rare but each serial rebuild costs a
 // lane ~50 k cycles, which the whole k_actors launch then waits for.
+// The record is only touched by this wave here, so workgroup-scope fences order
+// the lanes' global stores and loads (same CU); agent scope would also flush L2.
+__device__ __forceinline__ void wave_mem_fence() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup"); }
+
 __device__ __noinline__ void wave_start_retreat(DRec& r, int a, int lane) {
-  __threadfence();  // the owner lane's behaviour stores come first
+  wave_mem_fence();  // the owner lane's behaviour stores come first
   const int RA = r.RA;
   const int nrx = RAI(r, CBEV_AI_NRX, a);
   int cur = RAI(r, CBEV_AI_TIDX, a);
@@ -245,7 +256,7 @@ __device__ __noinline__ void wave_start_retreat(DRec& r, int a, int lane) {
   const int src = lane < nd ? nth_set_bit(km, lane) : 0;
   double qx = __shfl(px, src), qy = __shfl(py, src);  // deduplicated point `lane`
   if (nd < 2) {
-    const double x0 = __shfl(qx, 0), y0 = __shfl(qy, 0);
+    const double x0 = lane_value(qx, 0), y0 = lane_value(qy, 0);
     qx = lane == 1 ? x0 + 1e-3 : x0;
     qy = y0;
     nd = 2;
@@ -258,7 +269,9 @@ __device__ __noinline__ void wave_start_retreat(DRec& r, int a, int lane) {
   if (nd >= w) {  // Savitzky-Golay (mode='interp'): y first, then x, as the serial pass
     const int i = lane;
     double accy = 0.0, accx = 0.0;
-    for (int j = 0; j < w; ++j) {
+#pragma unroll
+    for (int j = 0; j < 11; ++j) {  // unrolled to the widest window: the coefficient loads go out together
+      if (j >= w) break;
       int idx;
       double c;
       if (i < h) {
@@ -283,7 +296,7 @@ __device__ __noinline__ void wave_start_retreat(DRec& r, int a, int lane) {
   const double seg = lane > 0 ? hypot(cxv - pcx, cyv - pcy) : 0.0;
   double total = 0.0, sv = 0.0;
   for (int k = 1; k < nd; ++k) {
-    total += __shfl(seg, k);
+    total += lane_value(seg, k);
     if (lane == k) sv = total;
   }
   double yawv = 0.0;
@@ -317,7 +330,7 @@ __device__ __noinline__ void wave_start_retreat(DRec& r, int a, int lane) {
     }
     double acc = 0.0, av = 0.0;
     for (int k = 1; k < nd; ++k) {
-      acc += __shfl(corr, k);
+      acc += lane_value(corr, k);
       if (lane == k) av = acc;
     }
     yawv = raw + av;
@@ -340,7 +353,7 @@ __device__ __noinline__ void wave_start_retreat(DRec& r, int a, int lane) {
   // ---- Actor.set_route_surface / Controller.set_route(jitter_start=False): pose at the
   // smoothed start, target index from there (calc_target_index), heading cyaw[idx]
   const int m = nd;
-  const double x0 = __shfl(cxv, 0), y0 = __shfl(cyv, 0);
+  const double x0 = lane_value(cxv, 0), y0 = lane_value(cyv, 0);
   const double yaw_old = RAD(r, CBEV_AD_YAW, a);
   const double fx = x0 + CB_WHEELBASE * cos(yaw_old), fy = y0 + CB_WHEELBASE * sin(yaw_old);
   const double dxl = fx - cxv, dyl = fy - cyv;
@@ -354,7 +367,7 @@ __device__ __noinline__ void wave_start_retreat(DRec& r, int a, int lane) {
   }
   group_argmin<64>(bd, bi);
   const int tidx = bi == 0x7fffffff ? 0 : bi;
-  const double yaw_new = __shfl(yawv, tidx);
+  const double yaw_new = lane_value(yawv, tidx);
   if (lane == 0) {
     RAD(r, CBEV_AD_GOAL_X, a) = gx0;
     RAD(r, CBEV_AD_GOAL_Y, a) = gy0;
@@ -367,7 +380,7 @@ __device__ __noinline__ void wave_start_retreat(DRec& r, int a, int lane) {
     RAD(r, CBEV_AD_YAW, a) = yaw_new;
     d_bset(r, a, CBEV_BST_RETREATING, RAD(r, CBEV_AD_CRUISE_MPS, a));
   }
-  __threadfence();  // the other lanes read these record fields next
+  wave_mem_fence();  // the other lanes read these record fields next
 }
 
 // Behaviour.apply (lead_brake.py:10-15, jaywalk.py:56-138). DEFER: a due
@@ -1050,6 +1063,11 @@ __device__ __forceinline__ int actor_search(const DRec& r, int nact, uint64_t li
 #ifndef CBEV_ACTORS_WAVES
 #define CBEV_ACTORS_WAVES 1
 #endif
+// WIDE: the context's capacities allow more than 64 actors or more than 64
+// actor route points, which take the serial per-lane paths (d_actor_step,
+// d_start_retreat). Contexts within 64 / 64 launch k_actors<false>, which
+// compiles without them: 106 instead of 229 VGPRs, 4 waves per SIMD instead of 2.
+template <bool WIDE>
 __global__ __launch_bounds__(256, CBEV_ACTORS_WAVES) void k_actors(KArgs K, uint8_t* __restrict__ recs, int n, int t_ahead) {
   const int lane = threadIdx.x & 63;
   const int e = xcd_env4_of_wg(blockIdx.x, threadIdx.x >> 6, n);
@@ -1058,7 +1076,7 @@ __global__ __launch_bounds__(256, CBEV_ACTORS_WAVES) void k_actors(KArgs K, uint
   const int nact = r.hi[CBEV_HI_NACT];
   if (nact == 0) return;
   const double t = t_ahead ? r.hd[CBEV_HD_T] + CB_DT : r.hd[CBEV_HD_T];
-  if (nact > 64) {
+  if (WIDE && nact > 64) {
     for (int a = lane; a < nact; a += 64) d_actor_step(r, a, t);
     return;
   }
@@ -1080,9 +1098,9 @@ __global__ __launch_bounds__(256, CBEV_ACTORS_WAVES) void k_actors(KArgs K, uint
         rm &= rm - 1;
         wave_start_retreat(r, k, lane);
       }
-    } else if (retreat) {
-      d_start_retreat(r, a);
-      __threadfence();
+    } else if (WIDE) {
+      if (retreat) d_start_retreat(r, a);
+      wave_mem_fence();
     }
   }
   if (a < nact) {
@@ -3100,6 +3118,10 @@ static KArgs kargs(const cbev_ctx* c) {
   return K;
 }
 
+typedef void (*ActorsKernel)(KArgs, uint8_t*, int, int);
+static ActorsKernel actors_kernel(const cbev_caps& C) {
+  return (C.actor_cap > 64 || C.actor_route_cap > 64) ? k_actors<true> : k_actors<false>;
+}
 static const void* raster_kernel(int size) {
   return size == 64 ? (const void*)k_raster<1> : size == 128 ? (const void*)k_raster<2> : (const void*)k_raster<4>;
 }
@@ -3337,7 +3359,7 @@ int cbev_step(cbev_ctx* c, void* records, int n, const void* actions, uint8_t* f
   if (ev) HIP_TRY(hipEventRecord(ev[0], s));
   if (c->step_mode == CBEV_STEP_FUSED) {
     // k_actors (clock look-ahead: k_step advances hd[T]) + one fused launch
-    if (c->C.actor_cap > 0) hipLaunchKernelGGL(k_actors, dim3(wg4), dim3(256), 0, s, K, (uint8_t*)records, n, 1);
+    if (c->C.actor_cap > 0) hipLaunchKernelGGL(actors_kernel(c->C), dim3(wg4), dim3(256), 0, s, K, (uint8_t*)records, n, 1);
     if (ev) HIP_TRY(hipEventRecord(ev[1], s));
     const dim3 grid((n + CBEV_STEP_NE - 1) / CBEV_STEP_NE);
     switch (c->P.size) {
@@ -3358,7 +3380,7 @@ int cbev_step(cbev_ctx* c, void* records, int n, const void* actions, uint8_t* f
   hipLaunchKernelGGL(k_hero, dim3((n + c->hero_ne - 1) / c->hero_ne), dim3(256),
                      (size_t)c->hero_ne * (c->hero_sb + 32), s, K,
                      (uint8_t*)records, n, actions, c->hero_ne, c->hero_sb);
-  if (c->C.actor_cap > 0) hipLaunchKernelGGL(k_actors, dim3(wg4), dim3(256), 0, s, K, (uint8_t*)records, n, 0);
+  if (c->C.actor_cap > 0) hipLaunchKernelGGL(actors_kernel(c->C), dim3(wg4), dim3(256), 0, s, K, (uint8_t*)records, n, 0);
   if (ev) HIP_TRY(hipEventRecord(ev[1], s));
   {
     const size_t lb = raster_lds_bytes(c->P);
