@@ -271,9 +271,8 @@ __device__ __noinline__ void wave_start_retreat(DRec& r, int a, int lane) {
     double accy = 0.0, accx = 0.0;
 #pragma unroll
     for (int j = 0; j < 11; ++j) {  // unrolled to the widest window: the coefficient loads go out together
-      if (j >= w) break;
-      int idx;
-      double c;
+      int idx = 0;
+      double c = 0.0;
       if (i < h) {
         idx = j;
         c = c_sg.left[ti][i][j];
@@ -285,8 +284,10 @@ __device__ __noinline__ void wave_start_retreat(DRec& r, int a, int lane) {
         c = c_sg.conv[ti][j];
       }
       const double vy = __shfl(qy, idx & 63), vx = __shfl(qx, idx & 63);
-      accy += c * vy;
-      accx += c * vx;
+      if (j < w) {  // the serial sum's terms, in its order
+        accy += c * vy;
+        accx += c * vx;
+      }
     }
     cxv = accx;
     cyv = accy;
@@ -1027,20 +1028,34 @@ __device__ __forceinline__ int actor_search(const DRec& r, int nact, uint64_t li
     const bool glive = aa < nact && ((livem >> (aa & 63)) & 1ull);
     const double* cx = r.acx + (int64_t)(aa & 63) * RA;
     const double* cy = r.acy + (int64_t)(aa & 63) * RA;
-    double m2 = INFINITY;
+    // pass 1: the smallest squared distance (first index) and the runner-up's
+    double m2 = INFINITY, s2 = INFINITY;
+    int i2 = 0x7fffffff;
     if (glive) {
 #pragma unroll 8
       for (int i = sub; i < gn; i += AW) {
         const double dx = gfx - cx[i], dy = gfy - cy[i];
         const double d2 = dx * dx + dy * dy;
-        m2 = d2 < m2 ? d2 : m2;
+        if (d2 < m2) {
+          s2 = m2;
+          m2 = d2;
+          i2 = i;
+        } else if (d2 < s2) {
+          s2 = d2;
+        }
       }
     }
-    m2 = group_min<AW>(m2);
+    group_min2<AW>(m2, i2, s2);
     const double lim = m2 * (1.0 + 1e-14);
+    // pass 2 (hypot over the candidates within (1 + 1e-14) of the minimum) only
+    // when a second point is a candidate; otherwise the arg-min is the answer
+    const bool need = !(s2 > lim);
     double bd = INFINITY;
     int bi = 0x7fffffff;
-    if (glive) {
+    if (!need) {
+      bd = 0.0;
+      bi = i2;
+    } else if (glive) {
       for (int i = sub; i < gn; i += AW) {
         const double dx = gfx - cx[i], dy = gfy - cy[i];
         if (!(dx * dx + dy * dy <= lim)) continue;

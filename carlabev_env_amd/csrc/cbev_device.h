@@ -158,6 +158,25 @@ __device__ __forceinline__ void group_argmin(double& v, int& i) {
     }
   }
 }
+// (minimum, its first index, the smallest other value) over W lanes: the
+// runner-up decides whether a second arg-min candidate exists
+template <int W>
+__device__ __forceinline__ void group_min2(double& m, int& i, double& s) {
+#pragma unroll
+  for (int off = W / 2; off > 0; off >>= 1) {
+    const double om = __shfl_xor(m, off, 64), os = __shfl_xor(s, off, 64);
+    const int oi = __shfl_xor(i, off, 64);
+    double ns = os < s ? os : s;
+    if (om < m || (om == m && oi < i)) {
+      ns = m < ns ? m : ns;
+      m = om;
+      i = oi;
+    } else {
+      ns = om < ns ? om : ns;
+    }
+    s = ns;
+  }
+}
 template <int W>
 __device__ __forceinline__ double group_min(double v) {
 #pragma unroll
