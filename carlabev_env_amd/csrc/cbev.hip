@@ -269,8 +269,10 @@ __device__ __noinline__ void wave_start_retreat(DRec& r, int a, int lane) {
   if (nd >= w) {  // Savitzky-Golay (mode='interp'): y first, then x, as the serial pass
     const int i = lane;
     double accy = 0.0, accx = 0.0;
-#pragma unroll
-    for (int j = 0; j < 11; ++j) {  // unrolled to the widest window: the coefficient loads go out together
+    // not unrolled: this callee's registers count against every k_actors wave
+    // (unrolled: 161 instead of 88 VGPRs, 3 instead of 5 waves per SIMD)
+#pragma unroll 1
+    for (int j = 0; j < 11; ++j) {
       int idx = 0;
       double c = 0.0;
       if (i < h) {
@@ -1031,8 +1033,11 @@ __device__ __forceinline__ int actor_search(const DRec& r, int nact, uint64_t li
     // pass 1: the smallest squared distance (first index) and the runner-up's
     double m2 = INFINITY, s2 = INFINITY;
     int i2 = 0x7fffffff;
+#ifndef CBEV_ACTOR_SEARCH_UNROLL  // route points per lane with loads in flight
+#define CBEV_ACTOR_SEARCH_UNROLL 8
+#endif
     if (glive) {
-#pragma unroll 8
+#pragma unroll CBEV_ACTOR_SEARCH_UNROLL
       for (int i = sub; i < gn; i += AW) {
         const double dx = gfx - cx[i], dy = gfy - cy[i];
         const double d2 = dx * dx + dy * dy;
