@@ -3,7 +3,7 @@ mkdir -p gpurun_out/rr
 export TMPDIR=/tmp
 timeout -k 10 300 python -u -m pytest tests -x -q -m gpu -k "reset or surface or bank" --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 || { echo pytest failed; tail -30 gpurun_out/pytest_gpu.log; exit 1; }
 tail -1 gpurun_out/pytest_gpu.log
-for cfg in 2 5; do for so in tools/micro/so/*.so; do
+for cfg in ${CFGS:-2 5}; do for so in tools/micro/so/*.so; do
   n=$(basename $so .so)_$cfg
   CBEV_LIB=$so timeout -k 10 200 rocprofv3 --kernel-trace --stats -d gpurun_out/rr/$n -o $n --output-format csv -- python bench.py --config $cfg --steps 200 --warmup 20 --no-cpu-baseline --no-wire > gpurun_out/rr/$n.log 2>&1 || { echo "$n failed"; tail -3 gpurun_out/rr/$n.log; exit 1; }
   python - "$n" <<'PY'
