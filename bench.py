@@ -319,7 +319,11 @@ def main():
             "raster_ms_per_launch": None if burst_ms is None else round(burst_ms, 5),
             "roofline": {"bound": "hbm", "kernel": "k_step" if fused else "k_raster", "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": traffic, "algorithmic_bytes_per_env": algo_bytes},
+                         "traffic": traffic, "algorithmic_bytes_per_env": algo_bytes,
+                         "timing": (f"HIP events around {args.raster_reps} back-to-back launches on the step stream"
+                                    if burst_ms is not None else "HIP events around each launch in the timed steps"),
+                         # the same bytes over the per-step event time (includes each launch's dispatch gap)
+                         "achieved_step_events": round(n * algo_bytes / (ms3[1] * 1e-3) / 1e9, 1)},
             "with_wire_obs": None if wire_value is None else round(wire_value, 1),
             "cpu_baseline": cpu,
         }
