@@ -20,6 +20,7 @@ import oracle as O
 from carlabev_env_amd import layout as LY
 from carlabev_env_amd._lib import check, lib
 from carlabev_env_amd.semantics import gray_lut, rgb_lut, semantic_lut, rgb_to_semantic_mask_ids, PALETTE
+from carlabev_env_amd.config import RandomNavigationReset, build_random_navigation_options
 from helpers import CAPS_FULL, action_stream, build_records, world
 
 pytestmark = pytest.mark.gpu
@@ -77,13 +78,30 @@ def compare_records(a: np.ndarray, b: np.ndarray, layout, tag=""):
         assert angles_close(va.acyaw[a, :m], vb.acyaw[a, :m]), (tag, "acyaw", a)
 
 
+def info_of(v, cause):
+    """The per-step export cbev_step writes to `info` (include/cbev.h), from an oracle record."""
+    o = np.zeros(16, np.float32)
+    o[0:7] = v.hd[LY.HD["C_SPEED"]:LY.HD["C_SPEED"] + 7]
+    o[7:11] = v.hd[LY.HD["U_GAS"]:LY.HD["U_GAS"] + 4]
+    o[11] = v.h("REWARD")
+    o[12] = v.h("DIST2WP")
+    o[13] = v.i("TILE")
+    o[14] = v.i("COLLIDED")
+    o[15] = v.i("NACTSTATE")
+    return o
+
+
 def run_parity(kinds, n_envs, steps, size=128, profile="discrete9_v1", reward="carl_base_v1", seed0=0, anchor_y=0.5,
-               act_seed=1234, edit=None, fov=False, mode=None):
-    cfg, P, padded, layout, builder = world(size, profile, reward, anchor_y)
-    recs, _ = build_records(builder, n_envs, kinds, seed0=seed0)
+               act_seed=1234, edit=None, fov=False, mode=None, caps=CAPS_FULL, options=None):
+    cfg, P, padded, layout, builder = world(size, profile, reward, anchor_y, caps=caps)
+    if options is None:
+        recs, _ = build_records(builder, n_envs, kinds, seed0=seed0)
+    else:  # explicit scene options (e.g. more vehicles than the difficulty presets)
+        recs, _ = builder.build_many([seed0 + i for i in range(n_envs)],
+                                     lambda k, s: dict(options[k % len(options)], scene_seed=s))
     if edit is not None:  # hand-made states on top of the seeded scenes
         edit(recs, layout, P)
-    dw = DevWorld(P, padded, CAPS_FULL)
+    dw = DevWorld(P, padded, caps)
     L = lib()
     if mode is not None:  # cbev_set_step_mode: the fused k_step must give the same results
         check(L.cbev_set_step_mode(dw.ctx, mode), "step mode")
@@ -99,7 +117,7 @@ def run_parity(kinds, n_envs, steps, size=128, profile="discrete9_v1", reward="c
     d_recs = torch.from_numpy(recs.copy()).cuda()
     d_frames = torch.zeros((n_envs, S, S), dtype=torch.uint8, device="cuda")
     check(L.cbev_reset(dw.ctx, ptr(d_recs), n_envs, None, 0, None, None, 0, ptr(d_frames), 1, None), "reset")
-    orc = O.Oracle(P, padded, CAPS_FULL.c(), layout.record_bytes)
+    orc = O.Oracle(P, padded, caps.c(), layout.record_bytes)
     h_frames = np.zeros((n_envs, S, S), np.uint8)
     for e in range(n_envs):
         orc.reset_obs(recs[e], h_frames[e])
@@ -118,8 +136,9 @@ def run_parity(kinds, n_envs, steps, size=128, profile="discrete9_v1", reward="c
         a = torch.from_numpy(np.ascontiguousarray(acts[t])).cuda()
         check(L.cbev_step(dw.ctx, ptr(d_recs), n_envs, ptr(a), ptr(d_frames), ptr(rew), ptr(term), ptr(trunc),
                           ptr(cause), ptr(info), None), "step")
+        h_cause = np.zeros(n_envs, np.int32)
         for e in range(n_envs):
-            orc.step_one(recs[e], np.ascontiguousarray(acts[t, e]), h_frames[e])
+            h_cause[e] = orc.step_one(recs[e], np.ascontiguousarray(acts[t, e]), h_frames[e])
             if omask is not None:
                 h_frames[e][omask] = 8  # CBEV_PX_BLACK
         torch.cuda.synchronize()
@@ -133,6 +152,12 @@ def run_parity(kinds, n_envs, steps, size=128, profile="discrete9_v1", reward="c
         assert np.array_equal(term.cpu().numpy(), np.array([v.i("TERM") for v in views], np.uint8))
         assert np.array_equal(trunc.cpu().numpy(), np.array([v.i("TRUNC") for v in views], np.uint8))
         assert np.allclose(rew.cpu().numpy(), [v.h("REWARD") for v in views], rtol=1e-9, atol=1e-12)
+        # this step's cause (not the record's sticky last non-None cause) and the per-step export
+        assert np.array_equal(cause.cpu().numpy(), h_cause), (t, cause.cpu().numpy(), h_cause)
+        want = np.stack([info_of(v, h_cause[e]) for e, v in enumerate(views)])
+        got = info.cpu().numpy()
+        assert np.array_equal(got[:, 13:], want[:, 13:]), (t, "info ints")
+        assert np.allclose(got, want, rtol=1e-6, atol=1e-6), (t, "info")
         n_term += int(term.sum())
     return n_term
 
@@ -367,3 +392,99 @@ def test_profile_raster_rerenders_the_step():
         # the fused step writes no render set-up: refused, not a wrong render
         check(L.cbev_set_step_mode(dw.ctx, 0), "mode")
         assert L.cbev_profile_raster(dw.ctx, ptr(d_recs), n, ptr(again), 1, None, ctypes.byref(ms)) != 0
+
+
+CAPS_WIDE = LY.Caps(128, 96, 128, 4)
+
+
+def test_parity_wide_actor_kernel():
+    """k_actors<true>: capacities above 64 actors / 64 route points select the wide kernel.
+    More than 64 vehicles take the per-lane d_actor_step path; jaywalk scenes with a
+    128-point actor route capacity rebuild a retreating pedestrian's route on one lane
+    (serial d_start_retreat) instead of the wave-wide rebuild (stanley_controller.py:100-123,
+    behavior/jaywalk.py:43-54)."""
+    many = dict(build_random_navigation_options(RandomNavigationReset(difficulty_id="rt_hard_v1")), num_vehicles=72)
+    run_parity(None, 6, 40, seed0=50_000, caps=CAPS_WIDE, options=[many])
+    run_parity(["jaywalk"], 24, 80, seed0=30_000, caps=CAPS_WIDE)
+
+
+def _sample_envs(n, k=160):
+    """>= k env ids spread over the batch: a stride over all of it plus the
+    workgroup / env-block / XCD-round boundaries (16-env staged workgroups, 64-env
+    blocks, 512-env XCD rounds) and the last env."""
+    ids = set(np.linspace(0, n - 1, k).astype(int).tolist())
+    for b in (16, 64, 512):
+        for j in range(0, n, max(b, n // 16)):
+            ids.update(x for x in (j - 1, j, j + 1) if 0 <= x < n)
+    ids.add(n - 1)
+    return np.array(sorted(ids))
+
+
+def run_full_size(kinds, n_envs, size=128, profile="discrete9_v1", seed0=0, steps=16, distinct=160, act_seed=1):
+    """The HIP path at a benchmarked batch size (grid shapes, XCD placement and
+    staging batches of the bench) against the oracle on a sampled subset of envs.
+    `distinct` seeded scenes are tiled over the batch (env e gets scene e % distinct);
+    every env gets its own action stream, so tiled copies diverge."""
+    cfg, P, padded, layout, builder = world(size, profile, "carl_base_v1", 0.5)
+    base, _ = build_records(builder, distinct, kinds, seed0=seed0)
+    recs = base[np.arange(n_envs) % distinct].copy()
+    dw = DevWorld(P, padded, CAPS_FULL)
+    L = lib()
+    S = P.size
+    rng = np.random.default_rng(act_seed)
+    if P.action_kind == 0:
+        p = np.ones(P.n_discrete)
+        p[1] += 4.0
+        acts = rng.choice(P.n_discrete, size=(steps, n_envs), p=p / p.sum()).astype(np.int32)
+    else:
+        acts = rng.uniform([0, -1, 0], [1, 1, 1], size=(steps, n_envs, 3)).astype(np.float32)
+    sample = _sample_envs(n_envs)
+    d_recs = torch.from_numpy(recs).cuda()
+    d_frames = torch.zeros((n_envs, S, S), dtype=torch.uint8, device="cuda")
+    check(L.cbev_reset(dw.ctx, ptr(d_recs), n_envs, None, 0, None, None, 0, ptr(d_frames), 1, None), "reset")
+    orc = O.Oracle(P, padded, CAPS_FULL.c(), layout.record_bytes)
+    h_recs = recs[sample].copy()
+    h_frames = np.zeros((len(sample), S, S), np.uint8)
+    rew = torch.zeros(n_envs, dtype=torch.float64, device="cuda")
+    term = torch.zeros(n_envs, dtype=torch.uint8, device="cuda")
+    trunc = torch.zeros_like(term)
+    cause = torch.zeros(n_envs, dtype=torch.int32, device="cuda")
+    info = torch.zeros((n_envs, 16), dtype=torch.float32, device="cuda")
+    for t in range(steps):
+        a = torch.from_numpy(np.ascontiguousarray(acts[t])).cuda()
+        check(L.cbev_step(dw.ctx, ptr(d_recs), n_envs, ptr(a), ptr(d_frames), ptr(rew), ptr(term), ptr(trunc),
+                          ptr(cause), ptr(info), None), "step")
+        h_cause = np.array([orc.step_one(h_recs[j], np.ascontiguousarray(acts[t, e]), h_frames[j])
+                            for j, e in enumerate(sample)], np.int32)
+        torch.cuda.synchronize()
+        sel = torch.from_numpy(sample).cuda()
+        df = d_frames[sel].cpu().numpy()
+        bad = np.argwhere(df != h_frames)
+        assert bad.size == 0, (t, sample[bad[0][0]], bad[:4])
+        dr = d_recs[sel].cpu().numpy()
+        for j, e in enumerate(sample):
+            compare_records(dr[j], h_recs[j], layout, tag=(t, int(e)))
+        views = [LY.RecordView(h_recs[j], layout) for j in range(len(sample))]
+        assert np.array_equal(term[sel].cpu().numpy(), [v.i("TERM") for v in views])
+        assert np.array_equal(trunc[sel].cpu().numpy(), [v.i("TRUNC") for v in views])
+        assert np.array_equal(cause[sel].cpu().numpy(), h_cause)
+        assert np.allclose(rew[sel].cpu().numpy(), [v.h("REWARD") for v in views], rtol=1e-9, atol=1e-12)
+        got, want = info[sel].cpu().numpy(), np.stack([info_of(v, 0) for v in views])
+        assert np.array_equal(got[:, 13:], want[:, 13:]) and np.allclose(got, want, rtol=1e-6, atol=1e-6), t
+    return len(sample)
+
+
+def test_full_size_config2():
+    assert run_full_size(["rt_no_traffic_v1"], 4096, seed0=10_000) >= 128
+
+
+def test_full_size_config3():
+    run_full_size(["rt_hard_v1"], 4096, seed0=20_000, act_seed=7)
+
+
+def test_full_size_config4_shard():
+    run_full_size(["rt_medium_v1"], 8192, profile="continuous_gsb_v1", seed0=40_000, act_seed=99)
+
+
+def test_full_size_config5():
+    run_full_size(["mix3"], 2048, size=256, seed0=30_000, steps=12)
