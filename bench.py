@@ -21,6 +21,8 @@ import argparse
 import ctypes
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -158,6 +160,86 @@ def cpu_baseline(cfgd, host_recs, env, seconds):
                       "per-step full padded-map restore as in scene.py:93"}
 
 
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int) -> int:
+    """`bench.py --gpus N` run by hand (no torch.distributed.run around it): start
+    N rank processes of this same script, one per GPU, with RANK / LOCAL_RANK /
+    WORLD_SIZE / MASTER_* set, and wait for them. The parent never touches the
+    GPU (it has not imported torch); rank 0 prints the JSON line. If any rank
+    fails, the others are terminated (by PID) so none waits in a barrier."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]], env=env,
+                                      stdout=None if r == 0 else subprocess.DEVNULL))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                log(f"[launcher] rank {procs.index(p)} exited with {code}; stopping the others")
+                for q in live:
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
+
+
+def dry_run(args, world, rank):
+    """CPU rehearsal of the N-rank path (gloo): rendezvous, the packed frame
+    gather of config 4 (FrameGather on CPU tensors), barrier-bracketed timing and
+    the max over ranks. No GPU and no env: `value` stays null."""
+    import torch
+    import torch.distributed as dist
+    from carlabev_env_amd.sharding import FrameGather
+    if world > 1:
+        dist.init_process_group("gloo")
+    n, S = args.envs or 8, CONFIGS[args.config]["size"]
+    g = FrameGather(n, S, "cpu") if world > 1 else None
+    frames = torch.full((n, S, S), rank, dtype=torch.uint8)
+    rew = torch.arange(n, dtype=torch.float64) + 1000 * rank
+    term = torch.zeros(n, dtype=torch.uint8)
+    ok = True
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        if g is not None:
+            g.gather(frames, rew, term)
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([el], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        el = float(tt.item())
+        if rank == 0:
+            f, r, _c, _t, _tr = g.gathered()
+            ok = all(bool((f[k * n:(k + 1) * n] == k).all()) and bool((r[k * n:(k + 1) * n] == rew - 1000 * rank + 1000 * k).all())
+                     for k in range(world))
+    if rank == 0:
+        print(json.dumps({"metric": "env-steps/sec (whole node) at N_envs x 128x128 semantic obs", "value": None,
+                          "unit": "env-steps/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": round(el / max(args.steps, 1) * 1e3, 4), "dry_run": True,
+                          "gather_ok": ok, "gather_bytes_per_step": None if g is None else g.bytes_per_step,
+                          "config": {"config_id": args.config, "envs_per_gpu": n, "global_envs": n * world}}),
+              flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -169,13 +251,21 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-wire", action="store_true")
     ap.add_argument("--raster-reps", type=int, default=50, help="back-to-back k_raster launches timed for the roofline")
+    ap.add_argument("--dry-run", action="store_true", help="CPU/gloo rehearsal of the N-rank path (no GPU, value null)")
     args = ap.parse_args()
 
-    import torch
-    import torch.distributed as dist
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and rank == 0:
+        log(f"[bench] WORLD_SIZE={world} overrides --gpus {args.gpus}")
+    if args.dry_run:
+        return dry_run(args, world, rank)
+
+    import torch
+    import torch.distributed as dist
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
     if world > 1:
@@ -188,14 +278,17 @@ def main():
     total_steps = args.warmup + args.steps
     acts = torch.from_numpy(make_actions(P, n, total_steps, cfgd["act_seed"], rank * n)).to(device)
     gather = cfgd.get("gather", False) and world > 1
-    from carlabev_env_amd.sharding import gather_frames
+    gatherer = None
+    if gather:
+        from carlabev_env_amd.sharding import FrameGather
+        gatherer = FrameGather(n, cfgd["size"], device, dst=0)
 
     env.auto_obs = False
 
     def one_step(t, wire):
         env.step_async_only(acts[t])
-        if gather:  # config 4: uint8 class-id frames + reward/term of every rank to rank 0 (RCCL)
-            gather_frames(env.frames(), env.reward, env.term, dst=0)
+        if gatherer is not None:  # config 4: frames + reward/cause/flags of every rank to rank 0, one RCCL gather
+            gatherer.gather(env.frames(), env.reward, env.term, env.trunc, env.cause)
         env.reset_from_bank(mask=env.term)  # canonical loop: reset(reset_mask=terminated)
         if wire:
             env._obs()
@@ -325,6 +418,7 @@ def main():
                          # the same bytes over the per-step event time (includes each launch's dispatch gap)
                          "achieved_step_events": round(n * algo_bytes / (ms3[1] * 1e-3) / 1e9, 1)},
             "with_wire_obs": None if wire_value is None else round(wire_value, 1),
+            "gather_bytes_per_step": None if gatherer is None else gatherer.bytes_per_step,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

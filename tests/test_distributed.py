@@ -80,6 +80,77 @@ def test_sharded_gather_matches_single_process():
     assert np.array_equal(got[2], ref[2])
 
 
+def test_bench_launcher_dry_run_two_ranks():
+    """`bench.py --gpus 2` started by hand spawns two ranks itself (gloo rehearsal:
+    rendezvous, the packed one-collective gather, max-over-ranks timing) and
+    rank 0 reports n_gpus 2."""
+    import json
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    out = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--gpus", "2", "--dry-run", "--steps", "3",
+                          "--envs", "4", "--config", "4"], env=env, capture_output=True, text=True, timeout=240)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 2 and rec["dry_run"] and rec["gather_ok"]
+    from carlabev_env_amd.sharding import payload_bytes
+    assert rec["gather_bytes_per_step"] == payload_bytes(4, 128)
+
+
+def _packed_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from carlabev_env_amd.sharding import FrameGather
+        n, S = 5, 16
+        g = FrameGather(n, S, "cpu")
+        send_ptr = g.send.data_ptr()
+        for step in range(3):  # buffers are reused across steps
+            gen = torch.Generator().manual_seed(100 * rank + step)
+            fr = torch.randint(0, 10, (n, S, S), dtype=torch.uint8, generator=gen)
+            rew = torch.randn(n, dtype=torch.float64, generator=gen)
+            term = (torch.rand(n, generator=gen) < 0.5).to(torch.uint8)
+            trunc = (torch.rand(n, generator=gen) < 0.5).to(torch.uint8)
+            cause = torch.randint(-1, 6, (n,), dtype=torch.int32, generator=gen)
+            g.gather(fr, rew, term, trunc, cause)
+            assert g.send.data_ptr() == send_ptr
+            if rank == 0:
+                q.put((step, tuple(t.clone().numpy() for t in g.gathered())))
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_packed_gather_all_fields():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_packed_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=240) for _ in range(3)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    n, S = 5, 16
+    for step, (fr, rew, cause, term, trunc) in got:
+        for r in range(world):
+            gen = torch.Generator().manual_seed(100 * r + step)
+            e_fr = torch.randint(0, 10, (n, S, S), dtype=torch.uint8, generator=gen).numpy()
+            e_rew = torch.randn(n, dtype=torch.float64, generator=gen).numpy()
+            e_term = (torch.rand(n, generator=gen) < 0.5).to(torch.uint8).numpy()
+            e_trunc = (torch.rand(n, generator=gen) < 0.5).to(torch.uint8).numpy()
+            e_cause = torch.randint(-1, 6, (n,), dtype=torch.int32, generator=gen).numpy()
+            sl = slice(r * n, (r + 1) * n)
+            assert np.array_equal(fr[sl], e_fr) and np.array_equal(rew[sl], e_rew)
+            assert np.array_equal(term[sl], e_term) and np.array_equal(trunc[sl], e_trunc)
+            assert np.array_equal(cause[sl], e_cause)
+
+
 def test_rank_ids_and_seeds():
     from carlabev_env_amd.sharding import action_seeds, rank_env_ids, scene_seeds
     assert list(rank_env_ids(1, 4)) == [4, 5, 6, 7]
