@@ -348,16 +348,15 @@ def main():
         el_prof, ms3, _ = timed(False, True)  # same workload with HIP events around each kernel (roofline)
         value = world * n * args.steps / el
         burst_ms = None
-        if lib().cbev_step_mode(env._ctx) == 1 and hasattr(lib(), "cbev_profile_raster"):
-            # k_raster's own launch duration: one more step (no reset, so every
-            # record holds this step's render set-up), then a burst of raster
-            # launches over it between two events (cbev_profile_raster); the
-            # per-kernel events above also count each launch's dispatch gap
-            env.step_async_only(acts[total_steps - 1])
-            bm = ctypes.c_double()
-            check(lib().cbev_profile_raster(env._ctx, env.records.data_ptr(), n, env.frames().data_ptr(),
-                                            args.raster_reps, env._stream(), ctypes.byref(bm)), "profile_raster")
-            burst_ms = bm.value
+        # k_raster's own launch duration: one more step (no reset, so every
+        # record holds this step's render set-up), then a burst of raster
+        # launches over it between two events (cbev_profile_raster); the
+        # per-kernel events above also count each launch's dispatch gap
+        env.step_async_only(acts[total_steps - 1])
+        bm = ctypes.c_double()
+        check(lib().cbev_profile_raster(env._ctx, env.records.data_ptr(), n, env.frames().data_ptr(),
+                                        args.raster_reps, env._stream(), ctypes.byref(bm)), "profile_raster")
+        burst_ms = bm.value
         wire_value = None
         if not args.no_wire:
             reseed()
@@ -365,17 +364,9 @@ def main():
             wire_value = world * n * args.steps / el_w
 
     S = P.size
-    mode = lib().cbev_step_mode(env._ctx)  # 0 fused, 1 split, 2 k_hero + raster/collide k_step
-    fused = mode != 1
-    # per env: S^2 texels sampled + S^2 frame bytes + ego state; the
-    # fused k_step also scans the ego route twice (16 B per smoothed point for the
-    # Stanley search, 16 B per raw point for the CaRL progress)
+    # per env: S^2 texels sampled + S^2 frame bytes + ego state
     algo_bytes = 2 * S * S + 64
-    if fused:
-        from carlabev_env_amd import layout as LY
-        hi = LY.batch_views(np.ascontiguousarray(host_recs).reshape(-1), env.layout, host_recs.shape[0])["hi"]
-        algo_bytes += int(round(16 * (mode == 0) * hi[:, LY.HI["NROUTE"]].mean() + 16 * hi[:, LY.HI["NRAW"]].mean()))
-    raster_ms = burst_ms if burst_ms is not None else ms3[1]
+    raster_ms = burst_ms if burst_ms is not None else ms3[2]
     achieved = n * algo_bytes / (raster_ms * 1e-3) / 1e9
     traffic = None
     pmc_path = os.path.join(REPO, "profiles", f"pmc_raster_config{args.config}.json")
@@ -406,17 +397,15 @@ def main():
                        "parallelism": f"env-sharded x{world}" + (" + RCCL gather" if gather else "")},
             "host_enqueue_ms_per_step": round(host_enq / args.steps * 1e3, 4),
             "ms_per_step_with_kernel_events": round(el_prof / args.steps * 1e3, 4),
-            "step_mode": ("fused", "split", "raster_collide")[mode],
-            "kernel_ms": ({("k_hero+k_actors" if mode == 2 else "k_actors"): round(ms3[0], 5), "k_step": round(ms3[1], 5)} if fused else
-                          {"k_hero+k_actors": round(ms3[0], 5), "k_raster": round(ms3[1], 5), "k_collide": round(ms3[2], 5)}),
+            "kernel_ms": {"k_actors": round(ms3[0], 5), "k_ego": round(ms3[1], 5), "k_raster": round(ms3[2], 5)},
             "raster_ms_per_launch": None if burst_ms is None else round(burst_ms, 5),
-            "roofline": {"bound": "hbm", "kernel": "k_step" if fused else "k_raster", "achieved": round(achieved, 1),
+            "roofline": {"bound": "hbm", "kernel": "k_raster", "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic, "algorithmic_bytes_per_env": algo_bytes,
                          "timing": (f"HIP events around {args.raster_reps} back-to-back launches on the step stream"
                                     if burst_ms is not None else "HIP events around each launch in the timed steps"),
                          # the same bytes over the per-step event time (includes each launch's dispatch gap)
-                         "achieved_step_events": round(n * algo_bytes / (ms3[1] * 1e-3) / 1e9, 1)},
+                         "achieved_step_events": round(n * algo_bytes / (ms3[2] * 1e-3) / 1e9, 1)},
             "with_wire_obs": None if wire_value is None else round(wire_value, 1),
             "gather_bytes_per_step": None if gatherer is None else gatherer.bytes_per_step,
             "cpu_baseline": cpu,

@@ -62,17 +62,12 @@ def lib():
     L.cbev_set_obs_size.restype = _I
     L.cbev_resize_obs.argtypes = [_P, _P, _I, _P, _I, _P, _I, _I64, _P]
     L.cbev_resize_obs.restype = _I
-    L.cbev_set_step_mode.argtypes = [_P, _I]
-    L.cbev_set_step_mode.restype = _I
-    L.cbev_step_mode.argtypes = [_P]
-    L.cbev_step_mode.restype = _I
     L.cbev_profile.argtypes = [_P, _I]
     L.cbev_profile.restype = _I
     L.cbev_profile_read.argtypes = [_P, _P, _P]
     L.cbev_profile_read.restype = _I
-    if os.environ.get("CBEV_LIB") is None or hasattr(L, "cbev_profile_raster"):  # (older experiment builds lack it)
-        L.cbev_profile_raster.argtypes = [_P, _P, _I, _P, _I, _P, _P]
-        L.cbev_profile_raster.restype = _I
+    L.cbev_profile_raster.argtypes = [_P, _P, _I, _P, _I, _P, _P]
+    L.cbev_profile_raster.restype = _I
     _lib = L
     return L
 
@@ -87,6 +82,4 @@ EXPORTED_SYMBOLS = ("cbev_abi_version", "cbev_params_size", "cbev_layout_of", "c
                     "cbev_create", "cbev_destroy", "cbev_set_map", "cbev_step", "cbev_reset", "cbev_bank_frames",
                     "cbev_reset_frames",
                     "cbev_expand_obs", "cbev_vector_obs", "cbev_set_fov_mask", "cbev_set_obs_size", "cbev_resize_obs", "cbev_profile", "cbev_profile_read",
-                    "cbev_profile_raster", "cbev_set_step_mode", "cbev_step_mode")
-
-STEP_FUSED, STEP_SPLIT = 0, 1  # cbev_set_step_mode (include/cbev.h)
+                    "cbev_profile_raster")

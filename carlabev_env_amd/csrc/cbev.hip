@@ -1,28 +1,30 @@
 // cbev.hip — MI355X (gfx950) kernels and C-ABI of the batched CarlaBEV step.
 //
-// One `CarlaBEV.step()` for N envs is three or four launches on the caller's stream:
+// One `CarlaBEV.step()` for N envs is two or three launches on the caller's
+// stream, in the reference's data order (actors, ego, render, collision):
 //
-//   k_hero     one thread per env: ego bicycle + Stanley target search,
-//              comfort kinematics, scene clock, dist2goal.
 //   k_actors   wave64 per env, lane per actor: behaviour FSM, PID + Stanley,
 //              bicycle (launched only when the record has actor slots).
-//              Reference: Scene._scene_step (scene.py:90-98), hero.py:88-187,
-//              actor.py:110-124, behavior/*.py, stanley_controller.py:51-123.
+//              Reference: ActorManager.step_all (actor_manager.py:111-119),
+//              actor.py:110-149, behavior/*.py, stanley_controller.py:51-123.
+//   k_ego      `ne` envs per workgroup, records staged in LDS: ego bicycle +
+//              Stanley target search, comfort kinematics, scene clock,
+//              dist2goal, the observation's render set-up; then ego tile, rect
+//              collisions (last hit in draw order wins), target consumption,
+//              actors_state/TTC, CaRL route progress, reward, episode
+//              accumulators, termination flags.
+//              Reference: hero.py:88-187, scene.py:90-140,
+//              carl_reward_fn.py:149-341, reward.py:80-278, stats.py:30-56,
+//              carlabev.py:177-185.
 //   k_raster   256-thread workgroup per env: stage the C x C crop of the padded
-//              class map into LDS (LDS-DMA, lane-linear odd-stride image),
-//              paint vehicles / pedestrians / visible targets / traffic lights
-//              in draw order, then the pygame rotate (16.16 fixed-point inverse
-//              map, stepped per lane, or exact rotate90) + compose at the ego
-//              anchor + ego overlay, written once to HBM as one palette id per
-//              pixel (64-byte contiguous runs per wave store).
+//              class map into LDS (lane-linear odd-stride nibble image), paint
+//              vehicles / pedestrians / the targets visible before this step's
+//              collisions / traffic lights in draw order, then the pygame rotate
+//              (16.16 fixed-point inverse map, stepped per lane, or exact
+//              rotate90) + compose at the ego anchor + ego overlay, written once
+//              to HBM as one palette id per pixel (64-byte runs per wave store).
 //              Reference: BaseMap.draw_fov (world.py:137-157), fov.py:70-99,
 //              actor_manager.py:121-132, hero.py:26-32.
-//   k_collide  one thread per env: ego tile, rect collisions (last hit in
-//              draw order wins), target consumption, actors_state/TTC, CaRL
-//              route progress (arg-min over raw segments), reward, episode
-//              accumulators, termination flags.
-//              Reference: scene.py:110-140, carl_reward_fn.py:149-341,
-//              reward.py:80-278, stats.py:30-56, carlabev.py:177-185.
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdarg.h>
@@ -504,13 +506,6 @@ __device__ __forceinline__ void d_crop_origin(const cbev_params& P, double x, do
 // rect_from_world_center (transforms.py:46-51): centre rounded half-even, x = c - w/2
 __device__ __forceinline__ int d_rect_lo(double w, int pad, int size) { return (int)rint((double)pad + w * 1.0) - size / 2; }
 
-// Phase mask for raster performance experiments (tools/raster_phases.sh):
-// 1 stage, 2 paint, 4 gather, 8 store, 16 read the render set-up, 32 output
-// pass. Products always build with all of them.
-#ifndef CBEV_RASTER_PHASES
-#define CBEV_RASTER_PHASES 63
-#endif
-
 // LDS image of the crop window. Nibble layout (S >= 128), packed like the map:
 // crop row r starts at dword r * sd and holds the packed map bytes from
 // xa = (xmin >> 1) & ~3 on (dword-aligned), so crop pixel (c, r) is texel shift + c
@@ -525,17 +520,13 @@ __device__ __forceinline__ int d_rect_lo(double w, int pad, int size) { return (
 // coordinates) and a byte read, without the nibble select. Texel address
 // = byte address r * 4 sd + shift + c; sd = dwords for 7 + C texels, odd.
 // Rows are dword-aligned in the map (16-byte loads at 4-byte alignment), so a
-// row carries at most 7 texels of slack: 182 x 25 dwords = 18.2 KB at S=128,
-// which leaves room for k_step's per-env state within the 20 KB that keeps 8
-// workgroups per CU.
+// row carries at most 7 texels of slack: 182 x 27 dwords = 19.7 KB at S=128,
+// which keeps 8 workgroups per CU.
 // At S=128 the byte image (182 x 55 dwords = 40 KB) leaves 4 workgroups per CU
 // instead of the nibble image's 8, and measured slower (37 vs 30 us per step
 // raster at 4096 envs) despite half the gather VALU: the raster needs the
 // occupancy to hide latency. S >= 128 keeps the nibble image.
-#ifndef CBEV_RASTER_BYTES_MAX  // largest S with the byte image (experiments: -DCBEV_RASTER_BYTES_MAX=128)
-#define CBEV_RASTER_BYTES_MAX 64
-#endif
-__host__ __device__ __forceinline__ constexpr bool raster_bytes(int S) { return S <= CBEV_RASTER_BYTES_MAX; }
+__host__ __device__ __forceinline__ constexpr bool raster_bytes(int S) { return S <= 64; }
 __host__ __device__ __forceinline__ int raster_stride_dwords(int S, int C) {
   return raster_bytes(S) ? ((C + 7 + 3) / 4) | 1 : ((C + 7 + 7) / 8) | 1;
 }
@@ -639,7 +630,7 @@ __device__ __forceinline__ RotSetup rot_setup(const cbev_params& P, float angle,
 
 // XCD-aware env placement. The dispatcher deals workgroups round-robin over
 // the 8 XCDs (workgroup w -> XCD w % 8), and each XCD has its own L2. The
-// thread-per-env kernels (k_hero, k_collide) put env block b = e / 64 on XCD
+// staged kernel (k_ego) puts env block b = e / 64 on XCD
 // b % 8; the per-env-workgroup kernels (k_raster, k_reset) and k_actors map
 // their workgroups so that env e is handled on that same XCD, keeping each
 // record in one L2 across the step's launches. Exact for n % 512 == 0, the
@@ -689,12 +680,14 @@ __device__ unsigned g_hwid[CBEV_NSTAMP][4096];                   // HW_ID (SE / 
 #define CBEV_STAMPW(kern, slot)
 #endif
 
-// ---- record staging for the thread-per-env kernels. A workgroup owns `ne`
-// envs (a divisor of 64, so a 64-env block stays on one XCD) and copies the
-// first `sbytes` of each record into LDS with LDS-DMA (16-byte lane-linear
-// pieces, all in flight at once), so the float64 scalar chains and the route
-// loops read LDS instead of waiting on HBM; the fields the kernel changes are
-// copied back at the end.
+// ---- record staging for k_ego. A workgroup owns `ne` envs (a divisor of 64,
+// so a 64-env block stays on one XCD) and copies the record ranges its float64
+// chains and element loops read into LDS with LDS-DMA (16-byte lane-linear
+// pieces, all in flight at once), packed per env as
+//   [HD, HI, cx, cy] [raw_x, raw_y] [vis, vis_draw]
+// (EgoPack). Everything read at one index only (cyaw at the target index,
+// raw_cum at two segments) or by a few lanes (actor fields) is read from the
+// record in HBM; the fields the kernel changes are copied back at the end.
 __device__ __forceinline__ int staged_env0(int w, int ne, int n) {
   const int n512 = n & ~511;
   if (w * ne >= n512) return w * ne;
@@ -702,32 +695,67 @@ __device__ __forceinline__ int staged_env0(int w, int ne, int n) {
   return 64 * ((w & 7) + 8 * (j / sub)) + ne * (j % sub);
 }
 
-__device__ __forceinline__ void stage_in(uint8_t* lds, const uint8_t* __restrict__ recs, int e0, int ne, int64_t rb,
-                                         int sbytes) {
-  const int nch = sbytes >> 4, total = ne * nch;
+struct EgoPack {
+  int n0, n1, n2;        // 16-byte pieces of the three ranges
+  int raw_off, vis_off;  // byte offsets of the second and third range in the packed image
+  int bytes;             // packed bytes per env
+};
+__host__ __device__ __forceinline__ EgoPack ego_pack(const cbev_layout& L) {
+  EgoPack p;
+  p.n0 = (int)(L.cyaw / 16);                   // HD, HI, cx, cy (the record's prefix)
+  p.n1 = (int)((L.raw_cum - L.raw_x) / 16);    // raw_x, raw_y
+  p.n2 = (int)((8 * L.vis_words + 15) / 16);   // vis, vis_draw
+  p.raw_off = 16 * p.n0;
+  p.vis_off = 16 * (p.n0 + p.n1);
+  p.bytes = 16 * (p.n0 + p.n1 + p.n2);
+  return p;
+}
+
+// DRec of a staged env: the packed ranges in LDS, every other group in HBM
+__device__ __forceinline__ DRec bind_ego(uint8_t* l, uint8_t* g, const KArgs& K, const EgoPack& p) {
+  DRec r = bind_rec(g, K.L, K.C);
+  r.hd = (double*)(l + K.L.hd);
+  r.hi = (int32_t*)(l + K.L.hi);
+  r.cx = (double*)(l + K.L.cx);
+  r.cy = (double*)(l + K.L.cy);
+  r.raw_x = (int32_t*)(l + p.raw_off);
+  r.raw_y = (int32_t*)(l + p.raw_off + (K.L.raw_y - K.L.raw_x));
+  r.vis = (uint32_t*)(l + p.vis_off);
+  r.vis_draw = r.vis + K.L.vis_words;
+  return r;
+}
+
+// record byte offset of packed piece c
+__device__ __forceinline__ int ego_src(const cbev_layout& L, const EgoPack& p, int c) {
+  return c < p.n0 ? 16 * c : c < p.n0 + p.n1 ? (int)L.raw_x + 16 * (c - p.n0) : (int)L.vis + 16 * (c - p.n0 - p.n1);
+}
+
+// LDS-DMA: piece q of the workgroup lands at LDS byte 16 q (lane-linear per wave)
+__device__ __forceinline__ void ego_stage_in(uint8_t* lds, const uint8_t* __restrict__ recs, int e0, int ne,
+                                             const KArgs& K, const EgoPack& p) {
+  const int nch = p.bytes >> 4, total = ne * nch;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int dk = 256 / nch, dc = 256 - dk * nch;
-  int k = threadIdx.x / nch, c = threadIdx.x - k * nch;
+  const int64_t rb = K.L.record_bytes;
   for (int b = wave * 64; b < total; b += 256) {
-    if (b + lane < total)
-      __builtin_amdgcn_global_load_lds((const void*)(recs + (int64_t)(e0 + k) * rb + 16 * c),
+    const int q = b + lane;
+    if (q < total) {
+      const int k = q / nch, c = q - k * nch;
+      __builtin_amdgcn_global_load_lds((const void*)(recs + (int64_t)(e0 + k) * rb + ego_src(K.L, p, c)),
                                        (__attribute__((address_space(3))) void*)(lds + 16 * b), 16, 0, 0);
-    k += dk;
-    c += dc;
-    if (c >= nch) {
-      c -= nch;
-      ++k;
     }
   }
 }
 
-__device__ __forceinline__ void stage_out(const uint8_t* lds, uint8_t* __restrict__ recs, int e0, int ne, int64_t rb,
-                                          int sbytes, int off, int bytes) {
-  const int nr = bytes >> 4;
-  for (int q = threadIdx.x; q < ne * nr; q += 256) {
-    const int k = q / nr, c = q - k * nr;
-    *(uint4*)(recs + (int64_t)(e0 + k) * rb + off + 16 * c) = *(const uint4*)(lds + k * sbytes + off + 16 * c);
+// the changed ranges back: HD + HI (the first pieces) and the vis group
+__device__ __forceinline__ void ego_stage_out(const uint8_t* lds, uint8_t* __restrict__ recs, int e0, int ne,
+                                              const KArgs& K, const EgoPack& p) {
+  const int nhh = (int)(K.L.cx / 16), nout = nhh + p.n2;
+  const int64_t rb = K.L.record_bytes;
+  for (int q = threadIdx.x; q < ne * nout; q += 256) {
+    const int k = q / nout, j = q - k * nout;
+    const int c = j < nhh ? j : p.n0 + p.n1 + (j - nhh);
+    *(uint4*)(recs + (int64_t)(e0 + k) * rb + ego_src(K.L, p, c)) = *(const uint4*)(lds + k * p.bytes + 16 * c);
   }
 }
 
@@ -749,7 +777,7 @@ __device__ __forceinline__ bool raster_fast(const cbev_params& P, const RotSetup
   return inb;
 }
 
-// The render set-up lives in the record's RS_* ints (written by k_hero, read by k_raster).
+// The render set-up lives in the record's RS_* ints (written by k_ego, read by k_raster).
 __device__ __forceinline__ void d_store_render_setup(const cbev_params& P, int32_t* hi, double x, double y,
                                                      float angle) {
   const RotSetup R = rot_setup(P, angle, raster_row_texels(P.size, P.crop));
@@ -763,7 +791,7 @@ __device__ __forceinline__ void d_store_render_setup(const cbev_params& P, int32
   hi[CBEV_HI_RS_FAST] = raster_fast(P, R);  // so every raster wave does not redo the corner test
 }
 
-// ============================================================== k_hero / k_actors
+// ============================================================== ego update / k_actors
 // Ego update: one thread per env, so all 64 lanes of a wave carry the float64
 // scalar chain of 64 envs (BaseAgent.physics_step, hero.py:88-138).
 // decode_action (envs/spaces.py:43-47); continuous: ContinuousAgent clips in float32
@@ -792,7 +820,7 @@ __device__ __forceinline__ double d_hero_delta(double v, float sa) {
   return d_radians((double)sa * steer_deg);
 }
 
-// Per-env values k_hero computes ahead of the scalar chain, on separate waves:
+// Per-env values k_ego computes ahead of the scalar chain, on separate waves:
 // cos / sin of the pre-update yaw (front axle and State.update) and
 // tan(clip(delta)) of State.update.
 struct HeroPre {
@@ -806,7 +834,7 @@ __device__ __forceinline__ void hero_env_a(const KArgs& K, DRec r, int e, const 
   double* hd = r.hd;
   int32_t* hi = r.hi;
   float g, sa, b;
-  if (gsb) {  // decoded ahead (k_step)
+  if (gsb) {  // decoded ahead
     g = gsb[0];
     sa = gsb[1];
     b = gsb[2];
@@ -820,7 +848,7 @@ __device__ __forceinline__ void hero_env_a(const KArgs& K, DRec r, int e, const 
   for (int k = 0; k < 8; ++k) s[k] = hd[CBEV_HD_X + k];
   // stanley_control's target search (bi: first arg-min, reduced by the workgroup);
   // its steering output is unused by the hero
-  if (bi >= 0) hi[CBEV_HI_TIDX] = hi[CBEV_HI_TIDX] >= bi ? hi[CBEV_HI_TIDX] : bi;  // bi < 0: k_step's search wave
+  hi[CBEV_HI_TIDX] = hi[CBEV_HI_TIDX] >= bi ? hi[CBEV_HI_TIDX] : bi;
   const double v = s[3];
   const int scale = K.P.scale;
   // BaseAgent.accelerate / steering / brake (hero.py:140-162)
@@ -892,116 +920,11 @@ __device__ __forceinline__ void hero_env_render_setup(const KArgs& K, DRec r) {
   d_store_render_setup(K.P, r.hi, hd[CBEV_HD_X], hd[CBEV_HD_Y], (float)(d_degrees(hd[CBEV_HD_YAW]) + 90));
 }
 
-__global__ __launch_bounds__(256) void k_hero(KArgs K, uint8_t* __restrict__ recs, int n,
-                                              const void* __restrict__ actions, int ne, int sbytes) {
-  extern __shared__ __align__(16) uint8_t lds[];
-  const int e0 = staged_env0(blockIdx.x, ne, n);
-  const int ne_eff = min(ne, n - e0);
-  if (ne_eff <= 0) return;
-  const int64_t rb = K.L.record_bytes;
-  const int tid = threadIdx.x;
-  const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  HeroPre* pre = (HeroPre*)(lds + ne * sbytes);  // [ne]
-  int* best = (int*)(pre + ne);                   // [ne] Stanley target search result
-  CBEV_STAMP(0, 0);
-  // the actions of this workgroup's envs, in flight with the record staging
-  // (wave 0 runs chain A, wave 1 the steering tangent)
-  float ag = 0.f, asa = 0.f, ab = 0.f;
-  if (wave <= 1 && lane < ne_eff) d_decode_action(K, actions, e0 + lane, &ag, &asa, &ab);
-  stage_in(lds, recs, e0, ne_eff, rb, sbytes);
-  __syncthreads();
-  CBEV_STAMP(0, 1);
-  // P1, one lane per env on two waves at once: cos / sin of the yaw (wave 0) and
-  // tan(clip(delta)) (wave 1)
-  if (lane < ne_eff) {
-    const double* hd = (const double*)(lds + lane * sbytes + K.L.hd);
-    if (wave == 0) {
-      pre[lane].cyaw = cos(hd[CBEV_HD_YAW]);
-      pre[lane].syaw = sin(hd[CBEV_HD_YAW]);
-    } else if (wave == 1) {
-      const double max_steer = 30.0 * (CB_PI / 180.0);
-      pre[lane].tdelta = tan(d_clip(d_hero_delta(hd[CBEV_HD_V], asa), -max_steer, max_steer));
-    }
-  }
-  __syncthreads();
-  CBEV_STAMP(3, 0);
-  // P2: Controller.calc_target_index (stanley_controller.py:51-62) on the
-  // pre-update state, over (env, route point) pairs, env k = tid / tpe. The
-  // squared distance is within a few ulp of hypot^2, so only points within
-  // (1 + 1e-14) of the smallest squared distance can hold the hypot minimum;
-  // hypot is evaluated for those (+inf elsewhere) and k's thread then takes the
-  // first minimum, as numpy's argmin does.
-  {
-    const int tpe = 256 / ne, k = tid / tpe, sub = tid - k * tpe;
-    if (k < ne_eff) {
-      const uint8_t* base = lds + k * sbytes;
-      const double* hd = (const double*)(base + K.L.hd);
-      const double* cx = (const double*)(base + K.L.cx);
-      const double* cy = (const double*)(base + K.L.cy);
-      const int nr = ((const int32_t*)(base + K.L.hi))[CBEV_HI_NROUTE];
-      const double fx = hd[CBEV_HD_X] + CB_WHEELBASE * pre[k].cyaw;
-      const double fy = hd[CBEV_HD_Y] + CB_WHEELBASE * pre[k].syaw;
-      double m2 = INFINITY;
-#pragma unroll 4
-      for (int i = sub; i < nr; i += tpe) {
-        const double dx = fx - cx[i], dy = fy - cy[i];
-        const double d2 = dx * dx + dy * dy;
-        m2 = d2 < m2 ? d2 : m2;
-      }
-      for (int o = tpe >> 1; o > 0; o >>= 1) {
-        const double t = __shfl_xor(m2, o, tpe);
-        m2 = t < m2 ? t : m2;
-      }
-      const double lim = m2 * (1.0 + 1e-14);
-      double bd = INFINITY;
-      int bi = 0x7fffffff;
-      for (int i = sub; i < nr; i += tpe) {
-        const double dx = fx - cx[i], dy = fy - cy[i];
-        if (dx * dx + dy * dy <= lim) {
-          const double h = hypot(dx, dy);
-          if (h < bd) {  // first minimum within this thread's (increasing) indices
-            bd = h;
-            bi = i;
-          }
-        }
-      }
-      for (int o = tpe >> 1; o > 0; o >>= 1) {  // smallest hypot, lowest index on ties
-        const double qd = __shfl_xor(bd, o, tpe);
-        const int qi = __shfl_xor(bi, o, tpe);
-        if (qd < bd || (qd == bd && qi < bi)) {
-          bd = qd;
-          bi = qi;
-        }
-      }
-      if (sub == 0) best[k] = bi == 0x7fffffff ? 0 : bi;
-    }
-  }
-  __syncthreads();
-  CBEV_STAMP(3, 1);
-  // A: the scalar chain, one thread per env
-  if (tid < ne_eff) {
-    const float gsb[3] = {ag, asa, ab};
-    hero_env_a(K, bind_rec(lds + tid * sbytes, K.L, K.C), e0 + tid, actions, best[tid], pre[tid], gsb);
-  }
-  __syncthreads();
-  CBEV_STAMP(3, 2);
-  // B: comfort + dist2goal (wave 1) beside the render set-up (wave 2)
-  if (lane < ne_eff) {
-    if (wave == 1) hero_env_comfort(bind_rec(lds + lane * sbytes, K.L, K.C));
-    else if (wave == 2) hero_env_render_setup(K, bind_rec(lds + lane * sbytes, K.L, K.C));
-  }
-  CBEV_STAMP(0, 2);
-  __syncthreads();
-  CBEV_STAMP(3, 3);
-  stage_out(lds, recs, e0, ne_eff, rb, sbytes, 0, (int)K.L.cx);  // HD + HI
-  CBEV_STAMP(0, 3);
-}
-
 // Scripted actors (ActorManager.step_all, actor_manager.py:111-119): one
-// wavefront per env, one lane per actor (vehicles then pedestrians). Runs after
-// k_hero, so the scene clock hd[T] is already advanced.
-// t_ahead = 1: launched before k_step, which advances the scene clock itself,
-// so the actors take hd[T] + dt (the same float64 sum k_step stores).
+// wavefront per env, one lane per actor (vehicles then pedestrians). Launched
+// before k_ego, which advances the scene clock itself (scene.py:91), so the
+// actors take hd[T] + dt (the same float64 sum k_ego stores); nothing the
+// actors read is written by the ego update.
 //
 // Up to 64 actors: Actor.step in three passes over the wave.
 //   1. lane per actor: behaviour, target speed, the frozen-at-route-end test,
@@ -1033,11 +956,8 @@ __device__ __forceinline__ int actor_search(const DRec& r, int nact, uint64_t li
     // pass 1: the smallest squared distance (first index) and the runner-up's
     double m2 = INFINITY, s2 = INFINITY;
     int i2 = 0x7fffffff;
-#ifndef CBEV_ACTOR_SEARCH_UNROLL  // route points per lane with loads in flight
-#define CBEV_ACTOR_SEARCH_UNROLL 8
-#endif
     if (glive) {
-#pragma unroll CBEV_ACTOR_SEARCH_UNROLL
+#pragma unroll 8
       for (int i = sub; i < gn; i += AW) {
         const double dx = gfx - cx[i], dy = gfy - cy[i];
         const double d2 = dx * dx + dy * dy;
@@ -1079,23 +999,19 @@ __device__ __forceinline__ int actor_search(const DRec& r, int nact, uint64_t li
   return best;
 }
 
-// waves per SIMD the register allocation must allow (occupancy vs spills)
-#ifndef CBEV_ACTORS_WAVES
-#define CBEV_ACTORS_WAVES 1
-#endif
 // WIDE: the context's capacities allow more than 64 actors or more than 64
 // actor route points, which take the serial per-lane paths (d_actor_step,
 // d_start_retreat). Contexts within 64 / 64 launch k_actors<false>, which
 // compiles without them: 106 instead of 229 VGPRs, 4 waves per SIMD instead of 2.
 template <bool WIDE>
-__global__ __launch_bounds__(256, CBEV_ACTORS_WAVES) void k_actors(KArgs K, uint8_t* __restrict__ recs, int n, int t_ahead) {
+__global__ __launch_bounds__(256) void k_actors(KArgs K, uint8_t* __restrict__ recs, int n) {
   const int lane = threadIdx.x & 63;
   const int e = xcd_env4_of_wg(blockIdx.x, threadIdx.x >> 6, n);
   if (e >= n) return;
   DRec r = bind_rec(recs + (int64_t)e * K.L.record_bytes, K.L, K.C);
   const int nact = r.hi[CBEV_HI_NACT];
   if (nact == 0) return;
-  const double t = t_ahead ? r.hd[CBEV_HD_T] + CB_DT : r.hd[CBEV_HD_T];
+  const double t = r.hd[CBEV_HD_T] + CB_DT;
   if (WIDE && nact > 64) {
     for (int a = lane; a < nact; a += 64) d_actor_step(r, a, t);
     return;
@@ -1197,7 +1113,7 @@ __global__ __launch_bounds__(256, CBEV_ACTORS_WAVES) void k_actors(KArgs K, uint
 //   CHECK = true: compose clipping (black outside the rotated surface) and the
 //   rotozoom background test (bg outside the source), per pixel.
 template <int G, bool R90, bool CHECK, int NW>
-__device__ __forceinline__ void raster_out_rows(const cbev_params& P, const RotSetup& R, const uint8_t* __restrict__ lds,
+__device__ __forceinline__ void raster_out(const cbev_params& P, const RotSetup& R, const uint8_t* __restrict__ lds,
                                            int shift, uint32_t bg, uint8_t* __restrict__ out, int nout,
                                            int64_t out_stride, int lane, int wave,
                                            const uint32_t* __restrict__ fov) {
@@ -1280,7 +1196,7 @@ __device__ __forceinline__ void raster_out_rows(const cbev_params& P, const RotS
             v = BYTES ? img[byte] : (img[byte] >> nsh) & 15u;
           }
         }
-        acc |= ((CBEV_RASTER_PHASES & 4) ? v : (uint32_t)(lane + b)) << (8 * b);
+        acc |= v << (8 * b);
       }
       w[d] = acc;
       if (!R90) qg += group_step;
@@ -1297,173 +1213,15 @@ __device__ __forceinline__ void raster_out_rows(const cbev_params& P, const RotS
         w[d] = (w[d] & ~fm) | (fm & (CBEV_PX_BLACK * 0x01010101u));
       }
     }
-    if (CBEV_RASTER_PHASES & 8) {
-      for (int k = 0; k < nout; ++k) {
-        uint8_t* ob = out + (int64_t)k * out_stride;
+    for (int k = 0; k < nout; ++k) {
+      uint8_t* ob = out + (int64_t)k * out_stride;
 #pragma unroll
-        for (int d = 0; d < 4; ++d)  // streamed out: keep the L2 for the map and the records
-          __builtin_nontemporal_store(w[d], (uint32_t*)(ob + (vo + (uint32_t)(256 * d))));
-      }
-    } else {
-      if ((w[0] ^ w[1] ^ w[2] ^ w[3]) == 0x7fffffffu) out[vo] = 1;  // keeps the gathers live
+      for (int d = 0; d < 4; ++d)  // streamed out: keep the L2 for the map and the records
+        __builtin_nontemporal_store(w[d], (uint32_t*)(ob + (vo + (uint32_t)(256 * d))));
     }
     pxy += chunk_step;
     sa += chunk_rows * R.vstep;
   }
-}
-
-// Output pass over one wave's chunks of 1024 output pixels (16 / G rows). A
-// chunk is four dword groups; group d covers columns [d S/4, (d+1) S/4) of
-// every row of the chunk: lane l owns the 4 consecutive pixels from column
-// d S/4 + 4 (l % 4G) of row l / 4G, gathers them (one LDS read per pixel, b =
-// 0..3) and stores them as one dword. A gather instruction therefore samples
-// 16 / G rows x 4G pixel blocks rather than one or two whole rows: whatever the
-// rotation, the 32 lanes of an LDS lane group then spread over the banks (the
-// rows of a block land in one dword of the odd-stride image, the blocks of a
-// row step 4 texels along the rotated row); with whole rows per instruction a
-// vertical source direction stepped 4 image rows per lane, i.e. 4 sd = 0 mod 4
-// dwords: 4-way conflicts. Each store instruction writes 4G-dword runs of
-// 16 / G rows; the wave's four groups complete every row of the chunk.
-// Source coordinates are stepped, not recomputed (pygame's rotozoom is affine
-// in the output pixel): per gather one 64-bit add, a 24-bit multiply-add for the
-// LDS byte address, the LDS read, the nibble extract and the pack; rotate90
-// steps an LDS texel address.
-//   CHECK = false: the rotated surface covers the whole output and every output
-//   pixel samples inside the crop (checked once per env at the four corners;
-//   the map is affine) -> no per-pixel tests.
-//   CHECK = true: compose clipping (black outside the rotated surface) and the
-//   rotozoom background test (bg outside the source), per pixel.
-template <int G, bool R90, bool CHECK, int NW>
-__device__ __forceinline__ void raster_out_blocks(const cbev_params& P, const RotSetup& R, const uint8_t* __restrict__ lds,
-                                           int shift, uint32_t bg, uint8_t* __restrict__ out, int nout,
-                                           int64_t out_stride, int lane, int wave,
-                                           const uint32_t* __restrict__ fov) {
-  constexpr int RPC = 16 / G;  // output rows per chunk
-  constexpr int S = 64 * G;    // == P.size
-  constexpr int LPR = 4 * G;   // lanes per output row in one dword group
-  constexpr int GC = S / 4;    // columns per dword group
-  constexpr bool BYTES = raster_bytes(S);
-  const int C = P.crop;
-  const uint32_t vmax = (uint32_t)((C << 16) - 1);
-  const int hero_w = P.hero_w;
-  const int hx0 = P.anchor_x - hero_w / 2, hy0 = P.anchor_y - hero_w / 2;
-  const int lrow = lane / LPR, lcol = 4 * (lane % LPR);
-  const uint32_t hblack = CBEV_PX_BLACK * 0x01010101u;
-  const int r0 = wave * RPC;
-  const int xx0 = lcol - R.rx0, yy0 = r0 + lrow - R.ry0;
-  // lane state at (output row r0 + lrow, column lcol) of this wave's first chunk
-  int sx = R.dx00 + xx0 * R.icos - yy0 * R.isin;  // 16.16 source x (general)
-  int sy = R.dy00 + xx0 * R.isin + yy0 * R.icos;  // 16.16 source y (general)
-  int sa = R.a00 + shift + xx0 * R.ustep + yy0 * R.vstep;  // LDS texel address (rotate90)
-  // the crop's texel offset rides in the integer part of sx, so the LDS byte is
-  // (sy >> 16) * sb + (sx >> 16) (byte image) or (sy >> 16) * sb + (sx >> 17) with
-  // the nibble (sx >> 16) & 1 (nibble image)
-  sx += shift << 16;
-  const uint8_t* img = lds;
-  const uint32_t sb = 4u * (uint32_t)raster_stride_dwords(S, C);  // LDS bytes per crop row
-  const int chunk_rows = NW * RPC;                // the NW output waves interleave chunks
-  const int nchunks = S / RPC;
-  // general path: (sx, sy) packed in one 64-bit value, so one 64-bit add steps
-  // both coordinates (the low word stays in [0, 2^32): no carry crosses over)
-  uint64_t pxy = ((uint64_t)(uint32_t)sy << 32) | (uint32_t)sx;
-  const uint64_t chunk_step =
-      (uint64_t)(((int64_t)(chunk_rows * R.icos) << 32) + (int64_t)(-chunk_rows * R.isin));
-  // one output row down: (dx, dy) += (-isin, icos); one column right: += (icos, isin)
-  const uint64_t group_step = (uint64_t)(((int64_t)(GC * R.isin) << 32) + (int64_t)(GC * R.icos));
-  const uint64_t col_step = (uint64_t)(((int64_t)R.isin << 32) + (int64_t)R.icos);
-  for (int ch = wave, r = r0; ch < nchunks; ch += NW, r += chunk_rows) {
-    const int row = r + lrow;  // this lane's output row
-    // the frame is written through the uniform base `out` plus a per-lane offset
-    const uint32_t vo = (uint32_t)(row * S + lcol);
-    const bool hero_rows = (unsigned)(r + RPC - 1 - hy0) < (unsigned)(RPC - 1 + hero_w);  // chunk meets the hero rows
-    const bool row_ok = !CHECK || (unsigned)(row - R.ry0) < (unsigned)R.ny;  // compose clip (rows)
-    asm volatile("" : "+v"(pxy), "+v"(sa));  // keep the per-gather offsets as scalar adds
-    uint32_t w[4];
-    uint64_t qg = pxy;  // general path: source coordinates of (row, column d GC + lcol)
-#pragma unroll
-    for (int d = 0; d < 4; ++d) {
-      uint32_t acc = 0;
-#pragma unroll
-      for (int b = 0; b < 4; ++b) {
-        uint32_t v;
-        // compose clip (columns): rotated-surface column of this pixel
-        const bool col_ok = !CHECK || (unsigned)(lcol + d * GC + b - R.rx0) < (unsigned)R.nx;
-        if (R90) {
-          const int a = sa + (d * GC + b) * R.ustep;
-          if (CHECK) {
-            const bool ok = col_ok && row_ok;
-            v = ok ? lds_texel<BYTES>(img, ok ? a : 0) : (uint32_t)CBEV_PX_BLACK;
-          } else {
-            v = lds_texel<BYTES>(img, a);
-          }
-        } else {
-          const uint64_t q = b == 0 ? qg : qg + (uint64_t)b * col_step;
-          const uint32_t dx = (uint32_t)q, dy = (uint32_t)(q >> 32);
-          const uint32_t byte = __umul24(dy >> 16, sb) + (BYTES ? (dx >> 16) : (dx >> 17));
-          const uint32_t nsh = BYTES ? 0u : (dx >> 14) & 4u;
-          if (CHECK) {  // bounds on the unshifted source coordinate
-            const int ux = (int)dx - (shift << 16);
-            const bool ok = col_ok && row_ok;
-            const bool in = (uint32_t)ux <= vmax && dy <= vmax;
-            const uint32_t s = BYTES ? img[(in && ok) ? byte : 0u] : (img[(in && ok) ? byte : 0u] >> nsh) & 15u;
-            v = !ok ? (uint32_t)CBEV_PX_BLACK : (in ? s : bg);
-          } else {
-            v = BYTES ? img[byte] : (img[byte] >> nsh) & 15u;
-          }
-        }
-        acc |= ((CBEV_RASTER_PHASES & 4) ? v : (uint32_t)(lane + b)) << (8 * b);
-      }
-      w[d] = acc;
-      if (!R90) qg += group_step;
-    }
-    if (hero_rows && (unsigned)(row - hy0) < (unsigned)hero_w) {  // Hero.draw: black w x w rect at the anchor (hero.py:26-32)
-#pragma unroll
-      for (int d = 0; d < 4; ++d) {
-        uint32_t hm = 0;
-#pragma unroll
-        for (int b = 0; b < 4; ++b)
-          if ((unsigned)(lcol + d * GC + b - hx0) < (unsigned)hero_w) hm |= 0xffu << (8 * b);
-        w[d] = (w[d] & ~hm) | (hm & hblack);
-      }
-    }
-    if (fov) {  // FovRenderer.apply_mask (fov.py:96-99): black corner triangles (uniform branch)
-#pragma unroll
-      for (int d = 0; d < 4; ++d) {
-        const uint32_t fm = fov[(vo + (uint32_t)(d * GC)) >> 2];
-        w[d] = (w[d] & ~fm) | (fm & hblack);
-      }
-    }
-    if (CBEV_RASTER_PHASES & 8) {
-      for (int k = 0; k < nout; ++k) {
-        uint8_t* ob = out + (int64_t)k * out_stride;
-#pragma unroll
-        for (int d = 0; d < 4; ++d)  // streamed out: keep the L2 for the map and the records
-          __builtin_nontemporal_store(w[d], (uint32_t*)(ob + (vo + (uint32_t)(d * GC))));
-      }
-    } else {
-      if ((w[0] ^ w[1] ^ w[2] ^ w[3]) == 0x7fffffffu) out[vo] = 1;  // keeps the gathers live
-    }
-    pxy += chunk_step;
-    sa += chunk_rows * R.vstep;
-  }
-}
-
-// Lane mapping of the output pass: rows (default) or column blocks
-// (CBEV_RASTER_BLOCKMAP=1). The block mapping halves the LDS bank-conflict
-// cycles (3.99 M -> 1.88 M per config-2 launch) but costs 12 % more VALU and
-// 32-byte store runs, and measured 4 % slower (30.2 vs 29.0 us per step raster).
-#ifndef CBEV_RASTER_BLOCKMAP
-#define CBEV_RASTER_BLOCKMAP 0
-#endif
-template <int G, bool R90, bool CHECK, int NW>
-__device__ __forceinline__ void raster_out(const cbev_params& P, const RotSetup& R, const uint8_t* __restrict__ lds,
-                                           int shift, uint32_t bg, uint8_t* __restrict__ out, int nout,
-                                           int64_t out_stride, int lane, int wave,
-                                           const uint32_t* __restrict__ fov) {
-  if (CBEV_RASTER_BLOCKMAP)
-    raster_out_blocks<G, R90, CHECK, NW>(P, R, lds, shift, bg, out, nout, out_stride, lane, wave, fov);
-  else
-    raster_out_rows<G, R90, CHECK, NW>(P, R, lds, shift, bg, out, nout, out_stride, lane, wave, fov);
 }
 
 template <int G, int NW = 4>
@@ -1511,7 +1269,7 @@ __device__ __forceinline__ PaintPre raster_paint_fetch(const DRec& r) {
     q.asz = RAI(r, CBEV_AI_SIZE, k);
   }
   if (k < q.nt) {
-    q.tvis = (r.vis[k >> 5] >> (k & 31)) & 1u;
+    q.tvis = (r.vis_draw[k >> 5] >> (k & 31)) & 1u;
     q.tx = r.cx[k];
     q.ty = r.cy[k];
   }
@@ -1541,7 +1299,7 @@ __device__ __forceinline__ void raster_paint(const KArgs& K, const DRec& r, cons
   const int C = P.crop;
   const int rt = raster_row_texels(P.size, C);  // texels per LDS row
   const int k = threadIdx.x >> 2, tq = threadIdx.x & 3;
-  if (CBEV_RASTER_PHASES & 2) {
+  {
     for (int pass = 0; pass < 2; ++pass) {  // vehicles, then pedestrians
       const int a0 = pass == 0 ? 0 : q.nveh, a1 = pass == 0 ? q.nveh : q.nact;
       if (a1 <= a0) continue;
@@ -1558,7 +1316,7 @@ __device__ __forceinline__ void raster_paint(const KArgs& K, const DRec& r, cons
     if (k < nt && q.tvis)
       paint_rect4<BYTES>(lds, rt, shift, C, P.pad, xmin, ymin, q.tx, q.ty, k < nt - 1 ? 2 : 4, tq, CBEV_PX_ROUTE);
     for (int i = NT / 4 + k; i < nt; i += NT / 4)
-      if ((r.vis[i >> 5] >> (i & 31)) & 1u)
+      if ((r.vis_draw[i >> 5] >> (i & 31)) & 1u)
         paint_rect4<BYTES>(lds, rt, shift, C, P.pad, xmin, ymin, r.cx[i], r.cy[i], i < nt - 1 ? 2 : 4, tq,
                            CBEV_PX_ROUTE);
     __syncthreads();
@@ -1576,13 +1334,9 @@ __device__ __forceinline__ void raster_paint(const KArgs& K, const DRec& r, cons
   }
 }
 
-struct NoSideWork {
-  __device__ void operator()(int) const {}
-};
-
 // One env's render set-up: crop origin, rotation, fast-path flag and the paint
 // inputs. RESET: BaseMap.reset's frame (theta = 0, no actors drawn,
-// world.py:92-100) at the record's pose; otherwise the RS_* ints k_hero wrote.
+// world.py:92-100) at the record's pose; otherwise the RS_* ints k_ego wrote.
 struct RasterJob {
   int xmin, ymin, shift, xa;  // crop origin, its texel offset in the dword-aligned LDS row, packed byte column
   RotSetup R;
@@ -1594,11 +1348,9 @@ template <bool RESET, int G>
 __device__ __forceinline__ void raster_origin(const KArgs& K, const DRec& r, RasterJob& J) {
   if (RESET) {
     d_crop_origin(K.P, r.hd[CBEV_HD_X], r.hd[CBEV_HD_Y], &J.xmin, &J.ymin);
-  } else if (CBEV_RASTER_PHASES & 16) {
+  } else {
     J.xmin = r.hi[CBEV_HI_RS_XMIN];
     J.ymin = r.hi[CBEV_HI_RS_YMIN];
-  } else {  // (phase experiments only) a fixed pose, no record read
-    J.xmin = J.ymin = 1000;
   }
   J.xa = (J.xmin >> 1) & ~3;  // packed byte column (dword aligned)
   J.shift = J.xmin - 2 * J.xa;  // texel offset (0..7)
@@ -1608,20 +1360,19 @@ template <bool RESET, int G>
 __device__ __forceinline__ void raster_rot(const KArgs& K, const DRec& r, RasterJob& J) {
   const cbev_params& P = K.P;
   const int rt = raster_row_texels(64 * G, P.crop);
-  if (RESET || !(CBEV_RASTER_PHASES & 16)) {  // BaseMap.reset: theta 0 -> rotate90 by one turn
+  if (RESET) {  // BaseMap.reset: theta 0 -> rotate90 by one turn
     J.R = rot_setup(P, 90.0f, rt);
-  } else {  // written by k_hero for this step
+  } else {  // written by k_ego for this step
     int32_t* w = (int32_t*)&J.R;
 #pragma unroll
     for (int k = 0; k < CBEV_RS_WORDS; ++k) w[k] = r.hi[CBEV_HI_RS_R90 + k];
   }
-  J.fast = (!RESET && (CBEV_RASTER_PHASES & 16)) ? r.hi[CBEV_HI_RS_FAST] != 0 : raster_fast(P, J.R);
+  J.fast = !RESET ? r.hi[CBEV_HI_RS_FAST] != 0 : raster_fast(P, J.R);
 }
 
 // Crop staging: 16-byte global loads of the nibble-packed map, lane-linear over
 // the window's row chunks (STAGE_U per thread in flight), then dword LDS stores.
-// Split in an issue half (loads into registers) and a commit half (LDS stores)
-// so k_raster can hold the next env's loads in flight across an output pass.
+// Issue half (loads into registers) and commit half (LDS stores).
 #define STAGE_U 5
 struct StageBuf {
   uint4 v[STAGE_U];
@@ -1684,133 +1435,69 @@ __device__ __forceinline__ void stage_commit(const KArgs& K, int q0, const Stage
 }
 template <int G, int NT = 256>
 __device__ __forceinline__ void stage_all(const KArgs& K, const RasterJob& J, uint8_t* __restrict__ lds) {
-  if (CBEV_RASTER_PHASES & 1) {
-    const int total = stage_total<G>(K.P);
-    for (int q0 = 0; q0 < total; q0 += NT * STAGE_U) {
-      StageBuf b;
-      stage_issue<G, NT>(K, J, q0, b);
-      stage_commit<G, NT>(K, q0, b, lds);
-    }
+  const int total = stage_total<G>(K.P);
+  for (int q0 = 0; q0 < total; q0 += NT * STAGE_U) {
+    StageBuf b;
+    stage_issue<G, NT>(K, J, q0, b);
+    stage_commit<G, NT>(K, q0, b, lds);
   }
 }
 
-// NW < NT / 64: waves NW.. run `side(lane)` (k_step: the collision / reward
-// pass) while waves 0..NW-1 write the frame; every other LDS access of `side`
-// must stay outside the crop image.
-template <int G, int NW = 4, class Side = NoSideWork, int NT = 256>
+// rotate (pygame transform.rotate / rotate90) + compose + ego overlay of the
+// painted crop image into `nout` frames out + k*out_stride
+template <int G, int NT = 256>
 __device__ __forceinline__ void raster_emit(const KArgs& K, const RasterJob& J, uint8_t* __restrict__ out, int nout,
-                                            int64_t out_stride, const uint8_t* __restrict__ lds,
-                                            const Side& side = Side()) {
+                                            int64_t out_stride, const uint8_t* __restrict__ lds) {
   constexpr bool BYTES = raster_bytes(64 * G);
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  // ---- rotate (pygame transform.rotate / rotate90) + compose + ego overlay
   const uint32_t bg = lds_texel<BYTES>(lds, J.shift);  // crop top-left pixel after painting
-  if (NW < NT / 64 && wave >= NW) {
-    side(lane);
-  } else if (CBEV_RASTER_PHASES & 32) {
-    raster_out_dispatch<G, NW>(K.P, J.R, J.fast, lds, J.shift, bg, out, nout, out_stride, lane, wave, K.fov);
-  }
+  raster_out_dispatch<G, NT / 64>(K.P, J.R, J.fast, lds, J.shift, bg, out, nout, out_stride, lane, wave, K.fov);
 }
 
-// Render one env's observation (whole 256-thread workgroup). The frame is
-// written to `nout` destinations out + k*out_stride (the frame-stack ring on reset).
-template <bool RESET, int G, int NW = 4, class Side = NoSideWork>
-__device__ __forceinline__ void raster_env(const KArgs& K, const DRec& r, uint8_t* __restrict__ out, int nout,
-                                           int64_t out_stride, uint8_t* __restrict__ lds,
-                                           const Side& side = Side()) {
-  constexpr bool BYTES = raster_bytes(64 * G);
+// BaseMap.reset's observation (theta = 0, nothing painted, world.py:92-100) of
+// one record by a 256-thread workgroup, into `nout` frames out + k*out_stride
+// (every slot of the frame-stack ring on reset).
+template <int G>
+__device__ __forceinline__ void raster_reset_env(const KArgs& K, const DRec& r, uint8_t* __restrict__ out, int nout,
+                                                 int64_t out_stride, uint8_t* __restrict__ lds) {
   RasterJob J;
-  raster_origin<RESET, G>(K, r, J);
-  raster_rot<RESET, G>(K, r, J);
-  J.pq = PaintPre{};
-  if (!RESET && (CBEV_RASTER_PHASES & 2)) J.pq = raster_paint_fetch(r);
+  raster_origin<true, G>(K, r, J);
+  raster_rot<true, G>(K, r, J);
   stage_all<G>(K, J, lds);
   __syncthreads();
-  if (!RESET) {
-    CBEV_STAMP(2, 1);
-    raster_paint<BYTES>(K, r, J.pq, J.xmin, J.ymin, J.shift, lds);
-    CBEV_STAMP(2, 2);
-  }
-  raster_emit<G, NW>(K, J, out, nout, out_stride, lds, side);
+  raster_emit<G>(K, J, out, nout, out_stride, lds);
 }
 
-// G = size / 64 (64-pixel gathers per output row). CBEV_RASTER_NE envs per
-// workgroup (envs g, g + ng, ... of env group g, so env blocks keep their XCD),
-// software-pipelined through one LDS image: the next env's crop loads are
-// issued into registers before this env's output pass and committed to LDS
-// after it, so their L2 latency hides under the frame stores. With 2 envs per
-// workgroup a 4096-env step is one dispatch round of 8 workgroups per CU.
-#ifndef CBEV_RASTER_NE
-#define CBEV_RASTER_NE 1
-#endif
-#ifndef CBEV_RASTER_PREFETCH  // hold the next env's crop loads in registers across the output pass
-#define CBEV_RASTER_PREFETCH 1
-#endif
-#ifndef CBEV_RASTER_WAVES
-#define CBEV_RASTER_WAVES 8
-#endif
-// Threads per k_raster workgroup: 8 waves at S=256, where the 68 KB crop image
+// One env per workgroup (G = size / 64 gathers per output row): crop staging,
+// paint in draw order, output. 8 waves at S=256, where the 68 KB crop image
 // leaves 2 workgroups per CU (4 waves each would leave the SIMDs half empty);
-// 4 waves below, where 8 workgroups share a CU.
-#ifndef CBEV_RASTER_NT256
-#define CBEV_RASTER_NT256 512
-#endif
-__host__ __device__ constexpr int raster_threads(int S) { return S >= 256 ? CBEV_RASTER_NT256 : 256; }
+// 4 waves below, where 8 workgroups share a CU. Measured alternatives (two envs
+// per workgroup with the next env's loads in flight, a persistent grid, a
+// column-block lane mapping, a byte image at S=128) are in DESIGN.md §3.
+__host__ __device__ constexpr int raster_threads(int S) { return S >= 256 ? 512 : 256; }
 
 template <int G>
-__global__ __launch_bounds__(raster_threads(64 * G)) __attribute__((amdgpu_waves_per_eu(CBEV_RASTER_WAVES))) void k_raster(
+__global__ __launch_bounds__(raster_threads(64 * G)) __attribute__((amdgpu_waves_per_eu(8))) void k_raster(
     KArgs K, uint8_t* __restrict__ recs, int n, uint8_t* __restrict__ frames) {
   extern __shared__ __align__(16) uint8_t lds[];
   constexpr bool BYTES = raster_bytes(64 * G);
-  constexpr int NT = raster_threads(64 * G), NW = NT / 64;
-  const int ng = (n + CBEV_RASTER_NE - 1) / CBEV_RASTER_NE;
-  const int g = xcd_env_of_wg(blockIdx.x, ng);
-  if (g >= ng) return;
+  constexpr int NT = raster_threads(64 * G);
+  const int e = xcd_env_of_wg(blockIdx.x, n);
+  if (e >= n) return;
   CBEV_STAMP(2, 0);
   const int64_t SS = (int64_t)K.P.size * K.P.size;
-  const bool one_batch = CBEV_RASTER_PREFETCH && stage_total<G>(K.P) <= NT * STAGE_U;
-  int e = g;
-  DRec r = bind_rec(recs + (int64_t)e * K.L.record_bytes, K.L, K.C);
+  const DRec r = bind_rec(recs + (int64_t)e * K.L.record_bytes, K.L, K.C);
   RasterJob J;
   raster_origin<false, G>(K, r, J);
   raster_rot<false, G>(K, r, J);
-  J.pq = PaintPre{};
-  if (CBEV_RASTER_PHASES & 2) J.pq = raster_paint_fetch(r);
+  J.pq = raster_paint_fetch(r);  // in flight under the staging
   stage_all<G, NT>(K, J, lds);
   __syncthreads();
   CBEV_STAMP(2, 1);
   raster_paint<BYTES, NT>(K, r, J.pq, J.xmin, J.ymin, J.shift, lds);
   CBEV_STAMP(2, 2);
-#pragma unroll
-  for (int k = 0; k < CBEV_RASTER_NE; ++k) {
-    const int en = e + ng;
-    const bool more = CBEV_RASTER_NE > 1 && k + 1 < CBEV_RASTER_NE && en < n;
-    DRec rn;
-    RasterJob Jn;
-    StageBuf b;
-    if (more) {  // the next env's crop loads, in flight across this output pass
-      rn = bind_rec(recs + (int64_t)en * K.L.record_bytes, K.L, K.C);
-      raster_origin<false, G>(K, rn, Jn);
-      if (one_batch && (CBEV_RASTER_PHASES & 1)) stage_issue<G, NT>(K, Jn, 0, b);
-    }
-    raster_emit<G, NW, NoSideWork, NT>(K, J, frames + (int64_t)e * SS, 1, 0, lds);
-    if (!more) break;
-    raster_rot<false, G>(K, rn, Jn);
-    Jn.pq = PaintPre{};
-    if (CBEV_RASTER_PHASES & 2) Jn.pq = raster_paint_fetch(rn);
-    __syncthreads();  // every wave is done reading this env's image
-    if (one_batch) {
-      if (CBEV_RASTER_PHASES & 1) stage_commit<G, NT>(K, 0, b, lds);
-    } else {
-      stage_all<G, NT>(K, Jn, lds);
-    }
-    __syncthreads();
-    raster_paint<BYTES, NT>(K, rn, Jn.pq, Jn.xmin, Jn.ymin, Jn.shift, lds);
-    e = en;
-    r = rn;
-    J = Jn;
-  }
+  raster_emit<G, NT>(K, J, frames + (int64_t)e * SS, 1, 0, lds);
   CBEV_STAMP(2, 3);
 }
 
@@ -1819,10 +1506,8 @@ __global__ __launch_bounds__(raster_threads(64 * G)) __attribute__((amdgpu_waves
 // every slot of the frame-stack ring (FrameStackObservation padding "reset").
 // The frame is rendered from the bank record itself, so no other workgroup's
 // stores need to be visible.
-#define RESET_WGS 1024  // multiple of 8: keeps xcd_env_of_wg's XCD placement
-#ifndef CBEV_RESET_MASKED_WGS  // k_reset_copy grid for masked resets (multiple of 8)
-#define CBEV_RESET_MASKED_WGS 1024
-#endif
+#define RESET_WGS 1024  // multiple of 8: keeps xcd_env_of_wg's XCD placement; also k_reset_copy's grid
+                        // for masked resets (1024 measured best of 128-4096)
 
 template <int G>
 __global__ __launch_bounds__(256) void k_reset(KArgs K, uint8_t* __restrict__ recs, int n,
@@ -1855,7 +1540,7 @@ __global__ __launch_bounds__(256) void k_reset(KArgs K, uint8_t* __restrict__ re
         for (int64_t i = threadIdx.x; i < rb / 16; i += 256) d4[i] = s4[i];
       }
       DRec r = bind_rec((uint8_t*)src, K.L, K.C);  // read-only use below
-      raster_env<true, G>(K, r, ring + (int64_t)e * SS, n_frames, (int64_t)n * SS, lds);
+      raster_reset_env<G>(K, r, ring + (int64_t)e * SS, n_frames, (int64_t)n * SS, lds);
       __syncthreads();  // the LDS image is reused by the next env
     }
   }
@@ -1871,7 +1556,7 @@ __global__ __launch_bounds__(256) void k_bank_frames(KArgs K, const uint8_t* __r
   const int64_t SS = (int64_t)K.P.size * K.P.size;
   for (int b = blockIdx.x; b < n_bank; b += gridDim.x) {
     DRec r = bind_rec((uint8_t*)bank + (int64_t)b * K.L.record_bytes, K.L, K.C);
-    raster_env<true, G>(K, r, frames + b * SS, 1, 0, lds);
+    raster_reset_env<G>(K, r, frames + b * SS, 1, 0, lds);
     __syncthreads();
   }
 }
@@ -1939,7 +1624,7 @@ __global__ __launch_bounds__(256) void k_reset_copy(KArgs K, uint8_t* __restrict
   }
 }
 
-// ============================================================== k_collide
+// ============================================================== collision / reward (k_ego S5-S6)
 // squared distance from (x, y) to raw-route segment i (carl_reward_fn.py:36-48)
 __device__ __forceinline__ double d_seg_dist2(const DRec& r, int i, double x, double y) {
   const int abx_i = r.raw_x[i + 1] - r.raw_x[i], aby_i = r.raw_y[i + 1] - r.raw_y[i];
@@ -1959,10 +1644,6 @@ __device__ __forceinline__ double d_carl_arc(const DRec& r, int i, double x, dou
   return r.raw_cum[i] + tt * sqrt((double)(abx_i * abx_i + aby_i * aby_i));
 }
 
-// Loop mask for performance experiments: 1 target loop, 2 route-progress loop.
-#ifndef CBEV_COLLIDE_PHASES
-#define CBEV_COLLIDE_PHASES 3
-#endif
 // signed distance to waypoint segment i (control/utils.py:165-197)
 __device__ __forceinline__ double d_lateral_seg(double px, double py, const double* wx, const double* wy, int i) {
   double abx = wx[i + 1] - wx[i], aby = wy[i + 1] - wy[i];
@@ -1990,7 +1671,7 @@ __device__ __forceinline__ int d_next_wps(int tidx, int nt) {
   return wend > tidx ? wend - tidx : 0;
 }
 
-// Per-env scratch of k_collide's cooperative pre-pass (LDS, after the staged
+// Per-env scratch of k_ego's cooperative collision pre-pass (LDS, after the staged
 // records): the element loops (raw-route segments, targets, actors) run over all
 // 256 threads of the workgroup as (env, element) pairs; the per-env thread then
 // only reduces in the reference's order.
@@ -2020,7 +1701,7 @@ struct CollPre {  // one env's reduced pre-pass results, as seen by collide_env
   double d2r;                   // lateral_error over next_wps(5)
 };
 
-// k_collide: reduce one env's scratch arrays in the reference's loop order
+// reduce one env's scratch arrays in the reference's loop order
 __device__ __forceinline__ CollPre coll_reduce_serial(const uint8_t* sk, const CollScratchLayout& SL, int nact,
                                                       int nraw) {
   CollPre p;
@@ -2066,7 +1747,7 @@ __device__ __forceinline__ void collide_env(const KArgs& K, DRec r, int e, const
 
   // ---- collisions (scene.py:110-140): hero rect vs vehicles, pedestrians, visible
   // targets; the last hit in iteration order (vehicles, pedestrians, then targets)
-  // wins; every visible target hit is consumed (rect tests in k_collide's pre-pass)
+  // wins; every visible target hit is consumed (rect tests in k_ego's pre-pass)
   CBEV_STAMP(4, 0);
   const int nact = hi[CBEV_HI_NACT];
   const int nt = hi[CBEV_HI_NROUTE];
@@ -2277,49 +1958,152 @@ __device__ __forceinline__ void collide_env(const KArgs& K, DRec r, int e, const
   CBEV_STAMP(4, 3);
 }
 
-__global__ __launch_bounds__(256) void k_collide(KArgs K, uint8_t* __restrict__ recs, int n,
-                                                 double* __restrict__ reward_out, uint8_t* __restrict__ term_out,
-                                                 uint8_t* __restrict__ trunc_out, int32_t* __restrict__ cause_out,
-                                                 float* __restrict__ info_out, int ne, int sbytes) {
-  const int64_t rb = K.L.record_bytes;
+// ============================================================== k_ego
+// The ego half of CarlaBEV.step() (scene.py:90-140, carlabev.py:159-185) for
+// `ne` envs per 256-thread workgroup, in one launch after k_actors and before
+// k_raster:
+//   S0  actions decoded; HD, HI, cx, cy, raw_x, raw_y and the vis words of the
+//       ne records staged into LDS (ego_stage_in)
+//   S1  cos / sin of the yaw (wave 0) beside tan(clip(delta)) (wave 1)
+//   S2  Controller.calc_target_index over (env, route point) pairs: squared
+//       distances, then hypot for the candidates within (1 + 1e-14) of the
+//       smallest, first minimum (stanley_controller.py:51-62)
+//   S3  the ego chain, one thread per env (BaseAgent.physics_step, hero.py:88-138)
+//   S4  comfort + dist2goal (wave 1) | render set-up of this step's observation
+//       (wave 2) | collision prologue (wave 0): ego tile load, hero rect, and the
+//       vis words the observation will draw (vis_draw: this step's render runs
+//       before its collision check, scene.py:93-95 vs 110-140)
+//   S5  collision / reward element loops over (env, element) pairs: raw-route
+//       segments and lateral error, visible targets, vehicles / pedestrians
+//   S6  the collision + reward + termination chain, one thread per env
+//       (collide_env)
+//   S7  HD, HI and the vis group back to the records
+// k_raster reads only what this kernel wrote (RS_* set-up, poses, vis_draw),
+// so collision no longer has to wait for the frame.
+__global__ __launch_bounds__(256) void k_ego(KArgs K, uint8_t* __restrict__ recs, int n,
+                                             const void* __restrict__ actions, double* __restrict__ reward_out,
+                                             uint8_t* __restrict__ term_out, uint8_t* __restrict__ trunc_out,
+                                             int32_t* __restrict__ cause_out, float* __restrict__ info_out, int ne) {
   extern __shared__ __align__(16) uint8_t lds[];
   const int e0 = staged_env0(blockIdx.x, ne, n);
   const int ne_eff = min(ne, n - e0);
   if (ne_eff <= 0) return;
   const cbev_params& P = K.P;
+  const EgoPack pk = ego_pack(K.L);
   const CollScratchLayout SL = coll_scratch_layout(K.C, K.L.vis_words);
-  uint8_t* scr = lds + ne * sbytes;
+  const int64_t rb = K.L.record_bytes;
+  uint8_t* scr = lds + ne * pk.bytes;          // [ne] collision scratch
+  HeroPre* pre = (HeroPre*)(scr + ne * SL.bytes);  // [ne]
+  int* best = (int*)(pre + ne);                   // [ne] target search result
   const int tid = threadIdx.x;
-  CBEV_STAMP(1, 0);
-  stage_in(lds, recs, e0, ne_eff, rb, sbytes);
+  const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  auto rec = [&](int k) { return bind_ego(lds + k * pk.bytes, recs + (int64_t)(e0 + k) * rb, K, pk); };
+  CBEV_STAMP(0, 0);
+  // S0 (wave 0 runs the chain, wave 1 the steering tangent)
+  float ag = 0.f, asa = 0.f, ab = 0.f;
+  if (wave <= 1 && lane < ne_eff) d_decode_action(K, actions, e0 + lane, &ag, &asa, &ab);
+  ego_stage_in(lds, recs, e0, ne_eff, K, pk);
   __syncthreads();
-  CBEV_STAMP(1, 1);
-  const int hw = P.hero_w;
-  // per-env prologue: hero rect, counters; the ego tile's map load
-  // (world.py:159-165) stays in flight through the pre-pass
-  int tile = 0;
-  if (tid < ne_eff) {
-    const double* hd = (const double*)(lds + tid * sbytes + K.L.hd);
-    const int tx = (int)d_clip(rint(hd[CBEV_HD_X]), 0, P.map_w - 1), ty = (int)d_clip(rint(hd[CBEV_HD_Y]), 0, P.map_h - 1);
-    tile = d_map_texel(K, tx + P.pad, ty + P.pad);
-    int* I = (int*)(scr + tid * SL.bytes + SL.ints);
-    I[CS_TGT_LAST] = -1;
-    I[CS_ACT_LAST] = -1;
-    I[CS_NAS] = 0;
-    I[3] = d_rect_lo(hd[CBEV_HD_X], P.pad, hw);
-    I[4] = d_rect_lo(hd[CBEV_HD_Y], P.pad, hw);
-    uint32_t* hitw = (uint32_t*)(scr + tid * SL.bytes + SL.hitw);
-    for (int w = 0; w < K.L.vis_words; ++w) hitw[w] = 0;
+  CBEV_STAMP(0, 1);
+  // S1
+  if (lane < ne_eff) {
+    const double* hd = (const double*)(lds + lane * pk.bytes + K.L.hd);
+    if (wave == 0) {
+      pre[lane].cyaw = cos(hd[CBEV_HD_YAW]);
+      pre[lane].syaw = sin(hd[CBEV_HD_YAW]);
+    } else if (wave == 1) {
+      const double max_steer = 30.0 * (CB_PI / 180.0);
+      pre[lane].tdelta = tan(d_clip(d_hero_delta(hd[CBEV_HD_V], asa), -max_steer, max_steer));
+    }
   }
   __syncthreads();
-  // ---- cooperative pre-pass over (env, element) pairs
-  CBEV_STAMP(5, 0);
+  // S2
   {
-    const int A = K.C.actor_cap;
-    // (env k, element i) pairs: env k = tid / tpe, elements sub, sub + tpe, ...
     const int tpe = 256 / ne, k = tid / tpe, sub = tid - k * tpe;
     if (k < ne_eff) {
-      DRec r = bind_rec(lds + k * sbytes, K.L, K.C);
+      const uint8_t* base = lds + k * pk.bytes;
+      const double* hd = (const double*)(base + K.L.hd);
+      const double* cx = (const double*)(base + K.L.cx);
+      const double* cy = (const double*)(base + K.L.cy);
+      const int nr = ((const int32_t*)(base + K.L.hi))[CBEV_HI_NROUTE];
+      const double fx = hd[CBEV_HD_X] + CB_WHEELBASE * pre[k].cyaw;
+      const double fy = hd[CBEV_HD_Y] + CB_WHEELBASE * pre[k].syaw;
+      double m2 = INFINITY;
+#pragma unroll 4
+      for (int i = sub; i < nr; i += tpe) {
+        const double dx = fx - cx[i], dy = fy - cy[i];
+        const double d2 = dx * dx + dy * dy;
+        m2 = d2 < m2 ? d2 : m2;
+      }
+      for (int o = tpe >> 1; o > 0; o >>= 1) {
+        const double t = __shfl_xor(m2, o, tpe);
+        m2 = t < m2 ? t : m2;
+      }
+      const double lim = m2 * (1.0 + 1e-14);
+      double bd = INFINITY;
+      int bi = 0x7fffffff;
+      for (int i = sub; i < nr; i += tpe) {
+        const double dx = fx - cx[i], dy = fy - cy[i];
+        if (dx * dx + dy * dy <= lim) {
+          const double h = hypot(dx, dy);
+          if (h < bd) {  // first minimum within this thread's (increasing) indices
+            bd = h;
+            bi = i;
+          }
+        }
+      }
+      for (int o = tpe >> 1; o > 0; o >>= 1) {  // smallest hypot, lowest index on ties
+        const double qd = __shfl_xor(bd, o, tpe);
+        const int qi = __shfl_xor(bi, o, tpe);
+        if (qd < bd || (qd == bd && qi < bi)) {
+          bd = qd;
+          bi = qi;
+        }
+      }
+      if (sub == 0) best[k] = bi == 0x7fffffff ? 0 : bi;
+    }
+  }
+  __syncthreads();
+  CBEV_STAMP(0, 2);
+  // S3
+  if (tid < ne_eff) {
+    const float gsb[3] = {ag, asa, ab};
+    hero_env_a(K, rec(tid), e0 + tid, actions, best[tid], pre[tid], gsb);
+  }
+  __syncthreads();
+  // S4
+  if (lane < ne_eff) {
+    if (wave == 1) {
+      hero_env_comfort(rec(lane));
+    } else if (wave == 2) {
+      hero_env_render_setup(K, rec(lane));
+    } else if (wave == 0) {
+      const DRec r = rec(lane);
+      const double x = r.hd[CBEV_HD_X], y = r.hd[CBEV_HD_Y];
+      const int tx = (int)d_clip(rint(x), 0, P.map_w - 1), ty = (int)d_clip(rint(y), 0, P.map_h - 1);
+      const int tile = d_map_texel(K, tx + P.pad, ty + P.pad);  // world.py:159-165
+      int* I = (int*)(scr + lane * SL.bytes + SL.ints);
+      I[CS_TGT_LAST] = -1;
+      I[CS_ACT_LAST] = -1;
+      I[CS_NAS] = 0;
+      I[3] = d_rect_lo(x, P.pad, P.hero_w);
+      I[4] = d_rect_lo(y, P.pad, P.hero_w);
+      uint32_t* hitw = (uint32_t*)(scr + lane * SL.bytes + SL.hitw);
+      for (int w = 0; w < K.L.vis_words; ++w) {
+        hitw[w] = 0;
+        r.vis_draw[w] = r.vis[w];
+      }
+      I[CS_TILE] = tile;
+    }
+  }
+  __syncthreads();
+  CBEV_STAMP(0, 3);
+  // S5 (env k, element i) pairs: env k = tid / tpe, elements sub, sub + tpe, ...
+  {
+    const int hw = P.hero_w;
+    const int tpe = 256 / ne, k = tid / tpe, sub = tid - k * tpe;
+    if (k < ne_eff) {
+      const DRec r = rec(k);
       uint8_t* sk = scr + k * SL.bytes;
       const double x = r.hd[CBEV_HD_X], y = r.hd[CBEV_HD_Y];
       // raw-route segments (carl_reward_fn.py:36-48): first strict arg-min over the
@@ -2330,7 +2114,7 @@ __global__ __launch_bounds__(256) void k_collide(KArgs K, uint8_t* __restrict__ 
       double bd = INFINITY;
       int bi = 0x7fffffff;
 #pragma unroll 4
-      for (int i = sub; (CBEV_COLLIDE_PHASES & 2) && i < nseg; i += tpe) {
+      for (int i = sub; i < nseg; i += tpe) {
         const double d = sqrt(d_seg_dist2(r, i, x, y));
         if (d < bd) {  // NaN never wins
           bd = d;
@@ -2372,7 +2156,6 @@ __global__ __launch_bounds__(256) void k_collide(KArgs K, uint8_t* __restrict__ 
         red[2] = le;
         ((int*)(sk + SL.ints))[CS_BSEG] = any ? bi : 0;
       }
-      CBEV_STAMP(5, 1);
       // visible targets vs the hero rect (target.py:37-44)
       int* I = (int*)(sk + SL.ints);
       const int hrx = I[3], hry = I[4];
@@ -2388,12 +2171,13 @@ __global__ __launch_bounds__(256) void k_collide(KArgs K, uint8_t* __restrict__ 
         }
       }
     }
-    CBEV_STAMP(5, 2);
-    // vehicles / pedestrians: rect hit, actors_state entry and both TTCs (scene.py:110-140,
+    // vehicles / pedestrians (fields read from HBM, field-major over the actor
+    // slots): rect hit, actors_state entry and both TTCs (scene.py:110-140,
     // reward_signals.py:15-94)
+    const int A = K.C.actor_cap;
     for (int q = tid; q < ne_eff * A; q += 256) {
       const int k = q / A, a = q - k * A;
-      DRec r = bind_rec(lds + k * sbytes, K.L, K.C);
+      const DRec r = rec(k);
       if (a >= r.hi[CBEV_HI_NACT]) continue;
       int* I = (int*)(scr + k * SL.bytes + SL.ints);
       const int hrx = I[3], hry = I[4];
@@ -2432,313 +2216,21 @@ __global__ __launch_bounds__(256) void k_collide(KArgs K, uint8_t* __restrict__ 
       ((double*)(scr + k * SL.bytes + SL.ttcs))[a] = ts;
     }
   }
-  if (tid < ne_eff) ((int*)(scr + tid * SL.bytes + SL.ints))[CS_TILE] = tile;
   __syncthreads();
-  CBEV_STAMP(5, 3);
+  CBEV_STAMP(1, 0);
+  // S6
   if (tid < ne_eff) {
-    const DRec rr = bind_rec(lds + tid * sbytes, K.L, K.C);
-    const CollPre pre = coll_reduce_serial(scr + tid * SL.bytes, SL, rr.hi[CBEV_HI_NACT], rr.hi[CBEV_HI_NRAW]);
-    collide_env(K, rr, e0 + tid, pre, reward_out, term_out, trunc_out, cause_out, info_out);
+    const DRec r = rec(tid);
+    const CollPre cp = coll_reduce_serial(scr + tid * SL.bytes, SL, r.hi[CBEV_HI_NACT], r.hi[CBEV_HI_NRAW]);
+    collide_env(K, r, e0 + tid, cp, reward_out, term_out, trunc_out, cause_out, info_out);
   }
+  __syncthreads();
+  CBEV_STAMP(1, 1);
+  // S7
+  ego_stage_out(lds, recs, e0, ne_eff, K, pk);
   CBEV_STAMP(1, 2);
-  __syncthreads();
-  stage_out(lds, recs, e0, ne_eff, rb, sbytes, 0, (int)K.L.cx);                                // HD + HI
-  stage_out(lds, recs, e0, ne_eff, rb, sbytes, (int)K.L.vis, (4 * K.L.vis_words + 15) & ~15);  // target visibility
-  CBEV_STAMP(1, 3);
 }
 
-// ============================================================== k_step (fused step)
-// One 256-thread workgroup runs the whole CarlaBEV.step() of NE envs (after
-// the scripted actors: k_actors is launched before it when the record has
-// actor slots): ego updates, render set-ups, each env's crop staging + paint +
-// frame, and the collision / reward pass.
-//
-// A float64 scalar chain costs a wavefront instruction per step whether one
-// lane or 64 run it, so the chains of the NE envs run side by side in lanes
-// 0..NE-1 (ego) and in lane groups of 64/NE (collision), and with NE = 2 the
-// 2048 workgroups of 4096 envs are all resident at once (8 per CU), so each
-// workgroup's chain latency overlaps the other seven's staging and stores.
-//   S0  HD + HI of the NE records -> LDS (the chains read and write there);
-//       actions prefetched
-//   S1  cos(yaw) (wave 0) | tan(clip(delta)) (wave 1) | sin(yaw) (wave 2)
-//   S2  ego chain A (wave 0) | Stanley target search (wave 1, 64/NE lanes per
-//       env over the route points, first arg-min by group reduction)
-//   S3  render set-up (wave 0) | comfort + dist2goal (wave 1)
-//   S4  per env: raster_env (crop staging, paint, output); for the last env the
-//       output runs on waves 0-2 beside collide_group for all NE envs (wave 3)
-//   S5  HD + HI back to the records
-// Reference: Scene._scene_step (scene.py:90-98), hero.py:88-187,
-// world.py:137-165, fov.py:70-99, scene.py:110-140, carl_reward_fn.py:149-341,
-// reward.py:80-278, stats.py:30-56, carlabev.py:177-185.
-#ifndef CBEV_STEP_NE
-#define CBEV_STEP_NE 2
-#endif
-
-// LDS of k_step: crop image | NE x (HD + HI) | NE x 8 doubles of ego pre-computation | NE x hit words
-__host__ __device__ __forceinline__ int step_img_bytes(int S, int C) { return (raster_image_bytes(S, C) + 15) & ~15; }
-__host__ __device__ __forceinline__ int step_hw_bytes(const cbev_layout& L) { return (4 * L.vis_words + 15) & ~15; }
-__host__ __device__ __forceinline__ int step_lds_bytes(int S, int C, const cbev_layout& L, int ne) {
-  return step_img_bytes(S, C) + ne * ((int)(L.cx - L.hd) + 64 + step_hw_bytes(L));
-}
-
-// Scene.collision_check + the CaRL / shaping reward pass of one env on a group
-// of W lanes (sub = lane within the group): element loops over the lanes
-// (raw-route segments, visible targets, actors), reduced with the reference's
-// order semantics (first strict arg-min, last hit in draw order, minimum TTC),
-// then collide_env's scalar chain on the group's first lane.
-template <int W>
-__device__ __forceinline__ void collide_group(const KArgs& K, const DRec& r, int e, int sub, uint32_t* hitw,
-                                              double* __restrict__ reward_out, uint8_t* __restrict__ term_out,
-                                              uint8_t* __restrict__ trunc_out, int32_t* __restrict__ cause_out,
-                                              float* __restrict__ info_out) {
-  const cbev_params& P = K.P;
-  const int hw = P.hero_w;
-  const int gshift = (threadIdx.x & 63) & ~(W - 1);  // this group's first lane
-  const double x = r.hd[CBEV_HD_X], y = r.hd[CBEV_HD_Y], yaw = r.hd[CBEV_HD_YAW], v = r.hd[CBEV_HD_V];
-  const int hrx = d_rect_lo(x, P.pad, hw), hry = d_rect_lo(y, P.pad, hw);
-  // raw-route segments (carl_reward_fn.py:36-48): lane-local first strict minimum
-  // in increasing index order, then the lexicographic (distance, index) minimum
-  const int nseg = r.hi[CBEV_HI_NRAW] - 1;
-  double bd = INFINITY;
-  int bi = 0x7fffffff;
-  for (int i = sub; (CBEV_COLLIDE_PHASES & 2) && i < nseg; i += W) {
-    const double d = sqrt(d_seg_dist2(r, i, x, y));
-    if (d < bd) {  // NaN never wins, as in the serial loop
-      bd = d;
-      bi = i;
-    }
-  }
-  group_argmin<W>(bd, bi);
-  // visible targets vs the hero rect (target.py:37-44); every hit is consumed
-  for (int w = sub; w < K.L.vis_words; w += W) hitw[w] = 0u;
-  const int nt = r.hi[CBEV_HI_NROUTE];
-  int tgt_last = -1;
-  for (int b0 = 0; b0 < nt; b0 += W) {
-    const int i = b0 + sub;
-    bool hit = false;
-    if (i < nt && ((r.vis[i >> 5] >> (i & 31)) & 1u)) {
-      const int sz = (i < nt - 1) ? 2 : 4;
-      const int trx = d_rect_lo(r.cx[i], P.pad, sz), try_ = d_rect_lo(r.cy[i], P.pad, sz);
-      hit = hrx < trx + sz && hry < try_ + sz && hrx + hw > trx && hry + hw > try_;
-    }
-    uint64_t m = __ballot(hit) >> gshift;  // this group's W bits: target b0 + b at bit b
-    if (W < 64) m &= (1ull << W) - 1;
-    if (sub == 0) {
-      if (W == 64) {
-        hitw[b0 >> 5] = (uint32_t)m;
-        if ((b0 >> 5) + 1 < K.L.vis_words) hitw[(b0 >> 5) + 1] = (uint32_t)(m >> 32);
-      } else {
-        hitw[b0 >> 5] |= (uint32_t)m << (b0 & 31);
-      }
-    }
-    if (m) tgt_last = b0 + 63 - __builtin_clzll(m);
-  }
-  // vehicles / pedestrians: rect hit, actors_state entry and both TTCs
-  // (scene.py:110-140, reward_signals.py:15-94)
-  const int nact = r.hi[CBEV_HI_NACT];
-  int act_last = -1, nas = 0;
-  double tcm = INFINITY, tsm = INFINITY;
-  for (int a = sub; a < nact; a += W) {
-    const int sz = RAI(r, CBEV_AI_SIZE, a);
-    const double ax = RAD(r, CBEV_AD_X, a), ay = RAD(r, CBEV_AD_Y, a);
-    const int arx = d_rect_lo(ax, P.pad, sz), ary = d_rect_lo(ay, P.pad, sz);
-    if (hw > 0 && sz > 0 && hrx < arx + sz && hry < ary + sz && hrx + hw > arx && hry + hw > ary) act_last = a;
-    const int ddx = (hrx + hw / 2) - (arx + sz / 2), ddy = (hry + hw / 2) - (ary + sz / 2);
-    const double dist = hypot((double)ddx, (double)ddy);
-    if (fabs(dist) < P.collide_min_dist) {
-      ++nas;
-      const double hx_m = x * CB_MPP, hy_m = y * CB_MPP, hv_m = v * CB_MPP;
-      const double hvx_m = hv_m * cos(yaw), hvy_m = hv_m * sin(yaw);
-      const double hvx = v * cos(yaw), hvy = v * sin(yaw);
-      const double av = RAD(r, CBEV_AD_V, a), ayaw = RAD(r, CBEV_AD_YAW, a);
-      const double avx = av * cos(ayaw), avy = av * sin(ayaw);
-      {  // compute_ttc_raw (reward_signals.py:46-94)
-        double rx_ = ax * CB_MPP - hx_m, ry_ = ay * CB_MPP - hy_m;
-        double rvx = avx * CB_MPP - hvx_m, rvy = avy * CB_MPP - hvy_m;
-        double nrm = sqrt(rx_ * rx_ + ry_ * ry_);
-        double rel = (rvx * rx_ + rvy * ry_) / (nrm + 1e-6);
-        if (!(rel >= 0)) {
-          const double tc = fabs(nrm / rel);
-          tcm = tc < tcm ? tc : tcm;
-        }
-      }
-      {  // compute_ttc (reward_signals.py:15-42)
-        double rx_ = ax - x, ry_ = ay - y;
-        double rvx = avx - hvx, rvy = avy - hvy;
-        double nrm = sqrt(rx_ * rx_ + ry_ * ry_);
-        double rel = (rvx * rx_ + rvy * ry_) / (nrm + 1e-6);
-        if (!(rel >= 0)) {
-          const double ts = fabs(nrm / rel);
-          tsm = ts < tsm ? ts : tsm;
-        }
-      }
-    }
-  }
-  act_last = group_max_i<W>(act_last);
-  nas = group_sum_i<W>(nas);
-  tcm = group_min<W>(tcm);
-  tsm = group_min<W>(tsm);
-  if (sub == 0) {
-    CollPre p;
-    p.tgt_last = tgt_last;
-    p.act_last = act_last;
-    p.nas = nas;
-    p.hitw = hitw;
-    p.ttc_carl = tcm;
-    p.ttc_sh = tsm;
-    p.bdist = bd < 1e9 ? bd : 1e9;
-    p.bseg = bd < 1e9 ? bi : 0;
-    p.tile = -1;
-    p.have_sd = 0;
-    p.s_t = p.d2r = 0.0;
-    collide_env(K, r, e, p, reward_out, term_out, trunc_out, cause_out, info_out);
-  }
-}
-
-// waves per SIMD the register allocation must allow (8: every workgroup the
-// LDS admits can be resident)
-#ifndef CBEV_STEP_WAVES
-#define CBEV_STEP_WAVES 8
-#endif
-template <int G, int NE>
-__global__ __launch_bounds__(256, CBEV_STEP_WAVES) void k_step(KArgs K, uint8_t* __restrict__ recs, int n,
-                                                                const void* __restrict__ actions,
-                                                                uint8_t* __restrict__ frames,
-                                                                double* __restrict__ reward_out,
-                                                                uint8_t* __restrict__ term_out,
-                                                                uint8_t* __restrict__ trunc_out,
-                                                                int32_t* __restrict__ cause_out,
-                                                                float* __restrict__ info_out) {
-  extern __shared__ __align__(16) uint8_t lds[];
-  constexpr int W = 64 / NE;  // collision lanes per env
-  const int npairs = (n + NE - 1) / NE;
-  const int e0 = NE * xcd_env_of_wg(blockIdx.x, npairs);
-  if (e0 >= n) return;
-  const int ne = min(NE, n - e0);
-  const int hh = (int)(K.L.cx - K.L.hd);  // HD + HI bytes (64-byte aligned groups)
-  const int hwb = step_hw_bytes(K.L);
-  uint8_t* lhh = lds + step_img_bytes(64 * G, K.P.crop);  // [NE][hh]
-  double* misc = (double*)(lhh + NE * hh);               // [NE][8]: cos yaw, sin yaw, tan delta, front axle x, y
-  uint8_t* hitb = (uint8_t*)(misc + 8 * NE);             // [NE][hwb]
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int64_t rb = K.L.record_bytes;
-  auto rec_of = [&](int k) {
-    DRec r = bind_rec(recs + (int64_t)(e0 + k) * rb, K.L, K.C);
-    r.hd = (double*)(lhh + k * hh);
-    r.hi = (int32_t*)(lhh + k * hh + (K.L.hi - K.L.hd));
-    return r;
-  };
-  CBEV_STAMP(2, 0);
-  // S0
-  float g = 0.f, sa = 0.f, b = 0.f;
-  if (wave <= 1 && lane < ne) d_decode_action(K, actions, e0 + lane, &g, &sa, &b);  // in flight during S0
-  {
-    const int q16 = hh / 16;
-    for (int q = tid; q < ne * q16; q += 256) {
-      const int k = q / q16, c = q - k * q16;
-      ((uint4*)(lhh + k * hh))[c] = ((const uint4*)(recs + (int64_t)(e0 + k) * rb + K.L.hd))[c];
-    }
-  }
-  __syncthreads();
-  CBEV_STAMP(3, 0);
-  // S1: the pre-update trig of State.update and the front axle of calc_target_index
-  if (lane < ne) {
-    const DRec r = rec_of(lane);
-    double* m = misc + 8 * lane;
-    if (wave == 0) {
-      const double c = cos(r.hd[CBEV_HD_YAW]);
-      m[0] = c;
-      m[3] = r.hd[CBEV_HD_X] + CB_WHEELBASE * c;
-    } else if (wave == 1) {
-      const double max_steer = 30.0 * (CB_PI / 180.0);
-      m[2] = tan(d_clip(d_hero_delta(r.hd[CBEV_HD_V], sa), -max_steer, max_steer));
-    } else if (wave == 2) {
-      const double sn = sin(r.hd[CBEV_HD_YAW]);
-      m[1] = sn;
-      m[4] = r.hd[CBEV_HD_Y] + CB_WHEELBASE * sn;
-    }
-  }
-  __syncthreads();
-  CBEV_STAMP(3, 1);
-  // S2
-  if (wave == 0) {
-    if (lane < ne) {
-      const double* m = misc + 8 * lane;
-      HeroPre hp;
-      hp.cyaw = m[0];
-      hp.syaw = m[1];
-      hp.tdelta = m[2];
-      const float gsb[3] = {g, sa, b};
-      hero_env_a(K, rec_of(lane), e0 + lane, actions, -1, hp, gsb);
-    }
-  } else if (wave == 1) {
-    // Controller.calc_target_index (stanley_controller.py:51-62), first arg-min of
-    // hypot: squared-distance pre-filter within (1 + 1e-14) of the minimum, as k_hero
-    const int k = lane / W, sub = lane - k * W;
-    const bool act = k < ne;
-    const DRec r = rec_of(act ? k : 0);
-    const double fx = misc[8 * k + 3], fy = misc[8 * k + 4];
-    const int nr = act ? r.hi[CBEV_HI_NROUTE] : 0;
-    double m2 = INFINITY;
-    for (int i = sub; i < nr; i += W) {
-      const double dx = fx - r.cx[i], dy = fy - r.cy[i];
-      const double d2 = dx * dx + dy * dy;
-      m2 = d2 < m2 ? d2 : m2;
-    }
-    m2 = group_min<W>(m2);
-    const double lim = m2 * (1.0 + 1e-14);
-    double bd = INFINITY;
-    int bi = 0x7fffffff;
-    for (int i = sub; i < nr; i += W) {
-      const double dx = fx - r.cx[i], dy = fy - r.cy[i];
-      if (dx * dx + dy * dy <= lim) {
-        const double h = hypot(dx, dy);
-        if (h < bd) {
-          bd = h;
-          bi = i;
-        }
-      }
-    }
-    group_argmin<W>(bd, bi);
-    if (act && sub == 0) {
-      bi = bi == 0x7fffffff ? 0 : bi;
-      r.hi[CBEV_HI_TIDX] = r.hi[CBEV_HI_TIDX] >= bi ? r.hi[CBEV_HI_TIDX] : bi;
-    }
-  }
-  __syncthreads();
-  CBEV_STAMP(3, 2);
-  // S3
-  if (lane < ne) {
-    if (wave == 0) hero_env_render_setup(K, rec_of(lane));
-    else if (wave == 1) hero_env_comfort(rec_of(lane));
-  }
-  __syncthreads();
-  CBEV_STAMP(3, 3);
-  // S4
-  const int64_t SS = (int64_t)K.P.size * K.P.size;
-  for (int k = 0; k < ne - 1; ++k) {
-    raster_env<false, G>(K, rec_of(k), frames + (e0 + k) * SS, 1, 0, lds);
-    __syncthreads();  // the next env's staging overwrites the crop image
-  }
-  auto side = [&](int ln) {
-    const int k = ln / W;
-    if (k < ne)
-      collide_group<W>(K, rec_of(k), e0 + k, ln - k * W, (uint32_t*)(hitb + k * hwb), reward_out, term_out,
-                       trunc_out, cause_out, info_out);
-  };
-  raster_env<false, G, 3>(K, rec_of(ne - 1), frames + (e0 + ne - 1) * SS, 1, 0, lds, side);
-  __syncthreads();
-  // S5
-  {
-    const int q16 = hh / 16;
-    for (int q = tid; q < ne * q16; q += 256) {
-      const int k = q / q16, c = q - k * q16;
-      ((uint4*)(recs + (int64_t)(e0 + k) * rb + K.L.hd))[c] = ((const uint4*)(lhh + k * hh))[c];
-    }
-  }
-  CBEV_STAMP(2, 3);
-}
 
 // ============================================================== reset / ring / expansion
 // The 16 per-palette-id words of an expansion (channel bitmask / gray value /
@@ -3033,28 +2525,23 @@ struct cbev_ctx {
   int64_t prof_n;
   hipEvent_t* prof_ev;  // 4 per recorded step
   int npitch;            // nibble-packed map pitch (bytes)
-  int hero_ne, hero_sb;  // staged thread-per-env kernels: envs per workgroup, staged bytes per record
-  int coll_ne, coll_sb, coll_scr;
+  int ego_ne;            // k_ego: envs per workgroup
+  int ego_lb;            // k_ego: dynamic LDS bytes per workgroup
   int obs_h, obs_w;   // wrapped frame size (ResizeObservation); == size when not resizing
   void* area_dev;     // INTER_AREA tables of cbev_set_obs_size
   AreaTab area;
   uint8_t* fov_dev;   // cbev_set_fov_mask
-  int step_mode;      // CBEV_STEP_FUSED (k_step) or CBEV_STEP_SPLIT (k_hero, k_raster, k_collide)
-  int step_lb;        // k_step dynamic LDS bytes
 };
 
-// envs per workgroup for a staged kernel: the largest divisor of 64 whose
-// records fit the LDS budget
-// Envs per workgroup for a staged kernel: small groups spread the record
-// staging (LDS-DMA throughput is per CU) and the chains over more CUs; the
-// largest divisor of 64 not above CBEV_STAGED_NE (default 8) whose records fit
-// the LDS budget.
-static int staged_ne(int sbytes) {
+// Envs per k_ego workgroup: small groups spread the record staging (LDS-DMA
+// throughput is per CU) and the chains over more CUs; the largest divisor of 64
+// not above CBEV_EGO_NE (default 16) whose LDS fits the budget.
+static int ego_ne_for(int per_env) {
   const int budget = 128 * 1024;
-  const char* v = getenv("CBEV_STAGED_NE");
+  const char* v = getenv("CBEV_EGO_NE");
   int ne = v ? atoi(v) : 16;
-  ne = ne >= 64 ? 64 : ne >= 32 ? 32 : ne >= 16 ? 16 : ne >= 8 ? 8 : 4;
-  while (ne > 4 && ne * sbytes > budget) ne >>= 1;
+  ne = ne >= 64 ? 64 : ne >= 32 ? 32 : ne >= 16 ? 16 : ne >= 8 ? 8 : ne >= 4 ? 4 : ne >= 2 ? 2 : 1;
+  while (ne > 1 && ne * per_env > budget) ne >>= 1;
   return ne;
 }
 
@@ -3141,17 +2628,12 @@ static KArgs kargs(const cbev_ctx* c) {
   return K;
 }
 
-typedef void (*ActorsKernel)(KArgs, uint8_t*, int, int);
+typedef void (*ActorsKernel)(KArgs, uint8_t*, int);
 static ActorsKernel actors_kernel(const cbev_caps& C) {
   return (C.actor_cap > 64 || C.actor_route_cap > 64) ? k_actors<true> : k_actors<false>;
 }
 static const void* raster_kernel(int size) {
   return size == 64 ? (const void*)k_raster<1> : size == 128 ? (const void*)k_raster<2> : (const void*)k_raster<4>;
-}
-static const void* step_kernel(int size) {
-  return size == 64    ? (const void*)k_step<1, CBEV_STEP_NE>
-         : size == 128 ? (const void*)k_step<2, CBEV_STEP_NE>
-                       : (const void*)k_step<4, CBEV_STEP_NE>;
 }
 static const void* bank_frames_kernel(int size) {
   return size == 64 ? (const void*)k_bank_frames<1> : size == 128 ? (const void*)k_bank_frames<2>
@@ -3209,14 +2691,17 @@ int cbev_create(const cbev_params* params, const cbev_caps* caps, int device, cb
   c->C = *caps;
   c->L = cbev_make_layout(*caps);
   c->device = device;
-  c->hero_sb = (int)c->L.raw_x;  // HD, HI, ego route cx / cy / cyaw
-  c->coll_sb = (int)c->L.acx;    // ... + raw route, visibility, actor AD / AI groups
-  c->hero_ne = staged_ne(c->hero_sb + 32);
-  c->coll_scr = coll_scratch_layout(c->C, c->L.vis_words).bytes;
-  c->coll_ne = staged_ne(c->coll_sb + c->coll_scr);
-  if (c->coll_ne * (c->coll_sb + c->coll_scr) > 160 * 1024 || c->hero_ne < 4 || c->coll_ne < 4) {
-    free(c);
-    return set_err(CBEV_EINVAL, "record prefix of %d bytes does not fit LDS", c->coll_sb);
+  {
+    // k_ego LDS per env: packed record ranges + collision scratch + HeroPre + target index
+    const int per_env = ego_pack(c->L).bytes + coll_scratch_layout(c->C, c->L.vis_words).bytes +
+                        (int)sizeof(HeroPre) + (int)sizeof(int);
+    c->ego_ne = ego_ne_for(per_env);
+    c->ego_lb = c->ego_ne * per_env;
+    if (c->ego_lb > 160 * 1024) {
+      const int nb = per_env;
+      free(c);
+      return set_err(CBEV_EINVAL, "a record's staged ranges (%d bytes) do not fit LDS", nb);
+    }
   }
   SgTables T;
   build_sg_tables(&T);
@@ -3228,23 +2713,11 @@ int cbev_create(const cbev_params* params, const cbev_caps* caps, int device, cb
   }
   c->obs_h = c->obs_w = P.size;
   if (e == hipSuccess)
-    e = hipFuncSetAttribute((const void*)k_hero, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            c->hero_ne * (c->hero_sb + 32));
-  if (e == hipSuccess)
-    e = hipFuncSetAttribute((const void*)k_collide, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            c->coll_ne * (c->coll_sb + c->coll_scr));
+    e = hipFuncSetAttribute((const void*)k_ego, hipFuncAttributeMaxDynamicSharedMemorySize, c->ego_lb);
   if (e == hipSuccess)
     e = hipFuncSetAttribute(raster_kernel(P.size), hipFuncAttributeMaxDynamicSharedMemorySize, (int)raster_lds_bytes(P));
   if (e == hipSuccess)
     e = hipFuncSetAttribute(reset_kernel(P.size), hipFuncAttributeMaxDynamicSharedMemorySize, (int)raster_lds_bytes(P));
-  c->step_lb = step_lds_bytes(P.size, P.crop, c->L, CBEV_STEP_NE);
-  {
-    // default: the split step (measured faster); CBEV_STEP_MODE=fused selects k_step
-    const char* m = getenv("CBEV_STEP_MODE");
-    c->step_mode = (m && strcmp(m, "fused") == 0) && c->step_lb <= 160 * 1024 ? CBEV_STEP_FUSED : CBEV_STEP_SPLIT;
-  }
-  if (e == hipSuccess && c->step_lb <= 160 * 1024)
-    e = hipFuncSetAttribute(step_kernel(P.size), hipFuncAttributeMaxDynamicSharedMemorySize, c->step_lb);
   if (e == hipSuccess)
     e = hipFuncSetAttribute(bank_frames_kernel(P.size), hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)raster_lds_bytes(P));
@@ -3255,17 +2728,6 @@ int cbev_create(const cbev_params* params, const cbev_caps* caps, int device, cb
   *out = c;
   return CBEV_OK;
 }
-
-int cbev_set_step_mode(cbev_ctx* c, int mode) {
-  if (!c) return set_err(CBEV_EINVAL, "null argument");
-  if (mode != CBEV_STEP_FUSED && mode != CBEV_STEP_SPLIT) return set_err(CBEV_EINVAL, "bad step mode %d", mode);
-  if (mode == CBEV_STEP_FUSED && c->step_lb > 160 * 1024)
-    return set_err(CBEV_EINVAL, "k_step needs %d bytes of LDS", c->step_lb);
-  c->step_mode = mode;
-  return CBEV_OK;
-}
-
-int cbev_step_mode(const cbev_ctx* c) { return c ? c->step_mode : -1; }
 
 int cbev_profile(cbev_ctx* c, int enable) {
   if (!c) return set_err(CBEV_EINVAL, "null argument");
@@ -3285,7 +2747,7 @@ int cbev_profile_read(cbev_ctx* c, double* ms3, int64_t* steps) {
   if (steps) *steps = c->prof_n;
   if (!c->prof_ev || c->prof_n == 0) return CBEV_OK;
   HIP_TRY(hipEventSynchronize(c->prof_ev[4 * (c->prof_n - 1) + 3]));
-  // events: 0 before k_hero, 1 after k_actors, 2 after k_raster, 3 after k_collide
+  // events: 0 before k_actors, 1 after k_actors, 2 after k_ego, 3 after k_raster
   for (int64_t i = 0; i < c->prof_n; ++i) {
     for (int k = 0; k < 3; ++k) {
       float ms = 0.f;
@@ -3299,13 +2761,12 @@ int cbev_profile_read(cbev_ctx* c, double* ms3, int64_t* steps) {
 int cbev_profile_raster(cbev_ctx* c, void* records, int n, uint8_t* frames, int reps, void* stream, double* ms) {
   if (!c || !records || !frames || !ms) return set_err(CBEV_EINVAL, "null argument");
   if (!c->map_dev) return set_err(CBEV_ESTATE, "cbev_set_map not called");
-  if (c->step_mode != CBEV_STEP_SPLIT) return set_err(CBEV_ESTATE, "the render set-up is written by the split step");
   if (n <= 0 || reps <= 0) return set_err(CBEV_EINVAL, "n and reps must be positive");
   HIP_TRY(hipSetDevice(c->device));
   hipStream_t s = (hipStream_t)stream;
   const KArgs K = kargs(c);
   const size_t lb = raster_lds_bytes(c->P);
-  const int rg = (n + CBEV_RASTER_NE - 1) / CBEV_RASTER_NE;
+  const int rg = n;
   hipEvent_t ev[2];
   HIP_TRY(hipEventCreate(&ev[0]));
   HIP_TRY(hipEventCreate(&ev[1]));
@@ -3380,44 +2841,19 @@ int cbev_step(cbev_ctx* c, void* records, int n, const void* actions, uint8_t* f
   hipEvent_t* ev = nullptr;
   if (c->prof_on && c->prof_n < CBEV_PROF_MAX) ev = c->prof_ev + 4 * c->prof_n++;
   if (ev) HIP_TRY(hipEventRecord(ev[0], s));
-  if (c->step_mode == CBEV_STEP_FUSED) {
-    // k_actors (clock look-ahead: k_step advances hd[T]) + one fused launch
-    if (c->C.actor_cap > 0) hipLaunchKernelGGL(actors_kernel(c->C), dim3(wg4), dim3(256), 0, s, K, (uint8_t*)records, n, 1);
-    if (ev) HIP_TRY(hipEventRecord(ev[1], s));
-    const dim3 grid((n + CBEV_STEP_NE - 1) / CBEV_STEP_NE);
-    switch (c->P.size) {
-      case 64: hipLaunchKernelGGL((k_step<1, CBEV_STEP_NE>), grid, dim3(256), c->step_lb, s, K, (uint8_t*)records, n,
-                                  actions, frames, reward, term, trunc, cause, info); break;
-      case 128: hipLaunchKernelGGL((k_step<2, CBEV_STEP_NE>), grid, dim3(256), c->step_lb, s, K, (uint8_t*)records, n,
-                                   actions, frames, reward, term, trunc, cause, info); break;
-      default: hipLaunchKernelGGL((k_step<4, CBEV_STEP_NE>), grid, dim3(256), c->step_lb, s, K, (uint8_t*)records, n,
-                                  actions, frames, reward, term, trunc, cause, info); break;
-    }
-    if (ev) {
-      HIP_TRY(hipEventRecord(ev[2], s));
-      HIP_TRY(hipEventRecord(ev[3], s));
-    }
-    HIP_TRY(hipGetLastError());
-    return CBEV_OK;
-  }
-  hipLaunchKernelGGL(k_hero, dim3((n + c->hero_ne - 1) / c->hero_ne), dim3(256),
-                     (size_t)c->hero_ne * (c->hero_sb + 32), s, K,
-                     (uint8_t*)records, n, actions, c->hero_ne, c->hero_sb);
-  if (c->C.actor_cap > 0) hipLaunchKernelGGL(actors_kernel(c->C), dim3(wg4), dim3(256), 0, s, K, (uint8_t*)records, n, 0);
+  if (c->C.actor_cap > 0) hipLaunchKernelGGL(actors_kernel(c->C), dim3(wg4), dim3(256), 0, s, K, (uint8_t*)records, n);
   if (ev) HIP_TRY(hipEventRecord(ev[1], s));
+  hipLaunchKernelGGL(k_ego, dim3((n + c->ego_ne - 1) / c->ego_ne), dim3(256), (size_t)c->ego_lb, s, K,
+                     (uint8_t*)records, n, actions, reward, term, trunc, cause, info, c->ego_ne);
+  if (ev) HIP_TRY(hipEventRecord(ev[2], s));
   {
     const size_t lb = raster_lds_bytes(c->P);
-    const int rg = (n + CBEV_RASTER_NE - 1) / CBEV_RASTER_NE;
     switch (c->P.size) {
-      case 64: hipLaunchKernelGGL(k_raster<1>, dim3(rg), dim3(raster_threads(64)), lb, s, K, (uint8_t*)records, n, frames); break;
-      case 128: hipLaunchKernelGGL(k_raster<2>, dim3(rg), dim3(raster_threads(128)), lb, s, K, (uint8_t*)records, n, frames); break;
-      default: hipLaunchKernelGGL(k_raster<4>, dim3(rg), dim3(raster_threads(256)), lb, s, K, (uint8_t*)records, n, frames); break;
+      case 64: hipLaunchKernelGGL(k_raster<1>, dim3(n), dim3(raster_threads(64)), lb, s, K, (uint8_t*)records, n, frames); break;
+      case 128: hipLaunchKernelGGL(k_raster<2>, dim3(n), dim3(raster_threads(128)), lb, s, K, (uint8_t*)records, n, frames); break;
+      default: hipLaunchKernelGGL(k_raster<4>, dim3(n), dim3(raster_threads(256)), lb, s, K, (uint8_t*)records, n, frames); break;
     }
   }
-  if (ev) HIP_TRY(hipEventRecord(ev[2], s));
-  hipLaunchKernelGGL(k_collide, dim3((n + c->coll_ne - 1) / c->coll_ne), dim3(256),
-                     (size_t)c->coll_ne * (c->coll_sb + c->coll_scr), s,
-                     K, (uint8_t*)records, n, reward, term, trunc, cause, info, c->coll_ne, c->coll_sb);
   if (ev) HIP_TRY(hipEventRecord(ev[3], s));
   HIP_TRY(hipGetLastError());
   return CBEV_OK;
@@ -3477,7 +2913,7 @@ int cbev_reset_frames(cbev_ctx* c, void* records, int n, const void* bank, int n
                                        reset_pieces_rec(c->L.record_bytes));
   // grid cap for masked resets (the canonical reset of the envs that terminated):
   // 1024 measured best (config 2: 6.0 / 6.2 / 6.6 / 7.6 / 10.9 us at 1024 / 256 / 128 / 2048 / 4096)
-  const int cap = mask ? CBEV_RESET_MASKED_WGS : RESET_WGS;
+  const int cap = mask ? RESET_WGS : RESET_WGS;
   const int grid = pieces >= cap ? cap : (int)((pieces + 7) & ~7);
   hipLaunchKernelGGL(k_reset_copy, dim3(grid), dim3(256), 0, (hipStream_t)stream, K, (uint8_t*)records, n,
                      (const uint8_t*)bank, n_bank, mask, bank_idx, bank_offset, bank_frames, frames, n_frames);

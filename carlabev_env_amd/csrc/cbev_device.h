@@ -49,6 +49,7 @@ struct DRec {
   double *cx, *cy, *cyaw, *raw_cum;
   int32_t *raw_x, *raw_y;
   uint32_t* vis;
+  uint32_t* vis_draw;  // vis_words words after vis: the bits this step's observation draws
   double* ad;
   int32_t* ai;
   double *acx, *acy, *acyaw, *aix, *aiy, *arx, *ary;
@@ -67,6 +68,7 @@ __device__ __forceinline__ DRec bind_rec(uint8_t* base, const cbev_layout& L, co
   r.raw_y = (int32_t*)(base + L.raw_y);
   r.raw_cum = (double*)(base + L.raw_cum);
   r.vis = (uint32_t*)(base + L.vis);
+  r.vis_draw = r.vis + L.vis_words;
   r.ad = (double*)(base + L.ad);
   r.ai = (int32_t*)(base + L.ai);
   r.acx = (double*)(base + L.acx);

@@ -111,7 +111,7 @@ class Layout:
         put("raw_y", 4 * R)
         put("raw_cum", 8 * R)
         vis_words = (R + 31) // 32
-        put("vis", 4 * vis_words)
+        put("vis", 8 * vis_words)  # vis, then vis_draw
         put("ad", 8 * len(AD) * A)
         put("ai", 4 * len(AI) * A)
         for n in ("acx", "acy", "acyaw", "aix", "aiy", "arx", "ary"):
@@ -141,6 +141,7 @@ class RecordView:
         self.raw_y = v("raw_y", np.int32, (R,))
         self.raw_cum = v("raw_cum", np.float64, (R,))
         self.vis = v("vis", np.uint32, (layout.vis_words,))
+        self.vis_draw = buf[o["vis"] + 4 * layout.vis_words:o["vis"] + 8 * layout.vis_words].view(np.uint32)
         self.ad = v("ad", np.float64, (len(AD), A))
         self.ai = v("ai", np.int32, (len(AI), A))
         self.acx = v("acx", np.float64, (A, RA))

@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define CBEV_ABI_VERSION 1
+#define CBEV_ABI_VERSION 2
 
 typedef struct cbev_ctx cbev_ctx;
 
@@ -52,7 +52,9 @@ void cbev_destroy(cbev_ctx* ctx);
  * copied into context-owned HBM. Replaces load_map (envs/utils.py:49-62). */
 int cbev_set_map(cbev_ctx* ctx, const uint8_t* padded_map_host, int64_t bytes);
 
-/* One `CarlaBEV.step(action)` (carlabev.py:223-231) for n envs:
+/* One `CarlaBEV.step(action)` (carlabev.py:223-231) for n envs: k_actors (when
+ * the record has actor slots), k_ego (ego update + collision / reward /
+ * termination), k_raster (the observation), in that order on `stream`:
  *   records      n state records (record_bytes each), updated in place
  *   actions      int32[n] discrete indices, or float32[n][3] continuous
  *   frames       uint8[n][S][S] palette-id observation (render(), carlabev.py:233-249)
@@ -61,18 +63,6 @@ int cbev_set_map(cbev_ctx* ctx, const uint8_t* padded_map_host, int64_t bytes);
 #define CBEV_INFO_FLOATS 16
 int cbev_step(cbev_ctx* ctx, void* records, int n, const void* actions, uint8_t* frames, double* reward,
               uint8_t* term, uint8_t* trunc, int32_t* cause, float* info, void* stream);
-
-/* How cbev_step runs on the device (results are identical):
- *   CBEV_STEP_SPLIT  k_hero, k_actors, k_raster, k_collide (default)
- *   CBEV_STEP_FUSED  k_actors (when the record has actor slots) + k_step, one
- *                    workgroup per 2 envs for ego update, raster and collision /
- *                    reward (the environment variable CBEV_STEP_MODE=fused
- *                    selects it at cbev_create)
- * Not stream-ordered: call it between steps. */
-#define CBEV_STEP_FUSED 0
-#define CBEV_STEP_SPLIT 1
-int cbev_set_step_mode(cbev_ctx* ctx, int mode);
-int cbev_step_mode(const cbev_ctx* ctx);
 
 /* Reset the envs selected by mask (uint8[n], NULL = all):
  *   if bank != NULL: records[i] = bank[b] with b = bank_idx[i], or, when
@@ -152,8 +142,7 @@ int cbev_resize_obs(cbev_ctx* ctx, const uint8_t* frames, int n, const uint8_t* 
  * step kernel (used by bench.py for the roofline figure). cbev_profile(ctx, 1)
  * resets the counters and starts recording (up to 8192 steps);
  * cbev_profile_read synchronises on the last event and returns the summed
- * milliseconds of [k_hero + k_actors, k_raster, k_collide] (split step) or
- * [k_actors, k_step, 0] (fused step) and the step count. */
+ * milliseconds of [k_actors, k_ego, k_raster] and the step count. */
 int cbev_profile(cbev_ctx* ctx, int enable);
 int cbev_profile_read(cbev_ctx* ctx, double* ms3, int64_t* steps);
 
@@ -161,10 +150,9 @@ int cbev_profile_read(cbev_ctx* ctx, double* ms3, int64_t* steps);
  * `stream`, timed with two HIP events around the burst (bench.py's roofline
  * figure: the per-kernel events of cbev_profile also count each launch's
  * dispatch gap). It re-renders the observation of the current records, so
- * call it right after a split-mode cbev_step (which writes the render set-up)
- * and before any reset: `frames` then receives the bytes that step wrote, less
- * the checkpoint targets that step's collision pass consumed after its render.
- * Synchronises; writes the milliseconds per launch to *ms. */
+ * call it right after a cbev_step (which writes the render set-up and the
+ * drawn target bits) and before any reset: `frames` then receives the bytes
+ * that step wrote. Synchronises; writes the milliseconds per launch to *ms. */
 int cbev_profile_raster(cbev_ctx* ctx, void* records, int n, uint8_t* frames, int reps, void* stream, double* ms);
 
 #ifdef __cplusplus

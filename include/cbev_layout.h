@@ -21,7 +21,7 @@
 
 #include <stdint.h>
 
-#define CBEV_LAYOUT_VERSION 1
+#define CBEV_LAYOUT_VERSION 2
 
 /* ---- hero + per-env scene/episode scalars, float64 -------------------- */
 #define CBEV_HD_FIELDS(F_)                                                     \
@@ -62,7 +62,7 @@
   F_(COLLIDED)       /* 0 none, 1 vehicle, 2 pedestrian, 3 target */          \
   F_(ACTOR_ID)       /* -1 None, -2 "goal", else int id */                     \
   F_(EP_LEN) F_(STEP) F_(SCENE_ID) F_(NACTSTATE) F_(PAD0)                         \
-  /* render set-up of the current observation (device scratch, k_hero -> k_raster): */ \
+  /* render set-up of the current observation (device scratch, k_ego -> k_raster): */ \
   F_(RS_XMIN) F_(RS_YMIN) /* crop origin in the padded map (fov.py:70-79) */        \
   F_(RS_R90) F_(RS_NX) F_(RS_NY) F_(RS_ISIN) F_(RS_ICOS) F_(RS_DX00) F_(RS_DY00)      \
   F_(RS_A00) F_(RS_USTEP) F_(RS_VSTEP) F_(RS_RX0) F_(RS_RY0)                        \
@@ -150,7 +150,11 @@ typedef struct cbev_layout {
   int64_t cx, cy, cyaw;                 /* double[route_cap] */
   int64_t raw_x, raw_y;                 /* int32[route_cap] */
   int64_t raw_cum;                      /* double[route_cap] */
-  int64_t vis;                          /* uint32[vis_words] target visibility */
+  int64_t vis;                          /* uint32[vis_words] target visibility, then
+                                           uint32[vis_words] the bits this step's
+                                           observation draws (before the step's
+                                           collisions consume targets, scene.py:93-95
+                                           run before scene.py:110-140) */
   int64_t ad, ai;                       /* double[AD][A], int32[AI][A] */
   int64_t acx, acy, acyaw;              /* double[A][RA] */
   int64_t aix, aiy;                     /* double[A][RA] initial raw route */
@@ -178,7 +182,7 @@ static inline cbev_layout cbev_make_layout(cbev_caps c) {
   L.raw_y = o;   o = cbev__align(o + 4 * R, 64);
   L.raw_cum = o; o = cbev__align(o + 8 * R, 64);
   L.vis_words = (int32_t)((R + 31) / 32);
-  L.vis = o;     o = cbev__align(o + 4 * (int64_t)L.vis_words, 64);
+  L.vis = o;     o = cbev__align(o + 8 * (int64_t)L.vis_words, 64);
   L.ad = o;      o = cbev__align(o + 8 * (int64_t)CBEV_AD_COUNT * A, 64);
   L.ai = o;      o = cbev__align(o + 4 * (int64_t)CBEV_AI_COUNT * A, 64);
   L.acx = o;     o = cbev__align(o + 8 * A * RA, 64);

@@ -645,11 +645,12 @@ typedef struct orc_rec {
   double *cx, *cy, *cyaw, *raw_cum;
   int32_t *raw_x, *raw_y;
   uint32_t* vis;
+  uint32_t* vis_draw; /* vis_words words after vis */
   double* ad;
   int32_t* ai;
   double *acx, *acy, *acyaw, *aix, *aiy, *arx, *ary;
   int32_t* ti;
-  int A, RA, T;
+  int A, RA, T, vis_words;
 } orc_rec;
 
 static orc_rec bind_record(uint8_t* rec, const cbev_caps* caps) {
@@ -664,6 +665,8 @@ static orc_rec bind_record(uint8_t* rec, const cbev_caps* caps) {
   r.raw_y = (int32_t*)(rec + L.raw_y);
   r.raw_cum = (double*)(rec + L.raw_cum);
   r.vis = (uint32_t*)(rec + L.vis);
+  r.vis_draw = r.vis + L.vis_words;
+  r.vis_words = L.vis_words;
   r.ad = (double*)(rec + L.ad);
   r.ai = (int32_t*)(rec + L.ai);
   r.acx = (double*)(rec + L.acx);
@@ -1110,6 +1113,8 @@ int orc_step(const cbev_params* P, const uint8_t* padded_map, const cbev_caps* c
     }
   }
   int nt = hi[CBEV_HI_NROUTE];
+  /* the bits this step's observation drew (the render ran before this check) */
+  for (int w = 0; w < r->vis_words; ++w) r->vis_draw[w] = r->vis[w];
   for (int i = 0; i < nt; ++i) { /* Target.isCollided (target.py:37-44) */
     if (!((r->vis[i >> 5] >> (i & 31)) & 1u)) continue;
     int sz = (i < nt - 1) ? 2 : 4;

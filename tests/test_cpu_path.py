@@ -22,7 +22,7 @@ def test_library_loads_and_exports_every_symbol():
     L = _lib.lib()
     for name in _lib.EXPORTED_SYMBOLS:
         assert hasattr(L, name), name
-    assert L.cbev_abi_version() == 1
+    assert L.cbev_abi_version() == 2
     assert L.cbev_params_size() == ctypes.sizeof(CbevParams)
 
 
@@ -128,9 +128,11 @@ def test_oracle_raster_matches_numpy_restatement_mid_episode():
             before = recs[e].copy()
             orc.step_one(recs[e], np.ascontiguousarray(acts[t, e]), frame)
             # the frame is drawn after dynamics and before collision consumption:
-            # rebuild that state = post-step record with the pre-step visibility bits
+            # rebuild that state = post-step record with the pre-step visibility
+            # bits, which the step also kept as vis_draw
             mid = recs[e].copy()
             vmid, vbef = LY.RecordView(mid, layout), LY.RecordView(before, layout)
+            assert np.array_equal(vmid.vis_draw, vbef.vis)
             vmid.vis[:] = vbef.vis
             ref = raster_ref.render(P, padded, vmid)
             assert np.array_equal(frame, ref), (t, e, np.argwhere(frame != ref)[:5])
