@@ -506,38 +506,21 @@ __device__ __forceinline__ void d_crop_origin(const cbev_params& P, double x, do
 // rect_from_world_center (transforms.py:46-51): centre rounded half-even, x = c - w/2
 __device__ __forceinline__ int d_rect_lo(double w, int pad, int size) { return (int)rint((double)pad + w * 1.0) - size / 2; }
 
-// LDS image of the crop window. Nibble layout (S >= 128), packed like the map:
-// crop row r starts at dword r * sd and holds the packed map bytes from
-// xa = (xmin >> 1) & ~3 on (dword-aligned), so crop pixel (c, r) is texel shift + c
-// of the row (shift = xmin - 2 xa, 0..7), i.e. "nibble address" r * 8 sd + shift + c:
-// byte >> 1 of it, high nibble when odd. sd = the dwords a row needs (7 + C
-// nibbles), rounded up to odd so that successive crop rows start in different
-// LDS banks and gathers along a rotated row spread over the banks at every
-// angle. Rows are staged as 16-byte chunks of the packed map (the last one
-// clipped to sd).
-// Byte layout (S <= 64): the staging unpacks the nibbles, one texel per LDS byte,
-// so a gather is an address (row * sb + column, two SDWA ops on the 16.16
-// coordinates) and a byte read, without the nibble select. Texel address
-// = byte address r * 4 sd + shift + c; sd = dwords for 7 + C texels, odd.
-// Rows are dword-aligned in the map (16-byte loads at 4-byte alignment), so a
-// row carries at most 7 texels of slack: 182 x 27 dwords = 19.7 KB at S=128,
-// which keeps 8 workgroups per CU.
-// At S=128 the byte image (182 x 55 dwords = 40 KB) leaves 4 workgroups per CU
-// instead of the nibble image's 8, and measured slower (37 vs 30 us per step
-// raster at 4096 envs) despite half the gather VALU: the raster needs the
-// occupancy to hide latency. S >= 128 keeps the nibble image.
-__host__ __device__ __forceinline__ constexpr bool raster_bytes(int S) { return S <= 64; }
-__host__ __device__ __forceinline__ int raster_stride_dwords(int S, int C) {
-  return raster_bytes(S) ? ((C + 7 + 3) / 4) | 1 : ((C + 7 + 7) / 8) | 1;
-}
+// LDS image of the crop window, nibble-packed like the map: crop row r starts
+// at dword r * sd and holds the packed map bytes from xa = (xmin >> 1) & ~3 on
+// (dword-aligned), so crop pixel (c, r) is texel shift + c of the row (shift =
+// xmin - 2 xa, 0..7), i.e. "nibble address" r * 8 sd + shift + c: byte >> 1 of
+// it, high nibble when odd. sd = the dwords a row needs (7 + C nibbles),
+// rounded up to odd so that successive crop rows start in different LDS banks
+// and gathers along a rotated row spread over the banks at every angle:
+// 182 x 25 dwords = 18.2 KB at S=128. (A byte-per-texel image halves the
+// gather VALU but at S=128 doubles the image, and measured slower: 37 vs 30 us
+// per raster launch at 4096 envs.)
+__host__ __device__ __forceinline__ int raster_stride_dwords(int S, int C) { return ((C + 7 + 7) / 8) | 1; }
 // texels per LDS row (the row stride of texel addresses)
-__host__ __device__ __forceinline__ int raster_row_texels(int S, int C) {
-  return (raster_bytes(S) ? 4 : 8) * raster_stride_dwords(S, C);
-}
+__host__ __device__ __forceinline__ int raster_row_texels(int S, int C) { return 8 * raster_stride_dwords(S, C); }
 // 16-byte chunks of the packed map per staged row (32 texels each)
-__host__ __device__ __forceinline__ int raster_row_chunks(int S, int C) {
-  return raster_bytes(S) ? (C + 7 + 31) / 32 : ((C + 7 + 7) / 8 + 3) / 4;
-}
+__host__ __device__ __forceinline__ int raster_row_chunks(int S, int C) { return ((C + 7 + 7) / 8 + 3) / 4; }
 // 16 bytes at 4-byte alignment (crop rows start at a dword of the packed map)
 typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
 __device__ __forceinline__ uint4 load16_a4(const uint8_t* p) {
@@ -545,29 +528,16 @@ __device__ __forceinline__ uint4 load16_a4(const uint8_t* p) {
   return make_uint4(t.x, t.y, t.z, t.w);
 }
 // texel-level helpers on the LDS image (texel address ta)
-template <bool BYTES>
 __device__ __forceinline__ uint32_t lds_texel(const uint8_t* lds, uint32_t ta) {
-  if (BYTES) return lds[ta];
   return (lds[ta >> 1] >> ((ta & 1u) << 2)) & 15u;
 }
-template <bool BYTES>
 __device__ __forceinline__ void lds_set_texel(uint8_t* lds, uint32_t ta, uint32_t col) {
-  if (BYTES) {
-    lds[ta] = (uint8_t)col;
-    return;
-  }
   uint32_t* w = (uint32_t*)lds + (ta >> 3);
   const uint32_t sh = (ta & 7u) << 2;
   atomicAnd(w, ~(15u << sh));
   atomicOr(w, col << sh);
 }
 __host__ __device__ __forceinline__ int raster_image_bytes(int S, int C) { return C * raster_stride_dwords(S, C) * 4; }
-// 8 packed texels (one map dword, texel 2k in the low nibble of byte k) -> 8 bytes
-__device__ __forceinline__ void unpack_texels(uint32_t w, uint32_t* o) {
-  const uint32_t lo = w & 0x0F0F0F0Fu, hi = (w >> 4) & 0x0F0F0F0Fu;
-  o[0] = __builtin_amdgcn_perm(hi, lo, 0x05010400u);
-  o[1] = __builtin_amdgcn_perm(hi, lo, 0x07030602u);
-}
 
 // Per-env rotation parameters (pygame transform.rotate, 16.16 fixed point;
 // rotate90 for exact multiples of 90 degrees) and the compose placement.
@@ -1098,46 +1068,43 @@ __global__ __launch_bounds__(256) void k_actors(KArgs K, uint8_t* __restrict__ r
 }
 
 
-// Output pass over one wave's chunks of 1024 output pixels (16 / G rows). A
-// chunk is four 256-pixel dword groups: in group d lane l owns the 4
-// consecutive output pixels 256 d + 4 l .. + 3 of the chunk (row r + d (4 / G)
-// + l / (16 G), columns 4 (l % (16 G)) .. + 3), gathers them one column step
-// apart and packs them into one dword, so each group is ONE 256-byte dword
-// store. Source coordinates are stepped, not recomputed (pygame's rotozoom is
-// affine in the output pixel): per gather one 64-bit add, a 24-bit
-// multiply-add for the LDS byte address, the LDS read, the nibble extract and
-// the pack.
+// Output pass over one wave's chunks of 1024 output pixels (16 / G rows). In a
+// chunk lane l owns the 16 consecutive pixels of row r + l / (4 G), columns
+// 16 (l % (4 G)) .. + 15: it gathers them one column step apart, packs them into
+// four dwords and writes them with ONE 16-byte store, so a chunk is one
+// 1 KiB wave store (the stores are issue-bound per instruction, not per byte).
+// Source coordinates are stepped, not recomputed (pygame's rotozoom is affine
+// in the output pixel): per gather one 64-bit add, a 24-bit multiply-add for
+// the LDS byte address, the LDS read, the nibble extract and the pack.
 //   CHECK = false: the rotated surface covers the whole output and every output
 //   pixel samples inside the crop (checked once per env at the four corners;
 //   the map is affine) -> no per-pixel tests.
 //   CHECK = true: compose clipping (black outside the rotated surface) and the
 //   rotozoom background test (bg outside the source), per pixel.
+typedef uint32_t u32x4_nt __attribute__((ext_vector_type(4)));
 template <int G, bool R90, bool CHECK, int NW>
 __device__ __forceinline__ void raster_out(const cbev_params& P, const RotSetup& R, const uint8_t* __restrict__ lds,
                                            int shift, uint32_t bg, uint8_t* __restrict__ out, int nout,
                                            int64_t out_stride, int lane, int wave,
                                            const uint32_t* __restrict__ fov) {
-  constexpr int RPC = 16 / G;  // output rows per chunk
-  constexpr int S = 64 * G;    // == P.size
-  constexpr int LPR = S / 4;   // lanes per output row
-  constexpr int RPD = 4 / G;   // output rows per dword group
-  constexpr bool BYTES = raster_bytes(S);
+  constexpr int S = 64 * G;     // == P.size
+  constexpr int LPR = S / 16;   // lanes per output row
+  constexpr int RPC = 64 / LPR; // output rows per chunk
   const int C = P.crop;
   const uint32_t vmax = (uint32_t)((C << 16) - 1);
   const int hero_w = P.hero_w;
   const int hx0 = P.anchor_x - hero_w / 2, hy0 = P.anchor_y - hero_w / 2;
-  const int lrow = lane / LPR, lcol = 4 * (lane % LPR);
-  // this lane's columns: hero byte mask (Hero.draw: black w x w rect at the
+  const int lrow = lane / LPR, lcol = 16 * (lane % LPR);
+  // this lane's columns: hero byte masks (Hero.draw: black w x w rect at the
   // anchor, hero.py:26-32) and the compose-clip column test
-  uint32_t hmask = 0, xok = 0;
+  uint32_t hmask[4] = {0u, 0u, 0u, 0u}, xok = 0;
 #pragma unroll
-  for (int b = 0; b < 4; ++b) {
+  for (int b = 0; b < 16; ++b) {
     const int u = lcol + b;
-    if (u >= hx0 && u < hx0 + hero_w) hmask |= 0xffu << (8 * b);
+    if (u >= hx0 && u < hx0 + hero_w) hmask[b >> 2] |= 0xffu << (8 * (b & 3));
     const int xx = u - R.rx0;
     if (xx >= 0 && xx < R.nx) xok |= 1u << b;
   }
-  const uint32_t hblack = hmask & (CBEV_PX_BLACK * 0x01010101u);
   const int r0 = wave * RPC;
   const int xx0 = lcol - R.rx0, yy0 = r0 + lrow - R.ry0;
   // lane state at (output row r0 + lrow, column lcol) of this wave's first chunk
@@ -1145,8 +1112,7 @@ __device__ __forceinline__ void raster_out(const cbev_params& P, const RotSetup&
   int sy = R.dy00 + xx0 * R.isin + yy0 * R.icos;  // 16.16 source y (general)
   int sa = R.a00 + shift + xx0 * R.ustep + yy0 * R.vstep;  // LDS texel address (rotate90)
   // the crop's texel offset rides in the integer part of sx, so the LDS byte is
-  // (sy >> 16) * sb + (sx >> 16) (byte image) or (sy >> 16) * sb + (sx >> 17) with
-  // the nibble (sx >> 16) & 1 (nibble image)
+  // (sy >> 16) * sb + (sx >> 17) with the nibble (sx >> 16) & 1
   sx += shift << 16;
   const uint8_t* img = lds;
   const uint32_t sb = 4u * (uint32_t)raster_stride_dwords(S, C);  // LDS bytes per crop row
@@ -1157,68 +1123,63 @@ __device__ __forceinline__ void raster_out(const cbev_params& P, const RotSetup&
   uint64_t pxy = ((uint64_t)(uint32_t)sy << 32) | (uint32_t)sx;
   const uint64_t chunk_step =
       (uint64_t)(((int64_t)(chunk_rows * R.icos) << 32) + (int64_t)(-chunk_rows * R.isin));
-  // one output row down: (dx, dy) += (-isin, icos); one column right: += (icos, isin)
-  const uint64_t group_step = (uint64_t)(((int64_t)(RPD * R.icos) << 32) + (int64_t)(-RPD * R.isin));
+  // one column right: (dx, dy) += (icos, isin)
   const uint64_t col_step = (uint64_t)(((int64_t)R.isin << 32) + (int64_t)R.icos);
   for (int ch = wave, r = r0; ch < nchunks; ch += NW, r += chunk_rows) {
+    const int row = r + lrow;
     // the frame is written through the uniform base `out` plus a per-lane offset
-    const uint32_t vo = (uint32_t)(r * S + 4 * lane);
-    const bool hero_rows = (unsigned)(r + RPC - 1 - hy0) < (unsigned)(RPC - 1 + hero_w);  // chunk meets the hero rows
+    const uint32_t vo = (uint32_t)(row * S + lcol);
     asm volatile("" : "+v"(pxy), "+v"(sa));  // keep the per-gather offsets as scalar adds
+    const bool rok = !CHECK || (unsigned)(row - R.ry0) < (unsigned)R.ny;
     uint32_t w[4];
-    uint64_t qg = pxy;  // general path: source coordinates of (row r + d RPD + lrow, column lcol)
 #pragma unroll
     for (int d = 0; d < 4; ++d) {
       uint32_t acc = 0;
 #pragma unroll
-      for (int b = 0; b < 4; ++b) {
+      for (int bb = 0; bb < 4; ++bb) {
+        const int b = 4 * d + bb;
         uint32_t v;
         if (R90) {
-          const int a = sa + d * RPD * R.vstep + b * R.ustep;
+          const int a = sa + b * R.ustep;
           if (CHECK) {
-            const bool ok = ((xok >> b) & 1u) && (unsigned)(r + d * RPD + lrow - R.ry0) < (unsigned)R.ny;
-            v = ok ? lds_texel<BYTES>(img, ok ? a : 0) : (uint32_t)CBEV_PX_BLACK;
+            const bool ok = ((xok >> b) & 1u) && rok;
+            v = ok ? lds_texel(img, ok ? a : 0) : (uint32_t)CBEV_PX_BLACK;
           } else {
-            v = lds_texel<BYTES>(img, a);
+            v = lds_texel(img, a);
           }
         } else {
-          const uint64_t q = b == 0 ? qg : qg + (uint64_t)b * col_step;
+          const uint64_t q = pxy + (uint64_t)b * col_step;
           const uint32_t dx = (uint32_t)q, dy = (uint32_t)(q >> 32);
-          const uint32_t byte = __umul24(dy >> 16, sb) + (BYTES ? (dx >> 16) : (dx >> 17));
-          const uint32_t nsh = BYTES ? 0u : (dx >> 14) & 4u;
+          const uint32_t byte = __umul24(dy >> 16, sb) + (dx >> 17);
+          const uint32_t nsh = (dx >> 14) & 4u;
           if (CHECK) {  // bounds on the unshifted source coordinate
             const int ux = (int)dx - (shift << 16);
-            const bool ok = ((xok >> b) & 1u) && (unsigned)(r + d * RPD + lrow - R.ry0) < (unsigned)R.ny;
+            const bool ok = ((xok >> b) & 1u) && rok;
             const bool in = (uint32_t)ux <= vmax && dy <= vmax;
-            const uint32_t s = BYTES ? img[(in && ok) ? byte : 0u] : (img[(in && ok) ? byte : 0u] >> nsh) & 15u;
+            const uint32_t s = (img[(in && ok) ? byte : 0u] >> nsh) & 15u;
             v = !ok ? (uint32_t)CBEV_PX_BLACK : (in ? s : bg);
           } else {
-            v = BYTES ? img[byte] : (img[byte] >> nsh) & 15u;
+            v = (img[byte] >> nsh) & 15u;
           }
         }
-        acc |= v << (8 * b);
+        acc |= v << (8 * bb);
       }
       w[d] = acc;
-      if (!R90) qg += group_step;
     }
-    if (hero_rows) {
+    if ((unsigned)(row - hy0) < (unsigned)hero_w) {
 #pragma unroll
-      for (int d = 0; d < 4; ++d)
-        if ((unsigned)(r + d * RPD + lrow - hy0) < (unsigned)hero_w) w[d] = (w[d] & ~hmask) | hblack;
+      for (int d = 0; d < 4; ++d) w[d] = (w[d] & ~hmask[d]) | (hmask[d] & (CBEV_PX_BLACK * 0x01010101u));
     }
     if (fov) {  // FovRenderer.apply_mask (fov.py:96-99): black corner triangles (uniform branch)
-#pragma unroll
-      for (int d = 0; d < 4; ++d) {
-        const uint32_t fm = fov[(vo >> 2) + 64 * d];
-        w[d] = (w[d] & ~fm) | (fm & (CBEV_PX_BLACK * 0x01010101u));
-      }
+      const uint4 fm = *(const uint4*)(fov + (vo >> 2));
+      w[0] = (w[0] & ~fm.x) | (fm.x & (CBEV_PX_BLACK * 0x01010101u));
+      w[1] = (w[1] & ~fm.y) | (fm.y & (CBEV_PX_BLACK * 0x01010101u));
+      w[2] = (w[2] & ~fm.z) | (fm.z & (CBEV_PX_BLACK * 0x01010101u));
+      w[3] = (w[3] & ~fm.w) | (fm.w & (CBEV_PX_BLACK * 0x01010101u));
     }
-    for (int k = 0; k < nout; ++k) {
-      uint8_t* ob = out + (int64_t)k * out_stride;
-#pragma unroll
-      for (int d = 0; d < 4; ++d)  // streamed out: keep the L2 for the map and the records
-        __builtin_nontemporal_store(w[d], (uint32_t*)(ob + (vo + (uint32_t)(256 * d))));
-    }
+    const u32x4_nt v4 = {w[0], w[1], w[2], w[3]};
+    for (int k = 0; k < nout; ++k)  // streamed out: keep the L2 for the map and the records
+      __builtin_nontemporal_store(v4, (u32x4_nt*)(out + (int64_t)k * out_stride + vo));
     pxy += chunk_step;
     sa += chunk_rows * R.vstep;
   }
@@ -1278,7 +1239,6 @@ __device__ __forceinline__ PaintPre raster_paint_fetch(const DRec& r) {
 
 // one rect of side sz (rect_from_world_center, transforms.py:46-51) by the 4
 // threads of tid >> 2: thread tq covers columns tq, tq + 4, ...
-template <bool BYTES>
 __device__ __forceinline__ void paint_rect4(uint8_t* lds, int rt, int shift, int C, int pad, int xmin, int ymin,
                                             double wx, double wy, int sz, int tq, uint32_t col) {
   const int rx = d_rect_lo(wx, pad, sz) - xmin, ry = d_rect_lo(wy, pad, sz) - ymin;
@@ -1287,12 +1247,18 @@ __device__ __forceinline__ void paint_rect4(uint8_t* lds, int rt, int shift, int
     if (py < 0 || py >= C) continue;
     for (int qx = tq; qx < sz; qx += 4) {
       const int px = rx + qx;
-      if (px >= 0 && px < C) lds_set_texel<BYTES>(lds, py * rt + shift + px, col);
+      if (px >= 0 && px < C) lds_set_texel(lds, py * rt + shift + px, col);
     }
   }
 }
 
-template <bool BYTES, int NT = 256>
+// workgroup barrier for LDS-only hand-offs: LDS operations retired, no vmcnt
+// wait, so LDS-DMA (k_raster's next crop image) stays in flight across it
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+template <int NT = 256>
 __device__ __forceinline__ void raster_paint(const KArgs& K, const DRec& r, const PaintPre& q, int xmin, int ymin,
                                              int shift, uint8_t* __restrict__ lds) {
   const cbev_params& P = K.P;
@@ -1304,22 +1270,22 @@ __device__ __forceinline__ void raster_paint(const KArgs& K, const DRec& r, cons
       const int a0 = pass == 0 ? 0 : q.nveh, a1 = pass == 0 ? q.nveh : q.nact;
       if (a1 <= a0) continue;
       const uint32_t col = pass == 0 ? CBEV_PX_VEHICLE : CBEV_PX_PEDESTRIAN;
-      if (k >= a0 && k < a1) paint_rect4<BYTES>(lds, rt, shift, C, P.pad, xmin, ymin, q.ax, q.ay, q.asz, tq, col);
+      if (k >= a0 && k < a1) paint_rect4(lds, rt, shift, C, P.pad, xmin, ymin, q.ax, q.ay, q.asz, tq, col);
       for (int a = NT / 4 + k; a < a1; a += NT / 4)  // more than NT / 4 actors: fetched here
         if (a >= a0)
-          paint_rect4<BYTES>(lds, rt, shift, C, P.pad, xmin, ymin, RAD(r, CBEV_AD_X, a), RAD(r, CBEV_AD_Y, a),
+          paint_rect4(lds, rt, shift, C, P.pad, xmin, ymin, RAD(r, CBEV_AD_X, a), RAD(r, CBEV_AD_Y, a),
                              RAI(r, CBEV_AI_SIZE, a), tq, col);
-      __syncthreads();
+      lds_barrier();
     }
     const int nt = q.nt;
     // checkpoints 2x2, goal 4x4 (scenes/utils.py:114-122)
     if (k < nt && q.tvis)
-      paint_rect4<BYTES>(lds, rt, shift, C, P.pad, xmin, ymin, q.tx, q.ty, k < nt - 1 ? 2 : 4, tq, CBEV_PX_ROUTE);
+      paint_rect4(lds, rt, shift, C, P.pad, xmin, ymin, q.tx, q.ty, k < nt - 1 ? 2 : 4, tq, CBEV_PX_ROUTE);
     for (int i = NT / 4 + k; i < nt; i += NT / 4)
       if ((r.vis_draw[i >> 5] >> (i & 31)) & 1u)
-        paint_rect4<BYTES>(lds, rt, shift, C, P.pad, xmin, ymin, r.cx[i], r.cy[i], i < nt - 1 ? 2 : 4, tq,
+        paint_rect4(lds, rt, shift, C, P.pad, xmin, ymin, r.cx[i], r.cy[i], i < nt - 1 ? 2 : 4, tq,
                            CBEV_PX_ROUTE);
-    __syncthreads();
+    lds_barrier();
     for (int t = 0; t < q.ntl; ++t) {  // traffic lights one at a time (colours may differ)
       const int rx = r.ti[CBEV_TI_RX * r.T + t] - xmin, ry = r.ti[CBEV_TI_RY * r.T + t] - ymin;
       const int rw = r.ti[CBEV_TI_RW * r.T + t], rh = r.ti[CBEV_TI_RH * r.T + t];
@@ -1327,9 +1293,9 @@ __device__ __forceinline__ void raster_paint(const KArgs& K, const DRec& r, cons
       for (int qy = threadIdx.x >> 4; qy < rh; qy += NT / 16)
         for (int qx = threadIdx.x & 15; qx < rw; qx += 16) {
           const int px = rx + qx, py = ry + qy;
-          if (px >= 0 && py >= 0 && px < C && py < C) lds_set_texel<BYTES>(lds, py * rt + shift + px, col);
+          if (px >= 0 && py >= 0 && px < C && py < C) lds_set_texel(lds, py * rt + shift + px, col);
         }
-      __syncthreads();
+      lds_barrier();
     }
   }
 }
@@ -1372,74 +1338,105 @@ __device__ __forceinline__ void raster_rot(const KArgs& K, const DRec& r, Raster
 
 // Crop staging: 16-byte global loads of the nibble-packed map, lane-linear over
 // the window's row chunks (STAGE_U per thread in flight), then dword LDS stores.
-// Issue half (loads into registers) and commit half (LDS stores).
+// Only the rows and 32-texel chunks the output samples are staged: the
+// output -> crop map is affine, so the sampled texels lie in the bounding box of
+// the four output corners' source texels (fast path; the slow path, with
+// background / clipping tests, stages the whole crop). The image layout stays
+// the whole crop's, so the gathers are unchanged. Roads are axis-aligned, so
+// most headings sample about a 130 x 130 box of the 182 x 182 crop (S=128).
 #define STAGE_U 5
 struct StageBuf {
   uint4 v[STAGE_U];
 };
+struct StageWin {
+  int y0, ny, c0, nc;  // crop rows [y0, y0 + ny), row chunks [c0, c0 + nc)
+};
 template <int G>
-__device__ __forceinline__ int stage_total(const cbev_params& P) {
-  return P.crop * raster_row_chunks(64 * G, P.crop);
+__device__ __forceinline__ StageWin stage_window(const cbev_params& P, const RasterJob& J) {
+  const int C = P.crop;
+  const int nch = raster_row_chunks(64 * G, C);
+  StageWin w{0, C, 0, nch};
+  if (!J.fast) return w;
+  const RotSetup& R = J.R;
+  const int S = 64 * G;
+  int xl = 1 << 30, xh = -(1 << 30), yl = 1 << 30, yh = -(1 << 30);
+  const int rt = raster_row_texels(S, C);
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const int xx = ((c & 1) ? S - 1 : 0) - R.rx0, yy = ((c & 2) ? S - 1 : 0) - R.ry0;
+    int tx, ty;
+    if (R.r90) {  // LDS texel address without the shift: row * rt + column
+      const int a = R.a00 + xx * R.ustep + yy * R.vstep;
+      ty = a / rt;
+      tx = a - ty * rt;
+    } else {
+      tx = (R.dx00 + xx * R.icos - yy * R.isin) >> 16;
+      ty = (R.dy00 + xx * R.isin + yy * R.icos) >> 16;
+    }
+    xl = min(xl, tx);
+    xh = max(xh, tx);
+    yl = min(yl, ty);
+    yh = max(yh, ty);
+  }
+  xl = max(xl, 0);
+  yl = max(yl, 0);
+  xh = min(xh, C - 1);
+  yh = min(yh, C - 1);
+  w.y0 = yl;
+  w.ny = yh - yl + 1;
+  w.c0 = (J.shift + xl) >> 5;
+  w.nc = ((J.shift + xh) >> 5) - w.c0 + 1;
+  return w;
 }
 template <int G, int NT = 256>
-__device__ __forceinline__ void stage_issue(const KArgs& K, const RasterJob& J, int q0, StageBuf& b) {
-  const int C = K.P.crop;
-  const int nch = raster_row_chunks(64 * G, C), total = C * nch;
-  const uint8_t* gbase = K.map + (int64_t)J.ymin * K.npitch + J.xa;
-  const int dr = NT / nch, dj = NT - dr * nch;
+__device__ __forceinline__ void stage_issue(const KArgs& K, const RasterJob& J, const StageWin& W, int q0,
+                                            StageBuf& b) {
+  const int total = W.ny * W.nc;
+  const uint8_t* gbase = K.map + (int64_t)(J.ymin + W.y0) * K.npitch + J.xa + 16 * W.c0;
+  const int dr = NT / W.nc, dj = NT - dr * W.nc;
   const int q = q0 + (int)threadIdx.x;
-  int r = q / nch, c = q - r * nch;
+  int r = q / W.nc, c = q - r * W.nc;
 #pragma unroll
   for (int u = 0; u < STAGE_U; ++u) {
     if (q + NT * u < total) b.v[u] = load16_a4(gbase + (int64_t)r * K.npitch + 16 * c);
     r += dr;
     c += dj;
-    if (c >= nch) { c -= nch; ++r; }
+    if (c >= W.nc) { c -= W.nc; ++r; }
   }
 }
 template <int G, int NT = 256>
-__device__ __forceinline__ void stage_commit(const KArgs& K, int q0, const StageBuf& b, uint8_t* __restrict__ lds) {
-  constexpr bool BYTES = raster_bytes(64 * G);
+__device__ __forceinline__ void stage_commit(const KArgs& K, const StageWin& W, int q0, const StageBuf& b,
+                                             uint8_t* __restrict__ lds) {
   const int C = K.P.crop;
   const int sd = raster_stride_dwords(64 * G, C);
-  const int nch = raster_row_chunks(64 * G, C), total = C * nch;
-  const int dr = NT / nch, dj = NT - dr * nch;
+  const int total = W.ny * W.nc;
+  const int dr = NT / W.nc, dj = NT - dr * W.nc;
   const int q = q0 + (int)threadIdx.x;
-  int row = q / nch, j = q - row * nch;
-  uint32_t* l32 = (uint32_t*)lds;
+  int row = q / W.nc, jj = q - row * W.nc;
+  uint32_t* l32 = (uint32_t*)lds + W.y0 * sd;
 #pragma unroll
   for (int u = 0; u < STAGE_U; ++u) {
     if (q + NT * u < total) {
-      if (BYTES) {  // 32 texels -> 8 dwords; the last chunk of a row may overhang the stride
-        uint32_t* d = l32 + row * sd + 8 * j;
-        uint32_t o[8];
-        unpack_texels(b.v[u].x, o);
-        unpack_texels(b.v[u].y, o + 2);
-        unpack_texels(b.v[u].z, o + 4);
-        unpack_texels(b.v[u].w, o + 6);
-#pragma unroll
-        for (int k = 0; k < 8; ++k)
-          if (8 * j + k < sd) d[k] = o[k];
-      } else {
-        uint32_t* d = l32 + row * sd + 4 * j;
-        d[0] = b.v[u].x;  // the last chunk of a row may overhang the stride
-        if (4 * j + 1 < sd) d[1] = b.v[u].y;
-        if (4 * j + 2 < sd) d[2] = b.v[u].z;
-        if (4 * j + 3 < sd) d[3] = b.v[u].w;
-      }
+      const int j = W.c0 + jj;  // chunk of the row
+      uint32_t* d = l32 + row * sd + 4 * j;
+      d[0] = b.v[u].x;  // the last chunk of a row may overhang the stride
+      if (4 * j + 1 < sd) d[1] = b.v[u].y;
+      if (4 * j + 2 < sd) d[2] = b.v[u].z;
+      if (4 * j + 3 < sd) d[3] = b.v[u].w;
     }
     row += dr;
-    j += dj;
-    if (j >= nch) { j -= nch; ++row; }
+    jj += dj;
+    if (jj >= W.nc) { jj -= W.nc; ++row; }
   }
 }
 template <int G, int NT = 256>
 __device__ __forceinline__ void stage_all(const KArgs& K, const RasterJob& J, uint8_t* __restrict__ lds) {
-  const int total = stage_total<G>(K.P);
+  const StageWin W = stage_window<G>(K.P, J);
+  const int total = W.ny * W.nc;
   for (int q0 = 0; q0 < total; q0 += NT * STAGE_U) {
     StageBuf b;
-    stage_issue<G, NT>(K, J, q0, b);
-    stage_commit<G, NT>(K, q0, b, lds);
+    stage_issue<G, NT>(K, J, W, q0, b);
+    stage_commit<G, NT>(K, W, q0, b, lds);
   }
 }
 
@@ -1448,10 +1445,9 @@ __device__ __forceinline__ void stage_all(const KArgs& K, const RasterJob& J, ui
 template <int G, int NT = 256>
 __device__ __forceinline__ void raster_emit(const KArgs& K, const RasterJob& J, uint8_t* __restrict__ out, int nout,
                                             int64_t out_stride, const uint8_t* __restrict__ lds) {
-  constexpr bool BYTES = raster_bytes(64 * G);
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t bg = lds_texel<BYTES>(lds, J.shift);  // crop top-left pixel after painting
+  const uint32_t bg = lds_texel(lds, J.shift);  // crop top-left pixel after painting
   raster_out_dispatch<G, NT / 64>(K.P, J.R, J.fast, lds, J.shift, bg, out, nout, out_stride, lane, wave, K.fov);
 }
 
@@ -1473,15 +1469,15 @@ __device__ __forceinline__ void raster_reset_env(const KArgs& K, const DRec& r, 
 // paint in draw order, output. 8 waves at S=256, where the 68 KB crop image
 // leaves 2 workgroups per CU (4 waves each would leave the SIMDs half empty);
 // 4 waves below, where 8 workgroups share a CU. Measured alternatives (two envs
-// per workgroup with the next env's loads in flight, a persistent grid, a
-// column-block lane mapping, a byte image at S=128) are in DESIGN.md §3.
+// per workgroup with the next env's loads in flight, two crop images per
+// workgroup filled by LDS-DMA while the other is written out, a persistent
+// grid, a column-block lane mapping, a byte image at S=128) are in DESIGN.md §3.
 __host__ __device__ constexpr int raster_threads(int S) { return S >= 256 ? 512 : 256; }
 
 template <int G>
 __global__ __launch_bounds__(raster_threads(64 * G)) __attribute__((amdgpu_waves_per_eu(8))) void k_raster(
     KArgs K, uint8_t* __restrict__ recs, int n, uint8_t* __restrict__ frames) {
   extern __shared__ __align__(16) uint8_t lds[];
-  constexpr bool BYTES = raster_bytes(64 * G);
   constexpr int NT = raster_threads(64 * G);
   const int e = xcd_env_of_wg(blockIdx.x, n);
   if (e >= n) return;
@@ -1495,7 +1491,7 @@ __global__ __launch_bounds__(raster_threads(64 * G)) __attribute__((amdgpu_waves
   stage_all<G, NT>(K, J, lds);
   __syncthreads();
   CBEV_STAMP(2, 1);
-  raster_paint<BYTES, NT>(K, r, J.pq, J.xmin, J.ymin, J.shift, lds);
+  raster_paint<NT>(K, r, J.pq, J.xmin, J.ymin, J.shift, lds);
   CBEV_STAMP(2, 2);
   raster_emit<G, NT>(K, J, frames + (int64_t)e * SS, 1, 0, lds);
   CBEV_STAMP(2, 3);
@@ -2098,6 +2094,7 @@ __global__ __launch_bounds__(256) void k_ego(KArgs K, uint8_t* __restrict__ recs
   }
   __syncthreads();
   CBEV_STAMP(0, 3);
+  CBEV_STAMP(1, 0);
   // S5 (env k, element i) pairs: env k = tid / tpe, elements sub, sub + tpe, ...
   {
     const int hw = P.hero_w;
@@ -2217,7 +2214,7 @@ __global__ __launch_bounds__(256) void k_ego(KArgs K, uint8_t* __restrict__ recs
     }
   }
   __syncthreads();
-  CBEV_STAMP(1, 0);
+  CBEV_STAMP(1, 1);
   // S6
   if (tid < ne_eff) {
     const DRec r = rec(tid);
@@ -2225,10 +2222,10 @@ __global__ __launch_bounds__(256) void k_ego(KArgs K, uint8_t* __restrict__ recs
     collide_env(K, r, e0 + tid, cp, reward_out, term_out, trunc_out, cause_out, info_out);
   }
   __syncthreads();
-  CBEV_STAMP(1, 1);
+  CBEV_STAMP(1, 2);
   // S7
   ego_stage_out(lds, recs, e0, ne_eff, K, pk);
-  CBEV_STAMP(1, 2);
+  CBEV_STAMP(1, 3);
 }
 
 
@@ -2644,6 +2641,7 @@ static const void* reset_kernel(int size) {
 }
 static size_t raster_lds_bytes(const cbev_params& P) { return (size_t)raster_image_bytes(P.size, P.crop); }
 
+
 extern "C" {
 
 int cbev_abi_version(void) { return CBEV_ABI_VERSION; }
@@ -2848,10 +2846,11 @@ int cbev_step(cbev_ctx* c, void* records, int n, const void* actions, uint8_t* f
   if (ev) HIP_TRY(hipEventRecord(ev[2], s));
   {
     const size_t lb = raster_lds_bytes(c->P);
+    const int rg = n;
     switch (c->P.size) {
-      case 64: hipLaunchKernelGGL(k_raster<1>, dim3(n), dim3(raster_threads(64)), lb, s, K, (uint8_t*)records, n, frames); break;
-      case 128: hipLaunchKernelGGL(k_raster<2>, dim3(n), dim3(raster_threads(128)), lb, s, K, (uint8_t*)records, n, frames); break;
-      default: hipLaunchKernelGGL(k_raster<4>, dim3(n), dim3(raster_threads(256)), lb, s, K, (uint8_t*)records, n, frames); break;
+      case 64: hipLaunchKernelGGL(k_raster<1>, dim3(rg), dim3(raster_threads(64)), lb, s, K, (uint8_t*)records, n, frames); break;
+      case 128: hipLaunchKernelGGL(k_raster<2>, dim3(rg), dim3(raster_threads(128)), lb, s, K, (uint8_t*)records, n, frames); break;
+      default: hipLaunchKernelGGL(k_raster<4>, dim3(rg), dim3(raster_threads(256)), lb, s, K, (uint8_t*)records, n, frames); break;
     }
   }
   if (ev) HIP_TRY(hipEventRecord(ev[3], s));

@@ -1,4 +1,4 @@
-"""Phase timing of the staged thread-per-env kernels (k_hero, k_collide) from
+"""Phase timing of k_ego (and k_raster / k_actors) from
 in-kernel s_memtime stamps. Builds a -DCBEV_TIMING variant of libcbev.so into
 gpurun_out/, runs config-2 steps through bench.build_env and prints, per
 kernel, the mean cycles of stage-in / compute / write-back over workgroups and
@@ -55,7 +55,7 @@ xcc = buf[2 * NS * 4096 * 4:].reshape(NS, 4096).astype(np.int64)
 hwid = xcc >> 32
 xcc = xcc & 0xFFFFFFFF
 buf = buf[:2 * NS * 4096 * 4].reshape(2, NS, 4096, 4)
-for k, name in enumerate(("k_hero", "k_collide", "k_raster", "k_hero after P1 / P2 / A / B (slots 0-3)", "collide_env(thread0)", "k_collide pre-pass: segs/targets/actors+sync", "k_actors: behaviour / search / stanley+update (per wave)")):
+for k, name in enumerate(("k_ego A: stage-in / S1+S2 search / S3 chain + S4", "k_ego B: S5 collision pre-pass / S6 collide chain / stage-out", "k_raster", "-", "collide_env(thread0)", "-", "k_actors: behaviour / search / stanley+update (per wave)")):
     if not (buf[0, k, :, 0] > 0).any():
         continue
     st = buf[0, k].astype(np.int64)
