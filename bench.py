@@ -71,7 +71,7 @@ def make_actions(P, n, steps, seed0, offset):
     return out
 
 
-def build_env(cfgd, n, rank, device):
+def build_env(cfgd, n, rank, device, info_mode="none"):
     """Vector env with every env reset to its seeded scene (host scene-gen)."""
     from carlabev_env_amd.config import EnvConfig
     from carlabev_env_amd.host_reset import HostResetBuilder
@@ -81,7 +81,7 @@ def build_env(cfgd, n, rank, device):
     action_mode = "continuous" if cfgd["action"].startswith("continuous") else "discrete"
     cfg = EnvConfig(size=S, obs_size=(S, S), obs_mode=cfgd["obs_mode"], render_mode="rgb_array",
                     action_mode=action_mode, action_profile_id=cfgd["action"])
-    env = CarlaBEVVectorEnv({"env": cfg, "num_envs": n}, device=device, caps=cfgd["caps"], info_mode="none")
+    env = CarlaBEVVectorEnv({"env": cfg, "num_envs": n}, device=device, caps=cfgd["caps"], info_mode=info_mode)
     first = rank * n
     t0 = time.time()
     host = np.zeros((n, env.rb), np.uint8)
@@ -252,6 +252,8 @@ def main():
     ap.add_argument("--no-wire", action="store_true")
     ap.add_argument("--raster-reps", type=int, default=50, help="back-to-back k_raster launches timed for the roofline")
     ap.add_argument("--dry-run", action="store_true", help="CPU/gloo rehearsal of the N-rank path (no GPU, value null)")
+    ap.add_argument("--info-mode", default="none", choices=("none", "full"),
+                    help="full: device episode statistics + a StepInfos per step (not read), as step() returns")
     args = ap.parse_args()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -273,7 +275,7 @@ def main():
     cfgd = CONFIGS[args.config]
     n = args.envs or cfgd["envs"]
     from carlabev_env_amd._lib import check, lib
-    env, host_recs = build_env(cfgd, n, rank, device)
+    env, host_recs = build_env(cfgd, n, rank, device, args.info_mode)
     P = env.params
     total_steps = args.warmup + args.steps
     acts = torch.from_numpy(make_actions(P, n, total_steps, cfgd["act_seed"], rank * n)).to(device)
@@ -287,6 +289,7 @@ def main():
 
     def one_step(t, wire):
         env.step_async_only(acts[t])
+        env.step_infos()
         if gatherer is not None:  # config 4: frames + reward/cause/flags of every rank to rank 0, one RCCL gather
             gatherer.gather(env.frames(), env.reward, env.term, env.trunc, env.cause)
         env.reset_from_bank(mask=env.term)  # canonical loop: reset(reset_mask=terminated)
@@ -392,6 +395,7 @@ def main():
             "vs_baseline": None,
             "dtype": "f64 state / u8 frames",
             "data": "synthetic seeded scenes (host scene-gen on the Town01 class map), seeded action streams",
+            "info_mode": args.info_mode,
             "config": {"workload": cfgd["workload"], "config_id": args.config, "envs_per_gpu": n,
                        "global_envs": n * world, "obs_size": S, "obs_mode": cfgd["obs_mode"],
                        "parallelism": f"env-sharded x{world}" + (" + RCCL gather" if gather else "")},

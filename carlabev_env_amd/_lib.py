@@ -62,6 +62,14 @@ def lib():
     L.cbev_set_obs_size.restype = _I
     L.cbev_resize_obs.argtypes = [_P, _P, _I, _P, _I, _P, _I, _I64, _P]
     L.cbev_resize_obs.restype = _I
+    L.cbev_set_episode_stats.argtypes = [_P, _P, _I, _P, _P, _I]
+    L.cbev_set_episode_stats.restype = _I
+    L.cbev_episode_slot.argtypes = [_P, _P]
+    L.cbev_episode_slot.restype = _I
+    L.cbev_wall_clock_hz.argtypes = [_P, _P]
+    L.cbev_wall_clock_hz.restype = _I
+    L.cbev_error_flags.argtypes = [_P, _P, _I]
+    L.cbev_error_flags.restype = _I
     L.cbev_profile.argtypes = [_P, _I]
     L.cbev_profile.restype = _I
     L.cbev_profile_read.argtypes = [_P, _P, _P]
@@ -82,4 +90,7 @@ EXPORTED_SYMBOLS = ("cbev_abi_version", "cbev_params_size", "cbev_layout_of", "c
                     "cbev_create", "cbev_destroy", "cbev_set_map", "cbev_step", "cbev_reset", "cbev_bank_frames",
                     "cbev_reset_frames",
                     "cbev_expand_obs", "cbev_vector_obs", "cbev_set_fov_mask", "cbev_set_obs_size", "cbev_resize_obs", "cbev_profile", "cbev_profile_read",
-                    "cbev_profile_raster")
+                    "cbev_profile_raster", "cbev_error_flags", "cbev_set_episode_stats", "cbev_episode_slot",
+                    "cbev_wall_clock_hz")
+
+ERR_ACTION_INDEX = 1  # CBEV_ERR_ACTION_INDEX (include/cbev.h)

@@ -551,6 +551,7 @@ struct RotSetup {
 };
 
 static_assert(sizeof(RotSetup) == 4 * CBEV_RS_WORDS, "RotSetup must match the record's RS_* ints");
+static_assert(sizeof(cbev_episode_stats) == 1856, "cbev_episode_stats is part of the C-ABI (layout.STATS_BYTES)");
 
 __device__ __forceinline__ RotSetup rot_setup(const cbev_params& P, float angle, int sb) {
   RotSetup R;
@@ -768,8 +769,16 @@ __device__ __forceinline__ void d_store_render_setup(const cbev_params& P, int32
 __device__ __forceinline__ void d_decode_action(const KArgs& K, const void* __restrict__ actions, int e, float* g,
                                                 float* sa, float* b) {
   if (K.P.action_kind == 0) {
+    // discrete_actions[int(action)]: Python's negative indices count from the
+    // end; anything else out of range is the reference's IndexError, reported
+    // through the context's error word (cbev_error_flags) and stepped as action 0
     int idx = ((const int32_t*)actions)[e];
-    idx = idx < 0 ? 0 : (idx >= K.P.n_discrete ? K.P.n_discrete - 1 : idx);
+    const int nd = K.P.n_discrete;
+    if (idx < 0) idx += nd;
+    if (idx < 0 || idx >= nd) {
+      atomicOr(K.err, CBEV_ERR_ACTION_INDEX);
+      idx = 0;
+    }
     *g = K.P.action_table[idx][0];
     *sa = K.P.action_table[idx][1];
     *b = K.P.action_table[idx][2];
@@ -1535,6 +1544,7 @@ __global__ __launch_bounds__(256) void k_reset(KArgs K, uint8_t* __restrict__ re
         uint4* d4 = (uint4*)dst;
         for (int64_t i = threadIdx.x; i < rb / 16; i += 256) d4[i] = s4[i];
       }
+      if (K.stats != nullptr && threadIdx.x == 0) K.stats[e].t0 = (double)wall_clock64();  // episode start
       DRec r = bind_rec((uint8_t*)src, K.L, K.C);  // read-only use below
       raster_reset_env<G>(K, r, ring + (int64_t)e * SS, n_frames, (int64_t)n * SS, lds);
       __syncthreads();  // the LDS image is reused by the next env
@@ -1613,6 +1623,7 @@ __global__ __launch_bounds__(256) void k_reset_copy(KArgs K, uint8_t* __restrict
         } else {
           const int64_t i = (int64_t)(c - pf) * 256 + threadIdx.x;  // uint4 index in the record
           if (i < rb / 16) ((uint4*)(recs + (int64_t)e * rb))[i] = ((const uint4*)(bank + (int64_t)b * rb))[i];
+          if (c == pf && threadIdx.x == 0 && K.stats != nullptr) K.stats[e].t0 = (double)wall_clock64();
         }
       }
     }
@@ -1724,6 +1735,81 @@ __device__ __forceinline__ CollPre coll_reduce_serial(const uint8_t* sk, const C
   p.tile = ints[CS_TILE];
   (void)nraw;
   return p;
+}
+
+// ---- episode statistics (Stats, stats.py:87-148) on the device
+// double-double accumulation: (hi, lo) += x with TwoSum, so the window sum of
+// up to CBEV_STATS_HIST returns is kept to ~2^-100 relative and an evicted
+// return leaves no drift
+__device__ __forceinline__ void d_dd_add(double& hi, double& lo, double x) {
+  const double s = hi + x;
+  const double bp = s - hi;
+  const double err = (hi - (s - bp)) + (x - bp);
+  const double t = lo + err;
+  hi = s + t;
+  lo = t - (hi - s);
+}
+__device__ __forceinline__ void d_stats_count(cbev_episode_stats* st, int cause, int d) {
+  if (cause == CBEV_CAUSE_SUCCESS) st->n_success += d;
+  else if (cause == CBEV_CAUSE_COLLISION) st->n_collision += d;
+  else if (cause == CBEV_CAUSE_OFF_ROAD) st->n_offroad += d;
+}
+// At termination (CarlaBEV._check_termination, carlabev.py:177-185): the
+// summary Stats.terminated() returns (get_episode_info over the window BEFORE
+// this episode, stats.py:106-148) + num_vehicles / len_ego_route + the
+// episode's elapsed device-clock time, as one row of this step's table; then
+// the episode enters the window (history.append, maxlen 200).
+__device__ __forceinline__ void d_episode_summary(const KArgs& K, const DRec& r, int e) {
+  cbev_episode_stats* st = K.stats + e;
+  const double* hd = r.hd;
+  const int32_t* hi = r.hi;
+  const int len = hi[CBEV_HI_EP_LEN];
+  const double n = len > 0 ? (double)len : 1.0;
+  const int cause = hi[CBEV_HI_CAUSE];
+  const int wn = st->n;
+  double row[CBEV_EP_COUNT];
+  row[CBEV_EP_ENV] = (double)e;
+  row[CBEV_EP_EPISODE] = (double)st->episode;
+  row[CBEV_EP_CAUSE] = (double)cause;
+  row[CBEV_EP_RETURN] = hd[CBEV_HD_EP_RETURN];
+  row[CBEV_EP_LENGTH] = (double)len;
+  row[CBEV_EP_MEAN_REWARD] = wn > 0 ? (st->sum_hi + st->sum_lo) / wn : 0.0;
+  row[CBEV_EP_SUCCESS_RATE] = wn > 0 ? (double)st->n_success / wn : 0.0;
+  row[CBEV_EP_COLLISION_RATE] = wn > 0 ? (double)st->n_collision / wn : 0.0;
+  row[CBEV_EP_UNFINISHED_RATE] = wn > 0 ? (double)st->n_offroad / wn : 0.0;
+  row[CBEV_EP_MEAN_SPEED] = hd[CBEV_HD_EP_SPEED] / n;
+  row[CBEV_EP_MEAN_TTC] = 0.0;       // info["reward"] never carries "ttc" (stats.py:42-46)
+  row[CBEV_EP_MEAN_PROGRESS] = 0.0;  // ... nor "progress"
+  row[CBEV_EP_MEAN_ABS_AL] = hd[CBEV_HD_EP_ABS_AL] / n;
+  row[CBEV_EP_MEAN_ABS_ALAT] = hd[CBEV_HD_EP_ABS_ALAT] / n;
+  row[CBEV_EP_MEAN_ABS_JL] = hd[CBEV_HD_EP_ABS_JL] / n;
+  row[CBEV_EP_MEAN_ABS_JLAT] = hd[CBEV_HD_EP_ABS_JLAT] / n;
+  row[CBEV_EP_MEAN_ABS_YR] = hd[CBEV_HD_EP_ABS_YR] / n;
+  row[CBEV_EP_MEAN_ABS_YACC] = hd[CBEV_HD_EP_ABS_YACC] / n;
+  row[CBEV_EP_VIOL_RATE] = hd[CBEV_HD_EP_VIOL] / n;
+  row[CBEV_EP_HARSH_RATE] = hd[CBEV_HD_EP_HARSH] / n;
+  row[CBEV_EP_NUM_VEH] = hd[CBEV_HD_NUM_VEH];
+  row[CBEV_EP_LEN_ROUTE_M] = hd[CBEV_HD_LEN_ROUTE_M];
+  row[CBEV_EP_SECONDS] = (double)(wall_clock64() - (uint64_t)st->t0) * K.tick_s;
+  row[CBEV_EP_CTX_ID] = (double)hi[CBEV_HI_CTX_ID];
+  const int slot = atomicAdd(K.ep_count, 1);
+  double* o = K.ep_rows + (int64_t)slot * CBEV_EP_COUNT;
+#pragma unroll
+  for (int k = 0; k < CBEV_EP_COUNT; ++k) o[k] = row[k];
+  // history.append(current), deque(maxlen=200)
+  const int h = st->head;
+  if (wn == CBEV_STATS_HIST) {
+    d_dd_add(st->sum_hi, st->sum_lo, -st->ret[h]);
+    d_stats_count(st, st->cause[h], -1);
+  } else {
+    st->n = wn + 1;
+  }
+  st->ret[h] = hd[CBEV_HD_EP_RETURN];
+  st->cause[h] = (uint8_t)cause;
+  d_dd_add(st->sum_hi, st->sum_lo, hd[CBEV_HD_EP_RETURN]);
+  d_stats_count(st, cause, 1);
+  st->head = h + 1 == CBEV_STATS_HIST ? 0 : h + 1;
+  st->episode += 1;
 }
 
 // One thread per env for the float64 scalar chain; the element loops come
@@ -1937,6 +2023,7 @@ __device__ __forceinline__ void collide_env(const KArgs& K, DRec r, int e, const
   hi[CBEV_HI_TERM] = terminal;
   hi[CBEV_HI_TRUNC] = terminal && cause == CBEV_CAUSE_MAX_ACTIONS;
   hi[CBEV_HI_STEP] += 1;
+  if (terminal && K.stats != nullptr) d_episode_summary(K, r, e);
   reward_out[e] = reward;
   term_out[e] = (uint8_t)terminal;
   trunc_out[e] = (uint8_t)(terminal && cause == CBEV_CAUSE_MAX_ACTIONS);
@@ -1994,6 +2081,7 @@ __global__ __launch_bounds__(256) void k_ego(KArgs K, uint8_t* __restrict__ recs
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   auto rec = [&](int k) { return bind_ego(lds + k * pk.bytes, recs + (int64_t)(e0 + k) * rb, K, pk); };
+  if (blockIdx.x == 0 && tid == 0 && K.ep_count_next != nullptr) *K.ep_count_next = 0;
   CBEV_STAMP(0, 0);
   // S0 (wave 0 runs the chain, wave 1 the steering tangent)
   float ag = 0.f, asa = 0.f, ab = 0.f;
@@ -2528,6 +2616,13 @@ struct cbev_ctx {
   void* area_dev;     // INTER_AREA tables of cbev_set_obs_size
   AreaTab area;
   uint8_t* fov_dev;   // cbev_set_fov_mask
+  int32_t* err_dev;   // CBEV_ERR_* bits set by the kernels
+  cbev_episode_stats* stats;  // cbev_set_episode_stats (caller-owned device buffers)
+  double* ep_rows;
+  int32_t* ep_counts;
+  int ep_ring, ep_n;
+  int64_t step_count;         // cbev_step calls since cbev_set_episode_stats
+  double tick_s;
 };
 
 // Envs per k_ego workgroup: small groups spread the record staging (LDS-DMA
@@ -2622,6 +2717,11 @@ static KArgs kargs(const cbev_ctx* c) {
   K.map = c->map_dev;
   K.npitch = c->npitch;
   K.fov = (const uint32_t*)c->fov_dev;
+  K.err = c->err_dev;
+  K.stats = c->stats;
+  K.ep_rows = nullptr;
+  K.ep_count = K.ep_count_next = nullptr;
+  K.tick_s = c->tick_s;
   return K;
 }
 
@@ -2705,6 +2805,13 @@ int cbev_create(const cbev_params* params, const cbev_caps* caps, int device, cb
   build_sg_tables(&T);
   hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(c_sg), &T, sizeof T);
   if (e == hipSuccess) e = hipMalloc(&c->lut_dev, 64 * sizeof(uint32_t));
+  if (e == hipSuccess) e = hipMalloc(&c->err_dev, sizeof(int32_t));
+  if (e == hipSuccess) e = hipMemset(c->err_dev, 0, sizeof(int32_t));
+  if (e == hipSuccess) {
+    int khz = 0;  // wall_clock64() rate
+    e = hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device);
+    c->tick_s = khz > 0 ? 1.0 / (1000.0 * khz) : 0.0;
+  }
   if (e == hipSuccess) {
     const uint32_t pal[16] = CBEV_PALETTE_RGB;
     e = hipMemcpyToSymbol(HIP_SYMBOL(c_palette_rgb), pal, sizeof pal);
@@ -2724,6 +2831,39 @@ int cbev_create(const cbev_params* params, const cbev_caps* caps, int device, cb
     return set_err(CBEV_EHIP, "cbev_create: %s", hipGetErrorString(e));
   }
   *out = c;
+  return CBEV_OK;
+}
+
+int cbev_set_episode_stats(cbev_ctx* c, void* stats, int n, double* rows, int32_t* counts, int ring) {
+  if (!c) return set_err(CBEV_EINVAL, "null argument");
+  if (stats && (!rows || !counts || ring < 3 || n <= 0))
+    return set_err(CBEV_EINVAL, "episode stats need rows, counts and a ring of at least 3 slots");
+  c->stats = (cbev_episode_stats*)stats;
+  c->ep_rows = rows;
+  c->ep_counts = counts;
+  c->ep_ring = stats ? ring : 0;
+  c->ep_n = stats ? n : 0;
+  c->step_count = 0;
+  return CBEV_OK;
+}
+
+int cbev_episode_slot(const cbev_ctx* c, int64_t* step_count) {
+  if (!c) return -1;
+  if (step_count) *step_count = c->step_count;
+  return c->ep_ring > 0 ? (int)((c->step_count + c->ep_ring - 1) % c->ep_ring) : -1;
+}
+
+int cbev_wall_clock_hz(const cbev_ctx* c, double* hz) {
+  if (!c || !hz) return set_err(CBEV_EINVAL, "null argument");
+  *hz = c->tick_s > 0 ? 1.0 / c->tick_s : 0.0;
+  return CBEV_OK;
+}
+
+int cbev_error_flags(cbev_ctx* c, int32_t* flags, int clear) {
+  if (!c || !flags) return set_err(CBEV_EINVAL, "null argument");
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipMemcpy(flags, c->err_dev, sizeof(int32_t), hipMemcpyDeviceToHost));
+  if (clear && *flags) HIP_TRY(hipMemset(c->err_dev, 0, sizeof(int32_t)));
   return CBEV_OK;
 }
 
@@ -2796,6 +2936,7 @@ void cbev_destroy(cbev_ctx* c) {
   }
   if (c->map_dev) (void)hipFree(c->map_dev);
   if (c->lut_dev) (void)hipFree(c->lut_dev);
+  if (c->err_dev) (void)hipFree(c->err_dev);
   if (c->area_dev) (void)hipFree(c->area_dev);
   if (c->fov_dev) (void)hipFree(c->fov_dev);
   free(c);
@@ -2841,6 +2982,14 @@ int cbev_step(cbev_ctx* c, void* records, int n, const void* actions, uint8_t* f
   if (ev) HIP_TRY(hipEventRecord(ev[0], s));
   if (c->C.actor_cap > 0) hipLaunchKernelGGL(actors_kernel(c->C), dim3(wg4), dim3(256), 0, s, K, (uint8_t*)records, n);
   if (ev) HIP_TRY(hipEventRecord(ev[1], s));
+  if (c->stats) {
+    if (n > c->ep_n) return set_err(CBEV_EINVAL, "n %d exceeds the %d envs of the episode stats", n, c->ep_n);
+    const int slot = (int)(c->step_count % c->ep_ring), next = (slot + 1) % c->ep_ring;
+    K.ep_rows = c->ep_rows + (int64_t)slot * c->ep_n * CBEV_EP_COUNT;
+    K.ep_count = c->ep_counts + slot;
+    K.ep_count_next = c->ep_counts + next;
+    c->step_count += 1;
+  }
   hipLaunchKernelGGL(k_ego, dim3((n + c->ego_ne - 1) / c->ego_ne), dim3(256), (size_t)c->ego_lb, s, K,
                      (uint8_t*)records, n, actions, reward, term, trunc, cause, info, c->ego_ne);
   if (ev) HIP_TRY(hipEventRecord(ev[2], s));

@@ -26,6 +26,13 @@ struct KArgs {
                        // texel x of a row in byte x >> 1, high nibble when x is odd
   int npitch;
   const uint32_t* fov;  // FOV corner mask, S*S bytes (0xff = black), or null (fov_masked off)
+  int32_t* err;         // device error word (CBEV_ERR_* bits, read by cbev_error_flags)
+  // episode statistics (cbev_set_episode_stats; null: off)
+  cbev_episode_stats* stats;  // [n] per env, kept across episodes
+  double* ep_rows;            // this step's summary rows [n][CBEV_EP_COUNT], first *ep_count used
+  int32_t* ep_count;          // this step's row count (zeroed by the step before)
+  int32_t* ep_count_next;     // the next step's row count, zeroed by this step
+  double tick_s;              // seconds per wall_clock64() tick
 };
 
 // class id of padded-map texel (x, y)

@@ -36,7 +36,7 @@ def _parse_fields(text: str, group: str) -> list[str]:
 def _load_names():
     with open(HEADER, "r", encoding="utf-8") as f:
         text = f.read()
-    return {g: _parse_fields(text, g) for g in ("HD", "HI", "AD", "AI", "TI")}
+    return {g: _parse_fields(text, g) for g in ("HD", "HI", "AD", "AI", "TI", "EP")}
 
 
 NAMES = _load_names()
@@ -45,6 +45,8 @@ HI = {n: i for i, n in enumerate(NAMES["HI"])}
 AD = {n: i for i, n in enumerate(NAMES["AD"])}
 AI = {n: i for i, n in enumerate(NAMES["AI"])}
 TI = {n: i for i, n in enumerate(NAMES["TI"])}
+EP = {n: i for i, n in enumerate(NAMES["EP"])}  # episode summary row columns (CBEV_EP_FIELDS)
+STATS_BYTES = 1856                              # sizeof(cbev_episode_stats)
 
 # enums mirrored from the header (values are part of the C-ABI)
 BEH = {"none": 0, "timed_brake": 1, "cross": 2, "stop_mid": 3, "yield_return": 4}

@@ -22,8 +22,9 @@ from __future__ import annotations
 
 import ctypes
 import os
-import time
+import weakref
 from collections import deque
+from collections.abc import Mapping
 
 import numpy as np
 import torch
@@ -32,7 +33,7 @@ from . import layout as LY
 from ._lib import check, lib
 from .config import EnvConfig, RunConfig, validate_run_config, get_action_profile_spec
 from .params import CbevParams, build_params, load_class_map, padded_map
-from .host_reset import HostResetBuilder, route_length_m
+from .host_reset import HostResetBuilder
 from .scene_gen import SceneGenerator
 from .semantics import gray_lut, rgb_lut, semantic_lut, semantic_mask_channels, PALETTE
 from . import obs_pipeline as OP
@@ -46,24 +47,86 @@ def _ptr(t: torch.Tensor | None):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else None
 
 
-class _EpisodeHistory:
-    """Per-env mirror of `Stats` history (stats.py:87-125), updated only at termination."""
+# episode_info keys (Stats.get_episode_info, stats.py:127-148, + carlabev.py:180-181)
+# -> summary row column (include/cbev_layout.h CBEV_EP_FIELDS) and the Python
+# type of the reference's value, which sets the batched array's dtype the way
+# SyncVectorEnv._add_info does (int -> int64, float -> float64, str -> object)
+_EP_KEYS = (("episode", "EPISODE", int), ("termination", "CAUSE", str), ("return", "RETURN", float),
+            ("length", "LENGTH", int), ("mean_reward", "MEAN_REWARD", float),
+            ("success_rate", "SUCCESS_RATE", float), ("collision_rate", "COLLISION_RATE", float),
+            ("unfinished_rate", "UNFINISHED_RATE", float), ("mean_speed", "MEAN_SPEED", float),
+            ("mean_ttc", "MEAN_TTC", float), ("mean_progress", "MEAN_PROGRESS", float),
+            ("mean_abs_accel_long", "MEAN_ABS_AL", float), ("mean_abs_accel_lat", "MEAN_ABS_ALAT", float),
+            ("mean_abs_jerk_long", "MEAN_ABS_JL", float), ("mean_abs_jerk_lat", "MEAN_ABS_JLAT", float),
+            ("mean_abs_yaw_rate", "MEAN_ABS_YR", float), ("mean_abs_yaw_acc", "MEAN_ABS_YACC", float),
+            ("comfort_violation_rate", "VIOL_RATE", float), ("harsh_brake_rate", "HARSH_RATE", float),
+            ("num_vehicles", "NUM_VEH", int), ("len_ego_route", "LEN_ROUTE_M", float))
+EP_RING = 8  # device slots of per-step episode rows (cbev_set_episode_stats)
 
-    def __init__(self, maxlen: int = 200):
-        self.causes = deque(maxlen=maxlen)
-        self.returns = deque(maxlen=maxlen)
-        self.episode = 0
+
+def _batched(values: dict, n: int) -> dict:
+    """{key: {env: value}} -> SyncVectorEnv._add_info's arrays + "_key" masks."""
+    out = {}
+    for key, per_env in values.items():
+        first = next(iter(per_env.values()))
+        if isinstance(first, (bool, int, float, np.number)) and not isinstance(first, bool):
+            arr = np.zeros(n, dtype=np.int64 if isinstance(first, (int, np.integer)) else np.float64)
+        elif isinstance(first, bool):
+            arr = np.zeros(n, dtype=np.bool_)
+        else:
+            arr = np.full(n, None, dtype=object)
+        mask = np.zeros(n, dtype=np.bool_)
+        for i, v in per_env.items():
+            arr[i] = v
+            mask[i] = True
+        out[key], out[f"_{key}"] = arr, mask
+    return out
+
+
+class StepInfos(Mapping):
+    """`infos` of one step() in info_mode="full": the vector-env dict the
+    reference returns ({} or {"episode_info": ..., "_episode_info": mask,
+    "episode": ..., "_episode": mask}), built from the device's episode rows the
+    first time it is read. Not reading it costs no host work and no sync."""
+
+    __slots__ = ("_env", "_step", "_event", "_d", "__weakref__")
+
+    def __init__(self, env, step: int, event):
+        self._env, self._step, self._event, self._d = env, step, event, None
+
+    def _get(self) -> dict:
+        if self._d is None:
+            self._d = self._env._materialize_infos(self._step, self._event)
+            self._env = self._event = None
+        return self._d
+
+    def __getitem__(self, key):
+        return self._get()[key]
+
+    def __iter__(self):
+        return iter(self._get())
+
+    def __len__(self):
+        return len(self._get())
+
+    def __repr__(self):
+        return repr(self._get())
 
 
 class CarlaBEVVectorEnv:
     metadata = {"autoreset_mode": "disabled", "render_modes": ["rgb_array"], "render_fps": 60}
 
     def __init__(self, cfg, *, num_envs: int | None = None, device=None, caps: dict | None = None,
-                 info_mode: str = "full", scene_generator=None, wrappers: bool = True):
+                 info_mode: str = "full", scene_generator=None, wrappers: bool = True, copy_obs: bool = True):
         """wrappers=False gives the base `CarlaBEV` observation of every env, as a
         `SyncVectorEnv` of unwrapped `CarlaBEV(cfg)` would: (S, S, 3) uint8 RGB for the
         BEV modes, float32[7] for obs_mode="vector" (carlabev.py:233-244, spaces.py:54-61).
-        The reference only allows "vector" on the bare env (config/env.py:310-314)."""
+        The reference only allows "vector" on the bare env (config/env.py:310-314).
+
+        copy_obs=True (default) returns a fresh observation tensor from every step() /
+        reset(), as SyncVectorEnv(copy=True) returns fresh arrays; copy_obs=False returns
+        the env's own buffer, which the next step() / reset() overwrites in place
+        (throughput loops that consume obs before stepping again)."""
         if isinstance(cfg, RunConfig):
             raw = cfg
         elif isinstance(cfg, dict) and "env" in cfg:
@@ -73,6 +136,7 @@ class CarlaBEVVectorEnv:
         run = validate_run_config(raw) if wrappers else (
             raw if isinstance(raw, RunConfig) else RunConfig.model_validate(dict(raw)))
         self.wrappers = bool(wrappers)
+        self.copy_obs = bool(copy_obs)
         self.run_cfg = run
         self.cfg: EnvConfig = run.env
         self.num_envs = int(num_envs if num_envs is not None else run.num_envs)
@@ -158,11 +222,20 @@ class CarlaBEVVectorEnv:
         self.single_action_space.seed(seed)
         self.generator = scene_generator or SceneGenerator(self.cfg, self.cfg.map_name)
         self.builder = HostResetBuilder(self.cfg, self.classes, self.params, self.layout, self.generator)
-        self.history = [_EpisodeHistory() for _ in range(N)]
         self.scene_context = [dict() for _ in range(N)]
-        self.num_vehicles = np.zeros(N, dtype=np.int64)
-        self.len_ego_route = np.zeros(N, dtype=np.float64)
-        self._t0 = np.full(N, time.perf_counter())
+        # scenario contexts by id (records carry CTX_ID): bank rows' ids stay, an env's
+        # host-reset id is released at its next host reset
+        self._ctx_table: dict[int, dict] = {0: {}}
+        self._ctx_next = 1
+        self._env_ctx = np.zeros(N, dtype=np.int64)
+        self._pending: deque = deque()  # (step, weakref(StepInfos)) not yet read
+        self._ep_step = 0
+        if info_mode == "full":  # Stats on the device (cbev_set_episode_stats)
+            self._ep_stats = torch.zeros((N, LY.STATS_BYTES), dtype=torch.uint8, device=dev)
+            self._ep_rows = torch.zeros((EP_RING, N, len(LY.EP)), dtype=torch.float64, device=dev)
+            self._ep_counts = torch.zeros(EP_RING, dtype=torch.int32, device=dev)
+            check(L.cbev_set_episode_stats(ctx, _ptr(self._ep_stats), N, _ptr(self._ep_rows), _ptr(self._ep_counts),
+                                           EP_RING), "cbev_set_episode_stats")
         self.bank = None
         self._bank_cursor = 0
         self.auto_obs = True  # reset_from_bank also expands the wire observation
@@ -202,11 +275,20 @@ class CarlaBEVVectorEnv:
         check(lib().cbev_bank_frames(self._ctx, _ptr(self.bank), B, _ptr(self.bank_frames), self._stream()),
               "cbev_bank_frames")
 
+    def _new_ctx_id(self, ctx: dict) -> int:
+        cid = self._ctx_next
+        self._ctx_next += 1
+        self._ctx_table[cid] = ctx
+        return cid
+
     def build_bank(self, seeds, options: dict | None = None) -> torch.Tensor:
+        """B seeded scenes as device records; each carries its scene scalars and the
+        id of its scenario context, so a bank reset reports them in episode_info."""
         options = dict(options or {})
         host = self._new_record_buffer(len(seeds))
         for k, s in enumerate(seeds):
-            self.build_reset_record(host[k], s, dict(options, scene_seed=int(s)))
+            _, _, ctx = self.build_reset_record(host[k], s, dict(options, scene_seed=int(s)))
+            LY.RecordView(host[k], self.layout).hi[LY.HI["CTX_ID"]] = self._new_ctx_id(ctx)
         return torch.from_numpy(host).to(self.device)
 
     def reset_from_bank(self, mask: torch.Tensor | None = None, bank_idx: torch.Tensor | None = None):
@@ -219,8 +301,16 @@ class CarlaBEVVectorEnv:
         if bank_idx is None:
             offset = self._bank_cursor
             self._bank_cursor = (self._bank_cursor + N) % B
-        if mask is not None and (mask.dtype != torch.uint8 or mask.device != self.device):
-            mask = mask.to(device=self.device, dtype=torch.uint8)
+        else:  # the kernels read N int32 bank rows on this device
+            bank_idx = torch.as_tensor(bank_idx)
+            if bank_idx.numel() != N:
+                raise ValueError(f"bank_idx has {bank_idx.numel()} entries, expected {N}")
+            bank_idx = bank_idx.reshape(N).to(device=self.device, dtype=torch.int32).contiguous()
+        if mask is not None:
+            mask = torch.as_tensor(mask)
+            if mask.numel() != N:
+                raise ValueError(f"reset mask has {mask.numel()} entries, expected {N}")
+            mask = mask.reshape(N).to(device=self.device, dtype=torch.uint8).contiguous()
         if self.resize:
             check(lib().cbev_reset_frames(self._ctx, _ptr(self.records), N, _ptr(self.bank), B, _ptr(mask),
                                           _ptr(bank_idx), offset, _ptr(self.bank_frames), _ptr(self.full), 1,
@@ -230,7 +320,10 @@ class CarlaBEVVectorEnv:
             check(lib().cbev_reset_frames(self._ctx, _ptr(self.records), N, _ptr(self.bank), B, _ptr(mask),
                                           _ptr(bank_idx), offset, _ptr(self.bank_frames), _ptr(self.ring), self.F,
                                           self._stream()), "cbev_reset_frames")
-        return self._obs() if self.auto_obs else None
+        if not self.auto_obs:
+            return None
+        obs = self._obs()
+        return obs.clone() if self.copy_obs else obs
 
     def _resize_into_ring(self, mask: torch.Tensor | None, all_slots: bool):
         """ResizeObservation + the mask/grayscale colour test of self.full into the ring:
@@ -255,13 +348,17 @@ class CarlaBEVVectorEnv:
         idx = np.flatnonzero(mask)
         host = self._new_record_buffer(max(len(idx), 1))
         spawn_infos = []
+        self._flush_pending(all_=True)  # contexts released below may still be read
         for k, i in enumerate(idx):
             info, spec, ctx = self.builder.build(host[k], seeds[i], options)
             spawn_infos.append(info)
             self.scene_context[i] = ctx
-            self.num_vehicles[i] = len(spec.vehicles)
-            self.len_ego_route[i] = route_length_m(spec)
-            self._t0[i] = time.perf_counter()
+            old = int(self._env_ctx[i])
+            if old:
+                self._ctx_table.pop(old, None)
+            cid = self._new_ctx_id(ctx)
+            self._env_ctx[i] = cid
+            LY.RecordView(host[k], self.layout).hi[LY.HI["CTX_ID"]] = cid
         if len(idx):
             staging = torch.from_numpy(host[:len(idx)]).to(self.device)
             bank_idx = np.zeros(N, dtype=np.int32)
@@ -276,6 +373,8 @@ class CarlaBEVVectorEnv:
                 check(lib().cbev_reset(self._ctx, _ptr(self.records), N, _ptr(staging), len(idx), _ptr(m), _ptr(bidx),
                                        0, _ptr(self.ring), self.F, self._stream()), "cbev_reset")
         obs = self._obs()
+        if self.copy_obs:
+            obs = obs.clone()
         infos = {}
         if len(idx):
             infos["spawn_validation"] = np.array([None] * N, dtype=object)
@@ -290,7 +389,14 @@ class CarlaBEVVectorEnv:
     def _actions_tensor(self, actions) -> torch.Tensor:
         if isinstance(actions, torch.Tensor) and actions.device == self.device and actions.is_contiguous() and (
                 actions.dtype == (torch.int32 if self.discrete else torch.float32)):
-            return actions
+            return actions  # device indices out of range set CBEV_ERR_ACTION_INDEX (errors())
+        if self.discrete and not (isinstance(actions, torch.Tensor) and actions.device.type != "cpu"):
+            # host actions: the reference's discrete_actions[int(action)] IndexError (spaces.py:46)
+            n = self.single_action_space.n
+            a_np = np.asarray(actions.cpu() if isinstance(actions, torch.Tensor) else actions).reshape(-1)
+            bad = (a_np < -n) | (a_np >= n)
+            if bad.any():
+                raise IndexError(f"discrete action {a_np[bad][0]} out of range for Discrete({n})")
         a = torch.as_tensor(actions, device=self.device)
         if self.discrete:
             a = a.reshape(self.num_envs).to(torch.int32).contiguous()
@@ -301,6 +407,9 @@ class CarlaBEVVectorEnv:
     def step_async_only(self, actions):
         """Enqueue one step; returns nothing and never synchronises (bench path)."""
         a = self._actions_tensor(actions)
+        if self.info_mode == "full":
+            self._flush_pending()
+            self._ep_step += 1
         self.head = (self.head + 1) % self.F
         frames = self.full if self.resize else self.ring[self.head]
         check(lib().cbev_step(self._ctx, _ptr(self.records), self.num_envs, _ptr(a), _ptr(frames), _ptr(self.reward),
@@ -310,13 +419,23 @@ class CarlaBEVVectorEnv:
             self._resize_into_ring(None, all_slots=False)
         return a
 
+    def errors(self, clear: bool = True) -> int:
+        """CBEV_ERR_* bits the kernels raised since the last call (synchronises the
+        device): ERR_ACTION_INDEX = a device action tensor held a discrete index outside
+        [-n, n), the reference's IndexError; that env stepped action 0."""
+        flags = ctypes.c_int32()
+        check(lib().cbev_error_flags(self._ctx, ctypes.byref(flags), 1 if clear else 0), "cbev_error_flags")
+        return int(flags.value)
+
     def step(self, actions):
         self.step_async_only(actions)
         obs = self._obs()
+        if self.copy_obs:
+            obs = obs.clone()
         rew = self.reward.clone()
         term = self.term.bool()
         trunc = self.trunc.bool()
-        infos = self._step_infos(term) if self.info_mode == "full" else {}
+        infos = self.step_infos()
         if self.info_mode == "device":
             infos = {"cause": self.cause.clone(), "comfort": self.info[:, :11].clone()}
         return obs, rew, term, trunc, infos
@@ -336,55 +455,62 @@ class CarlaBEVVectorEnv:
                                     self._stream()), "cbev_expand_obs")
         return self.obs_buf
 
-    def _step_infos(self, term: torch.Tensor) -> dict:
-        done = term.to("cpu").numpy()
-        if not done.any():
+    def step_infos(self):
+        """`infos` of the step just queued: a StepInfos (info_mode="full"), read
+        from the device only when accessed; {} otherwise."""
+        if self.info_mode != "full":
             return {}
-        idx = np.flatnonzero(done)
-        rec = self.records[torch.from_numpy(idx).to(self.device)].to("cpu").numpy()
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.device))
+        infos = StepInfos(self, self._ep_step - 1, ev)
+        self._pending.append((self._ep_step - 1, weakref.ref(infos)))
+        return infos
+
+    def _flush_pending(self, all_: bool = False):
+        """Read the StepInfos whose device rows the next step would recycle (or all,
+        all_=True) if the caller still holds them; forget the rest."""
+        limit = self._ep_step + 1 - EP_RING  # step self._ep_step zeroes the slot of this step
+        while self._pending and (all_ or self._pending[0][0] <= limit):
+            _, ref = self._pending.popleft()
+            obj = ref()
+            if obj is not None:
+                obj._get()
+
+    def _materialize_infos(self, step: int, event) -> dict:
+        """Vector-env infos of `step` from its device rows (SyncVectorEnv._add_info
+        layout: {"episode_info": {key: array, "_key": mask}, "_episode_info": mask,
+        "episode": {"r", "l", "t"} + masks, "_episode": mask}; {} when no env
+        terminated). The scenario context is merged as carlabev.py:181-182 does."""
+        event.synchronize()
+        slot = step % EP_RING
+        cnt = int(self._ep_counts[slot].item())
+        if cnt == 0:
+            return {}
+        rows = self._ep_rows[slot, :cnt].cpu().numpy()
+        rows = rows[np.argsort(rows[:, LY.EP["ENV"]], kind="stable")]
         N = self.num_envs
-        ep = {}
-        cause_names = {v: k for k, v in LY.CAUSE.items()}
-        keys = ("episode", "termination", "return", "length", "mean_reward", "success_rate", "collision_rate",
-                "unfinished_rate", "mean_speed", "mean_ttc", "mean_progress", "mean_abs_accel_long",
-                "mean_abs_accel_lat", "mean_abs_jerk_long", "mean_abs_jerk_lat", "mean_abs_yaw_rate",
-                "mean_abs_yaw_acc", "comfort_violation_rate", "harsh_brake_rate", "num_vehicles", "len_ego_route")
-        for k in keys:
-            ep[k] = np.zeros(N, dtype=object if k == "termination" else np.float64)
-        r_ep = np.zeros(N)
-        l_ep = np.zeros(N, dtype=np.int64)
-        t_ep = np.zeros(N)
-        now = time.perf_counter()
-        for j, i in enumerate(idx):
-            v = LY.RecordView(rec[j], self.layout)
-            n = max(v.i("EP_LEN"), 1)
-            h = self.history[i]
-            # Stats.terminated(): summary over the history *before* this episode
-            hist_c = list(h.causes)
-            hist_r = list(h.returns)
-            cause = cause_names.get(v.i("CAUSE"))
-            ret = float(v.h("EP_RETURN"))
-            vals = {
-                "episode": h.episode, "termination": cause, "return": ret, "length": v.i("EP_LEN"),
-                "mean_reward": float(np.mean(hist_r)) if hist_r else 0.0,
-                "success_rate": hist_c.count("success") / len(hist_c) if hist_c else 0.0,
-                "collision_rate": hist_c.count("collision") / len(hist_c) if hist_c else 0.0,
-                "unfinished_rate": hist_c.count("off_road") / len(hist_c) if hist_c else 0.0,
-                "mean_speed": float(v.h("EP_SPEED")) / n, "mean_ttc": 0.0, "mean_progress": 0.0,
-                "mean_abs_accel_long": float(v.h("EP_ABS_AL")) / n, "mean_abs_accel_lat": float(v.h("EP_ABS_ALAT")) / n,
-                "mean_abs_jerk_long": float(v.h("EP_ABS_JL")) / n, "mean_abs_jerk_lat": float(v.h("EP_ABS_JLAT")) / n,
-                "mean_abs_yaw_rate": float(v.h("EP_ABS_YR")) / n, "mean_abs_yaw_acc": float(v.h("EP_ABS_YACC")) / n,
-                "comfort_violation_rate": float(v.h("EP_VIOL")) / n, "harsh_brake_rate": float(v.h("EP_HARSH")) / n,
-                "num_vehicles": float(self.num_vehicles[i]), "len_ego_route": float(self.len_ego_route[i]),
-            }
-            for k in keys:
-                ep[k][i] = vals[k]
-            h.causes.append(cause)
-            h.returns.append(ret)
-            h.episode += 1
-            r_ep[i], l_ep[i], t_ep[i] = ret, v.i("EP_LEN"), round(now - self._t0[i], 6)
-        return {"episode_info": ep, "_episode_info": done.astype(bool),
-                "episode": {"r": r_ep, "l": l_ep, "t": t_ep}, "_episode": done.astype(bool)}
+        env_ids = rows[:, LY.EP["ENV"]].astype(np.int64)
+        summary: dict = {}
+        for key, col, typ in _EP_KEYS:
+            c = rows[:, LY.EP[col]]
+            if key == "termination":
+                vals = [LY.CAUSE_NAME.get(int(v)) for v in c]
+            elif typ is int:
+                vals = [int(v) for v in c]
+            else:
+                vals = [float(v) for v in c]
+            summary[key] = dict(zip(env_ids.tolist(), vals))
+        for j, i in enumerate(env_ids.tolist()):
+            ctx = self._ctx_table.get(int(rows[j, LY.EP["CTX_ID"]]), {})
+            for k, v in ctx.items():
+                summary.setdefault(k, {})[i] = v
+        done = np.zeros(N, dtype=np.bool_)
+        done[env_ids] = True
+        episode = {"r": dict(zip(env_ids.tolist(), rows[:, LY.EP["RETURN"]].tolist())),
+                   "l": dict(zip(env_ids.tolist(), rows[:, LY.EP["LENGTH"]].astype(np.int64).tolist())),
+                   "t": dict(zip(env_ids.tolist(), np.round(rows[:, LY.EP["SECONDS"]], 6).tolist()))}
+        return {"episode_info": _batched(summary, N), "_episode_info": done,
+                "episode": _batched(episode, N), "_episode": done.copy()}
 
     def render(self):
         """Tuple of per-env (S, S, 3) uint8 RGB frames, like SyncVectorEnv.render()."""

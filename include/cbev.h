@@ -64,6 +64,33 @@ int cbev_set_map(cbev_ctx* ctx, const uint8_t* padded_map_host, int64_t bytes);
 int cbev_step(cbev_ctx* ctx, void* records, int n, const void* actions, uint8_t* frames, double* reward,
               uint8_t* term, uint8_t* trunc, int32_t* cause, float* info, void* stream);
 
+/* Episode statistics on the device (Stats, src/deeprl/stats.py:87-148, and
+ * CarlaBEV._check_termination, carlabev.py:177-185), so `infos["episode_info"]`
+ * needs no per-step host work. The caller owns the buffers (device memory):
+ *   stats   cbev_episode_stats[n], zeroed before first use, kept across episodes
+ *   rows    float64[ring][n][CBEV_EP_COUNT]; counts int32[ring], zeroed
+ * Step s (the s-th cbev_step after this call, from 0) writes one row per env
+ * that terminated into rows[s % ring] (in no particular order, counts[s % ring]
+ * of them) and zeroes counts[(s + 1) % ring], so a slot stays readable until
+ * step s + ring - 1 is queued (ring >= 3). cbev_reset / cbev_reset_frames stamp
+ * each reset env's episode start on the device clock (CBEV_EP_SECONDS).
+ * stats = NULL turns it off. Not stream-ordered: call it between steps. */
+int cbev_set_episode_stats(cbev_ctx* ctx, void* stats, int n, double* rows, int32_t* counts, int ring);
+/* Slot of the latest step's rows (-1 when off) and the step count. */
+int cbev_episode_slot(const cbev_ctx* ctx, int64_t* step_count);
+/* Rate of the device clock the episode times use. */
+int cbev_wall_clock_hz(const cbev_ctx* ctx, double* hz);
+
+/* Errors the kernels detect are not stream-ordered return codes: they set bits
+ * of a context error word, read (and cleared, if clear != 0) by this call,
+ * which synchronises the device.
+ *   CBEV_ERR_ACTION_INDEX  a discrete action outside [-n, n) (the reference's
+ *                          IndexError in discrete_actions[int(action)],
+ *                          envs/spaces.py:46); that env stepped action 0.
+ *                          Negative indices in [-n, 0) count from the end. */
+#define CBEV_ERR_ACTION_INDEX 1
+int cbev_error_flags(cbev_ctx* ctx, int32_t* flags_host, int clear);
+
 /* Reset the envs selected by mask (uint8[n], NULL = all):
  *   if bank != NULL: records[i] = bank[b] with b = bank_idx[i], or, when
  *   bank_idx == NULL, b = (i + bank_offset) % n_bank (device-side scene bank);

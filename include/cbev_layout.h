@@ -44,7 +44,9 @@
   /* episode accumulators (stats.py:30-56) */                                 \
   F_(EP_RETURN) F_(EP_SPEED) F_(EP_ABS_AL) F_(EP_ABS_ALAT) F_(EP_ABS_JL)           \
   F_(EP_ABS_JLAT) F_(EP_ABS_YR) F_(EP_ABS_YACC) F_(EP_VIOL) F_(EP_HARSH)           \
-  F_(EP_TTC) F_(EP_PROGRESS)
+  F_(EP_TTC) F_(EP_PROGRESS)                                                     \
+  /* scene scalars episode_info reports (carlabev.py:177-185), set by the host */ \
+  F_(NUM_VEH) F_(LEN_ROUTE_M)
 
 /* ---- hero + per-env int32 scalars ------------------------------------- */
 #define CBEV_HI_FIELDS(F_)                                                     \
@@ -61,7 +63,8 @@
   F_(TILE)           /* SemanticClass of hero tile (world.py:159-165) */       \
   F_(COLLIDED)       /* 0 none, 1 vehicle, 2 pedestrian, 3 target */          \
   F_(ACTOR_ID)       /* -1 None, -2 "goal", else int id */                     \
-  F_(EP_LEN) F_(STEP) F_(SCENE_ID) F_(NACTSTATE) F_(PAD0)                         \
+  F_(EP_LEN) F_(STEP) F_(SCENE_ID) F_(NACTSTATE)                                 \
+  F_(CTX_ID)         /* host id of the scene's scenario context (episode_info) */ \
   /* render set-up of the current observation (device scratch, k_ego -> k_raster): */ \
   F_(RS_XMIN) F_(RS_YMIN) /* crop origin in the padded map (fov.py:70-79) */        \
   F_(RS_R90) F_(RS_NX) F_(RS_NY) F_(RS_ISIN) F_(RS_ICOS) F_(RS_DX00) F_(RS_DY00)      \
@@ -197,6 +200,35 @@ static inline cbev_layout cbev_make_layout(cbev_caps c) {
   L.pad = 0;
   return L;
 }
+
+/* ---- per-env episode statistics on the device ----------------------------
+ * The state of `Stats` (src/deeprl/stats.py:87-148) that outlives an episode,
+ * one struct per env, kept across resets: the last CBEV_STATS_HIST episodes'
+ * returns and causes (a ring), their cause counts and a double-double running
+ * sum of their returns, the finished-episode count, and the device clock at
+ * the episode's reset (for RecordEpisodeStatistics' elapsed time). */
+#define CBEV_STATS_HIST 200
+typedef struct cbev_episode_stats {
+  double ret[CBEV_STATS_HIST];  /* returns of the window, ring */
+  double sum_hi, sum_lo;        /* sum of ret over the window (double-double) */
+  double t0;                    /* device wall clock ticks at the episode's reset */
+  int32_t n, head, episode;     /* window length, next ring slot, episodes finished */
+  int32_t n_success, n_collision, n_offroad;  /* causes in the window */
+  uint8_t cause[CBEV_STATS_HIST];             /* CBEV_CAUSE_* of the window, ring */
+  uint8_t pad[8];
+} cbev_episode_stats;             /* 1856 bytes */
+
+/* One row per env that terminated in a step (Stats.get_episode_info at
+ * termination, stats.py:127-148, plus carlabev.py:180-182's scene scalars and
+ * RecordEpisodeStatistics' elapsed time), float64. */
+#define CBEV_EP_FIELDS(F_)                                                     \
+  F_(ENV) F_(EPISODE) F_(CAUSE) F_(RETURN) F_(LENGTH) F_(MEAN_REWARD)             \
+  F_(SUCCESS_RATE) F_(COLLISION_RATE) F_(UNFINISHED_RATE) F_(MEAN_SPEED)          \
+  F_(MEAN_TTC) F_(MEAN_PROGRESS) F_(MEAN_ABS_AL) F_(MEAN_ABS_ALAT) F_(MEAN_ABS_JL) \
+  F_(MEAN_ABS_JLAT) F_(MEAN_ABS_YR) F_(MEAN_ABS_YACC) F_(VIOL_RATE) F_(HARSH_RATE)  \
+  F_(NUM_VEH) F_(LEN_ROUTE_M) F_(SECONDS) F_(CTX_ID)
+#define CBEV_ENUM_EP(n) CBEV_EP_##n,
+enum { CBEV_EP_FIELDS(CBEV_ENUM_EP) CBEV_EP_COUNT };
 
 /* Static simulation parameters (one per context), all derived on the host
  * from EnvConfig (config/env.py:43-181) and the reward/action presets. */

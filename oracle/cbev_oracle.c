@@ -1059,6 +1059,7 @@ int orc_step(const cbev_params* P, const uint8_t* padded_map, const cbev_caps* c
   float g, s, b;
   if (P->action_kind == 0) {
     int idx = *(const int32_t*)action;
+    if (idx < 0) idx += P->n_discrete; /* discrete_actions[int(action)]: negative from the end (spaces.py:46) */
     if (idx < 0 || idx >= P->n_discrete) return -1;
     g = P->action_table[idx][0];
     s = P->action_table[idx][1];
