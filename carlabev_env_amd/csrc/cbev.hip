@@ -2086,6 +2086,20 @@ __global__ __launch_bounds__(256) void k_ego(KArgs K, uint8_t* __restrict__ recs
   // S0 (wave 0 runs the chain, wave 1 the steering tangent)
   float ag = 0.f, asa = 0.f, ab = 0.f;
   if (wave <= 1 && lane < ne_eff) d_decode_action(K, actions, e0 + lane, &ag, &asa, &ab);
+  // the (env, actor) pair of S5 this thread takes first: its actor's fields are
+  // loaded now, in flight under S0-S4 (slots past NACT hold zeros and are skipped)
+  const int A = K.C.actor_cap;
+  double pax = 0.0, pay = 0.0, payaw = 0.0, pav = 0.0;
+  int pasz = 0;
+  if (tid < ne_eff * A) {
+    const int k = tid / A, a = tid - k * A;
+    const DRec g = bind_rec(recs + (int64_t)(e0 + k) * rb, K.L, K.C);
+    pax = RAD(g, CBEV_AD_X, a);
+    pay = RAD(g, CBEV_AD_Y, a);
+    payaw = RAD(g, CBEV_AD_YAW, a);
+    pav = RAD(g, CBEV_AD_V, a);
+    pasz = RAI(g, CBEV_AI_SIZE, a);
+  }
   ego_stage_in(lds, recs, e0, ne_eff, K, pk);
   __syncthreads();
   CBEV_STAMP(0, 1);
@@ -2161,6 +2175,10 @@ __global__ __launch_bounds__(256) void k_ego(KArgs K, uint8_t* __restrict__ recs
       hero_env_comfort(rec(lane));
     } else if (wave == 2) {
       hero_env_render_setup(K, rec(lane));
+    } else if (wave == 3) {  // the updated yaw's cos / sin for the actors' TTCs (S5)
+      const double yaw = ((const double*)(lds + lane * pk.bytes + K.L.hd))[CBEV_HD_YAW];
+      pre[lane].cyaw = cos(yaw);
+      pre[lane].syaw = sin(yaw);
     } else if (wave == 0) {
       const DRec r = rec(lane);
       const double x = r.hd[CBEV_HD_X], y = r.hd[CBEV_HD_Y];
@@ -2259,16 +2277,16 @@ __global__ __launch_bounds__(256) void k_ego(KArgs K, uint8_t* __restrict__ recs
     // vehicles / pedestrians (fields read from HBM, field-major over the actor
     // slots): rect hit, actors_state entry and both TTCs (scene.py:110-140,
     // reward_signals.py:15-94)
-    const int A = K.C.actor_cap;
     for (int q = tid; q < ne_eff * A; q += 256) {
       const int k = q / A, a = q - k * A;
       const DRec r = rec(k);
       if (a >= r.hi[CBEV_HI_NACT]) continue;
       int* I = (int*)(scr + k * SL.bytes + SL.ints);
       const int hrx = I[3], hry = I[4];
-      const double x = r.hd[CBEV_HD_X], y = r.hd[CBEV_HD_Y], yaw = r.hd[CBEV_HD_YAW], v = r.hd[CBEV_HD_V];
-      const int sz = RAI(r, CBEV_AI_SIZE, a);
-      const double ax = RAD(r, CBEV_AD_X, a), ay = RAD(r, CBEV_AD_Y, a);
+      const double x = r.hd[CBEV_HD_X], y = r.hd[CBEV_HD_Y], v = r.hd[CBEV_HD_V];
+      const bool mine = q == tid;  // prefetched at S0
+      const int sz = mine ? pasz : RAI(r, CBEV_AI_SIZE, a);
+      const double ax = mine ? pax : RAD(r, CBEV_AD_X, a), ay = mine ? pay : RAD(r, CBEV_AD_Y, a);
       const int arx = d_rect_lo(ax, P.pad, sz), ary = d_rect_lo(ay, P.pad, sz);
       if (hw > 0 && sz > 0 && hrx < arx + sz && hry < ary + sz && hrx + hw > arx && hry + hw > ary)
         atomicMax(&I[CS_ACT_LAST], a);
@@ -2278,9 +2296,10 @@ __global__ __launch_bounds__(256) void k_ego(KArgs K, uint8_t* __restrict__ recs
       if (fabs(dist) < P.collide_min_dist) {  // actors_state entry
         atomicAdd(&I[CS_NAS], 1);
         const double hx_m = x * CB_MPP, hy_m = y * CB_MPP, hv_m = v * CB_MPP;
-        const double hvx_m = hv_m * cos(yaw), hvy_m = hv_m * sin(yaw);
-        const double hvx = v * cos(yaw), hvy = v * sin(yaw);
-        const double av = RAD(r, CBEV_AD_V, a), ayaw = RAD(r, CBEV_AD_YAW, a);
+        const double cyaw = pre[k].cyaw, syaw = pre[k].syaw;  // cos / sin of the updated yaw (S4)
+        const double hvx_m = hv_m * cyaw, hvy_m = hv_m * syaw;
+        const double hvx = v * cyaw, hvy = v * syaw;
+        const double av = mine ? pav : RAD(r, CBEV_AD_V, a), ayaw = mine ? payaw : RAD(r, CBEV_AD_YAW, a);
         const double avx = av * cos(ayaw), avy = av * sin(ayaw);
         {  // compute_ttc_raw (reward_signals.py:46-94)
           double rx_ = ax * CB_MPP - hx_m, ry_ = ay * CB_MPP - hy_m;
@@ -2627,11 +2646,13 @@ struct cbev_ctx {
 
 // Envs per k_ego workgroup: small groups spread the record staging (LDS-DMA
 // throughput is per CU) and the chains over more CUs; the largest divisor of 64
-// not above CBEV_EGO_NE (default 16) whose LDS fits the budget.
-static int ego_ne_for(int per_env) {
+// not above CBEV_EGO_NE (default below) whose LDS fits the budget.
+static int ego_ne_for(int per_env, int actor_cap) {
   const int budget = 128 * 1024;
   const char* v = getenv("CBEV_EGO_NE");
-  int ne = v ? atoi(v) : 16;
+  // default: 16 envs, fewer when their (env, actor) pairs would need more than one
+  // pass of the 256 threads in S5
+  int ne = v ? atoi(v) : (actor_cap <= 16 ? 16 : actor_cap <= 32 ? 8 : 4);
   ne = ne >= 64 ? 64 : ne >= 32 ? 32 : ne >= 16 ? 16 : ne >= 8 ? 8 : ne >= 4 ? 4 : ne >= 2 ? 2 : 1;
   while (ne > 1 && ne * per_env > budget) ne >>= 1;
   return ne;
@@ -2793,7 +2814,7 @@ int cbev_create(const cbev_params* params, const cbev_caps* caps, int device, cb
     // k_ego LDS per env: packed record ranges + collision scratch + HeroPre + target index
     const int per_env = ego_pack(c->L).bytes + coll_scratch_layout(c->C, c->L.vis_words).bytes +
                         (int)sizeof(HeroPre) + (int)sizeof(int);
-    c->ego_ne = ego_ne_for(per_env);
+    c->ego_ne = ego_ne_for(per_env, c->C.actor_cap);
     c->ego_lb = c->ego_ne * per_env;
     if (c->ego_lb > 160 * 1024) {
       const int nb = per_env;
