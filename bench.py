@@ -240,6 +240,54 @@ def dry_run(args, world, rank):
         dist.destroy_process_group()
 
 
+def start_scene_pool(cfgd, workers, rank, world):
+    """Host workers building fresh seeded scenes (global ids 2_000_000 + rank,
+    + world, ...) for the bank, started before the GPU is touched."""
+    from carlabev_env_amd import layout as LY
+    from carlabev_env_amd.config import EnvConfig
+    from carlabev_env_amd.scene_pool import ScenePool
+    S = cfgd["size"]
+    action_mode = "continuous" if cfgd["action"].startswith("continuous") else "discrete"
+    cfg = EnvConfig(size=S, obs_size=(S, S), obs_mode=cfgd["obs_mode"], render_mode="rgb_array",
+                    action_mode=action_mode, action_profile_id=cfgd["action"])
+    rb = LY.Layout.make(LY.Caps(**cfgd["caps"])).record_bytes
+    return ScenePool(cfg.model_dump(), cfgd["caps"], cfgd["difficulty"], cfgd["seed0"], rb, workers=workers,
+                     first_gid=2_000_000 + rank, stride=world)
+
+
+def fresh_pass(env, pool, one_step, args, world, n, device):
+    """The canonical loop with the bank refreshed from the host ScenePool while it
+    runs: every 4 steps the finished scenes replace the oldest bank rows (and
+    their cached reset frames are rendered). Reports the pool's scene rate, the
+    device's reset rate and the share of resets a fresh scene can have served."""
+    import torch
+    pool.request(4 * pool.batch * pool.workers)
+    pool.poll(timeout=30.0)  # workers up and producing
+    total = args.warmup + args.steps
+    for t in range(args.warmup):
+        one_step(t, False)
+    torch.cuda.synchronize()
+    term0 = env.termination_count()
+    d0 = pool.delivered
+    slot = 0
+    t0 = time.perf_counter()
+    for t in range(args.warmup, total):
+        one_step(t, False)
+        if t % 4 == 0:
+            gids, recs = pool.poll(max_scenes=env.bank.shape[0])
+            if len(gids):
+                slot = env.refresh_bank(slot, recs)
+                pool.request(len(gids))
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    resets = env.termination_count() - term0
+    fresh_scenes = pool.delivered - d0
+    return {"workers": pool.workers, "value": round(world * n * args.steps / el, 1),
+            "scenes_per_s": round(fresh_scenes / el, 1), "resets_per_s": round(resets / el, 1),
+            "fresh_reset_frac": round(min(1.0, fresh_scenes / resets), 4) if resets else 1.0,
+            "note": "per rank; resets beyond the fresh scenes reuse bank scenes (recycled)"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -252,6 +300,8 @@ def main():
     ap.add_argument("--no-wire", action="store_true")
     ap.add_argument("--raster-reps", type=int, default=50, help="back-to-back k_raster launches timed for the roofline")
     ap.add_argument("--dry-run", action="store_true", help="CPU/gloo rehearsal of the N-rank path (no GPU, value null)")
+    ap.add_argument("--fresh-workers", type=int, default=4,
+                    help="host processes feeding fresh seeded scenes into the reset bank in a last timed pass (0: off)")
     ap.add_argument("--info-mode", default="none", choices=("none", "full"),
                     help="full: device episode statistics + a StepInfos per step (not read), as step() returns")
     args = ap.parse_args()
@@ -266,14 +316,18 @@ def main():
     if args.dry_run:
         return dry_run(args, world, rank)
 
+    cfgd = CONFIGS[args.config]
+    n = args.envs or cfgd["envs"]
+    pool = None
+    if args.fresh_workers > 0:  # spawned before this process touches the GPU
+        pool = start_scene_pool(cfgd, args.fresh_workers, rank, world)
+
     import torch
     import torch.distributed as dist
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
     if world > 1:
         dist.init_process_group("nccl", device_id=device)
-    cfgd = CONFIGS[args.config]
-    n = args.envs or cfgd["envs"]
     from carlabev_env_amd._lib import check, lib
     env, host_recs = build_env(cfgd, n, rank, device, args.info_mode)
     P = env.params
@@ -365,6 +419,10 @@ def main():
             reseed()
             el_w, _, _ = timed(True, False)
             wire_value = world * n * args.steps / el_w
+        fresh = None
+        if pool is not None:
+            reseed()
+            fresh = fresh_pass(env, pool, one_step, args, world, n, device)
 
     S = P.size
     # per env: S^2 texels sampled + S^2 frame bytes + ego state
@@ -411,11 +469,14 @@ def main():
                          # the same bytes over the per-step event time (includes each launch's dispatch gap)
                          "achieved_step_events": round(n * algo_bytes / (ms3[2] * 1e-3) / 1e9, 1)},
             "with_wire_obs": None if wire_value is None else round(wire_value, 1),
+            "fresh_resets": fresh,
             "gather_bytes_per_step": None if gatherer is None else gatherer.bytes_per_step,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
     env.close()
+    if pool is not None:
+        pool.close()
     if world > 1:
         dist.destroy_process_group()
 

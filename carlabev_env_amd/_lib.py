@@ -68,6 +68,8 @@ def lib():
     L.cbev_episode_slot.restype = _I
     L.cbev_wall_clock_hz.argtypes = [_P, _P]
     L.cbev_wall_clock_hz.restype = _I
+    L.cbev_termination_count.argtypes = [_P, _P]
+    L.cbev_termination_count.restype = _I
     L.cbev_error_flags.argtypes = [_P, _P, _I]
     L.cbev_error_flags.restype = _I
     L.cbev_profile.argtypes = [_P, _I]
@@ -91,6 +93,6 @@ EXPORTED_SYMBOLS = ("cbev_abi_version", "cbev_params_size", "cbev_layout_of", "c
                     "cbev_reset_frames",
                     "cbev_expand_obs", "cbev_vector_obs", "cbev_set_fov_mask", "cbev_set_obs_size", "cbev_resize_obs", "cbev_profile", "cbev_profile_read",
                     "cbev_profile_raster", "cbev_error_flags", "cbev_set_episode_stats", "cbev_episode_slot",
-                    "cbev_wall_clock_hz")
+                    "cbev_wall_clock_hz", "cbev_termination_count")
 
 ERR_ACTION_INDEX = 1  # CBEV_ERR_ACTION_INDEX (include/cbev.h)

@@ -2023,7 +2023,10 @@ __device__ __forceinline__ void collide_env(const KArgs& K, DRec r, int e, const
   hi[CBEV_HI_TERM] = terminal;
   hi[CBEV_HI_TRUNC] = terminal && cause == CBEV_CAUSE_MAX_ACTIONS;
   hi[CBEV_HI_STEP] += 1;
-  if (terminal && K.stats != nullptr) d_episode_summary(K, r, e);
+  if (terminal) {
+    atomicAdd(K.nterm, 1ull);
+    if (K.stats != nullptr) d_episode_summary(K, r, e);
+  }
   reward_out[e] = reward;
   term_out[e] = (uint8_t)terminal;
   trunc_out[e] = (uint8_t)(terminal && cause == CBEV_CAUSE_MAX_ACTIONS);
@@ -2636,6 +2639,7 @@ struct cbev_ctx {
   AreaTab area;
   uint8_t* fov_dev;   // cbev_set_fov_mask
   int32_t* err_dev;   // CBEV_ERR_* bits set by the kernels
+  unsigned long long* nterm_dev;  // terminations counted by k_ego
   cbev_episode_stats* stats;  // cbev_set_episode_stats (caller-owned device buffers)
   double* ep_rows;
   int32_t* ep_counts;
@@ -2739,6 +2743,7 @@ static KArgs kargs(const cbev_ctx* c) {
   K.npitch = c->npitch;
   K.fov = (const uint32_t*)c->fov_dev;
   K.err = c->err_dev;
+  K.nterm = c->nterm_dev;
   K.stats = c->stats;
   K.ep_rows = nullptr;
   K.ep_count = K.ep_count_next = nullptr;
@@ -2828,6 +2833,8 @@ int cbev_create(const cbev_params* params, const cbev_caps* caps, int device, cb
   if (e == hipSuccess) e = hipMalloc(&c->lut_dev, 64 * sizeof(uint32_t));
   if (e == hipSuccess) e = hipMalloc(&c->err_dev, sizeof(int32_t));
   if (e == hipSuccess) e = hipMemset(c->err_dev, 0, sizeof(int32_t));
+  if (e == hipSuccess) e = hipMalloc(&c->nterm_dev, sizeof(unsigned long long));
+  if (e == hipSuccess) e = hipMemset(c->nterm_dev, 0, sizeof(unsigned long long));
   if (e == hipSuccess) {
     int khz = 0;  // wall_clock64() rate
     e = hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device);
@@ -2877,6 +2884,15 @@ int cbev_episode_slot(const cbev_ctx* c, int64_t* step_count) {
 int cbev_wall_clock_hz(const cbev_ctx* c, double* hz) {
   if (!c || !hz) return set_err(CBEV_EINVAL, "null argument");
   *hz = c->tick_s > 0 ? 1.0 / c->tick_s : 0.0;
+  return CBEV_OK;
+}
+
+int cbev_termination_count(cbev_ctx* c, int64_t* count) {
+  if (!c || !count) return set_err(CBEV_EINVAL, "null argument");
+  HIP_TRY(hipSetDevice(c->device));
+  unsigned long long v = 0;
+  HIP_TRY(hipMemcpy(&v, c->nterm_dev, sizeof v, hipMemcpyDeviceToHost));
+  *count = (int64_t)v;
   return CBEV_OK;
 }
 
@@ -2958,6 +2974,7 @@ void cbev_destroy(cbev_ctx* c) {
   if (c->map_dev) (void)hipFree(c->map_dev);
   if (c->lut_dev) (void)hipFree(c->lut_dev);
   if (c->err_dev) (void)hipFree(c->err_dev);
+  if (c->nterm_dev) (void)hipFree(c->nterm_dev);
   if (c->area_dev) (void)hipFree(c->area_dev);
   if (c->fov_dev) (void)hipFree(c->fov_dev);
   free(c);

@@ -27,6 +27,7 @@ struct KArgs {
   int npitch;
   const uint32_t* fov;  // FOV corner mask, S*S bytes (0xff = black), or null (fov_masked off)
   int32_t* err;         // device error word (CBEV_ERR_* bits, read by cbev_error_flags)
+  unsigned long long* nterm;  // terminations since cbev_create (cbev_termination_count)
   // episode statistics (cbev_set_episode_stats; null: off)
   cbev_episode_stats* stats;  // [n] per env, kept across episodes
   double* ep_rows;            // this step's summary rows [n][CBEV_EP_COUNT], first *ep_count used

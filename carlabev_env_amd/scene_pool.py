@@ -1,0 +1,123 @@
+"""Host scene feed for fresh seeded resets (host half).
+
+The reference builds a new scene on every reset (`CarlaBEV.reset`,
+carlabev.py:96-148 -> `SceneGenerator.build_scene`, scene_generator.py:95-191),
+on the CPU, one env at a time. Here the device resets from a scene bank
+(`CarlaBEVVectorEnv.reset_from_bank`), so the host's job is to keep that bank
+supplied with fresh scenes at the rate the device terminates episodes.
+
+`ScenePool` runs that host work in worker processes (spawned, so they never
+inherit a process that has touched the GPU): each builds packed records for
+the global scene ids it is handed, seeded as the reference seeds a reset
+(scene_seed = seed0 + global id, randomness.py:13-65), and returns the bytes.
+The caller drains finished scenes without blocking (`poll`) and writes them
+into bank slots (`CarlaBEVVectorEnv.refresh_bank`).
+"""
+from __future__ import annotations
+
+import multiprocessing as mp
+import queue
+import time
+
+import numpy as np
+
+
+def scene_options(difficulty: str, gid: int) -> dict:
+    """Reset options of global scene id `gid`: random navigation at a difficulty
+    preset, or "mix3" = lead_brake / jaywalk / red_light_runner by gid % 3."""
+    from .config import RandomNavigationReset, build_random_navigation_options
+    if difficulty == "mix3":
+        return {"scene": ("lead_brake", "jaywalk", "red_light_runner")[gid % 3]}
+    return build_random_navigation_options(RandomNavigationReset(difficulty_id=difficulty))
+
+
+def make_builder(cfg_dict: dict, caps: dict):
+    """The HostResetBuilder a CarlaBEVVectorEnv with this config and these
+    capacities uses (vector_env.py), without torch or the GPU."""
+    from . import layout as LY
+    from .config import EnvConfig
+    from .host_reset import HostResetBuilder
+    from .params import build_params, load_class_map
+    from .scene_gen import SceneGenerator
+    cfg = EnvConfig.model_validate(cfg_dict)
+    classes = load_class_map(cfg.map_name, int(cfg.size))
+    params = build_params(cfg, classes)
+    layout = LY.Layout.make(LY.Caps(**caps))
+    return HostResetBuilder(cfg, classes, params, layout, SceneGenerator(cfg, cfg.map_name)), layout
+
+
+def _worker(cfg_dict, caps, difficulty, seed0, tasks, results):
+    builder, layout = make_builder(cfg_dict, caps)
+    rb = layout.record_bytes
+    while True:
+        task = tasks.get()
+        if task is None:
+            return
+        gids = task
+        out = np.zeros((len(gids), rb), np.uint8)
+        try:
+            for k, gid in enumerate(gids):
+                builder.build(out[k], None, dict(scene_options(difficulty, gid), scene_seed=seed0 + gid))
+        except Exception as exc:  # noqa: BLE001 - reported to the caller by poll()
+            results.put((None, f"{type(exc).__name__}: {exc}"))
+            continue
+        results.put((gids, out.tobytes()))
+
+
+class ScenePool:
+    """`workers` processes building packed scene records for global ids
+    first_gid, first_gid + stride, ... in order of request."""
+
+    def __init__(self, cfg_dict: dict, caps: dict, difficulty: str, seed0: int, record_bytes: int, workers: int = 4,
+                 first_gid: int = 0, stride: int = 1, batch: int = 16):
+        ctx = mp.get_context("spawn")
+        self.rb = record_bytes
+        self.batch = batch
+        self._tasks = ctx.Queue()
+        self._results = ctx.Queue()
+        self._next = first_gid
+        self._stride = stride
+        self.requested = 0
+        self.delivered = 0
+        self.workers = workers
+        self._procs = [ctx.Process(target=_worker, args=(cfg_dict, caps, difficulty, seed0, self._tasks, self._results),
+                                   daemon=True) for _ in range(workers)]
+        for p in self._procs:
+            p.start()
+
+    def request(self, n: int):
+        """Queue n more scenes (in batches)."""
+        while n > 0:
+            k = min(n, self.batch)
+            self._tasks.put([self._next + self._stride * i for i in range(k)])
+            self._next += self._stride * k
+            self.requested += k
+            n -= k
+
+    def poll(self, max_scenes: int | None = None, timeout: float = 0.0) -> tuple[list, np.ndarray]:
+        """Finished scenes, without blocking beyond `timeout` seconds for the first
+        batch: (global ids, records uint8[k][record_bytes])."""
+        gids, recs = [], []
+        n = 0
+        deadline = time.perf_counter() + timeout
+        while max_scenes is None or n < max_scenes:
+            try:
+                wait = max(0.0, deadline - time.perf_counter()) if not recs else 0.0
+                g, b = self._results.get(timeout=wait) if wait > 0 else self._results.get_nowait()
+            except queue.Empty:
+                break
+            if g is None:
+                raise RuntimeError(f"scene pool worker failed: {b}")
+            gids.extend(g)
+            recs.append(np.frombuffer(b, np.uint8).reshape(len(g), self.rb))
+            n += len(g)
+        self.delivered += n
+        return gids, (np.concatenate(recs) if recs else np.zeros((0, self.rb), np.uint8))
+
+    def close(self):
+        for _ in self._procs:
+            self._tasks.put(None)
+        for p in self._procs:
+            p.join(timeout=10)
+            if p.is_alive():
+                p.terminate()

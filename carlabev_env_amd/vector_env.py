@@ -275,6 +275,36 @@ class CarlaBEVVectorEnv:
         check(lib().cbev_bank_frames(self._ctx, _ptr(self.bank), B, _ptr(self.bank_frames), self._stream()),
               "cbev_bank_frames")
 
+    def refresh_bank(self, slot0: int, records: np.ndarray) -> int:
+        """Write k fresh scene records (uint8[k][record_bytes], e.g. from a ScenePool)
+        into bank rows slot0, slot0 + 1, ... (wrapping) and render their cached reset
+        frames; stream-ordered, no sync. Returns the next slot."""
+        if self.bank is None:
+            raise RuntimeError("no scene bank attached")
+        B, k = self.bank.shape[0], int(records.shape[0])
+        if k == 0:
+            return slot0
+        if records.shape[1] != self.rb or k > B:
+            raise ValueError(f"expected at most {B} records of {self.rb} bytes")
+        src = torch.from_numpy(np.ascontiguousarray(records)).pin_memory()
+        done = 0
+        s = slot0 % B
+        while done < k:
+            m = min(k - done, B - s)
+            self.bank[s:s + m].copy_(src[done:done + m], non_blocking=True)
+            check(lib().cbev_bank_frames(self._ctx, _ptr(self.bank[s:s + m]), m, _ptr(self.bank_frames[s:s + m]),
+                                         self._stream()), "cbev_bank_frames")
+            done += m
+            s = (s + m) % B
+        self._refresh_keep = src  # the pinned staging must outlive the async copy
+        return s
+
+    def termination_count(self) -> int:
+        """Episodes terminated so far on this env's device context (synchronises)."""
+        n = ctypes.c_int64()
+        check(lib().cbev_termination_count(self._ctx, ctypes.byref(n)), "cbev_termination_count")
+        return int(n.value)
+
     def _new_ctx_id(self, ctx: dict) -> int:
         cid = self._ctx_next
         self._ctx_next += 1

@@ -81,6 +81,10 @@ int cbev_episode_slot(const cbev_ctx* ctx, int64_t* step_count);
 /* Rate of the device clock the episode times use. */
 int cbev_wall_clock_hz(const cbev_ctx* ctx, double* hz);
 
+/* Episodes terminated in all cbev_step calls since cbev_create (synchronises):
+ * the reset demand a host scene feed has to meet. */
+int cbev_termination_count(cbev_ctx* ctx, int64_t* count);
+
 /* Errors the kernels detect are not stream-ordered return codes: they set bits
  * of a context error word, read (and cleared, if clear != 0) by this call,
  * which synchronises the device.
