@@ -71,7 +71,7 @@ def make_actions(P, n, steps, seed0, offset):
     return out
 
 
-def build_env(cfgd, n, rank, device, info_mode="none"):
+def build_env(cfgd, n, rank, device, info_mode="none", cache=None):
     """Vector env with every env reset to its seeded scene (host scene-gen)."""
     from carlabev_env_amd.config import EnvConfig
     from carlabev_env_amd.host_reset import HostResetBuilder
@@ -84,19 +84,31 @@ def build_env(cfgd, n, rank, device, info_mode="none"):
     env = CarlaBEVVectorEnv({"env": cfg, "num_envs": n}, device=device, caps=cfgd["caps"], info_mode=info_mode)
     first = rank * n
     t0 = time.time()
-    host = np.zeros((n, env.rb), np.uint8)
-    for i in range(n):
-        gid = first + i
-        opts = dict(scene_options(cfgd, gid), scene_seed=cfgd["seed0"] + gid)
-        env.builder.build(host[i], None, opts)
-    recs = torch.from_numpy(host).to(device)
-    # bank of further seeded scenes for the canonical reset-on-termination loop
     nb = min(n, 512)
-    bank = np.zeros((nb, env.rb), np.uint8)
-    for i in range(nb):
-        gid = 1_000_000 + first + i
-        env.builder.build(bank[i], None, dict(scene_options(cfgd, gid), scene_seed=cfgd["seed0"] + gid))
-    log(f"[rank {rank}] built {n} scenes + {nb} bank scenes in {time.time() - t0:.1f}s")
+    key = None
+    if cache:  # scenes are a pure function of (config, n, rank): reuse them across runs on one box
+        os.makedirs(cache, exist_ok=True)
+        key = os.path.join(cache, f"cfg{cfgd['seed0']}_{cfgd['difficulty']}_{n}_{rank}_{env.rb}")
+    if key and os.path.exists(key + "_recs.npy"):
+        host = np.load(key + "_recs.npy")
+        bank = np.load(key + "_bank.npy")
+        log(f"[rank {rank}] loaded {n} scenes + {nb} bank scenes from {cache}")
+    else:
+        host = np.zeros((n, env.rb), np.uint8)
+        for i in range(n):
+            gid = first + i
+            opts = dict(scene_options(cfgd, gid), scene_seed=cfgd["seed0"] + gid)
+            env.builder.build(host[i], None, opts)
+        # bank of further seeded scenes for the canonical reset-on-termination loop
+        bank = np.zeros((nb, env.rb), np.uint8)
+        for i in range(nb):
+            gid = 1_000_000 + first + i
+            env.builder.build(bank[i], None, dict(scene_options(cfgd, gid), scene_seed=cfgd["seed0"] + gid))
+        log(f"[rank {rank}] built {n} scenes + {nb} bank scenes in {time.time() - t0:.1f}s")
+        if key:
+            np.save(key + "_recs.npy", host)
+            np.save(key + "_bank.npy", bank)
+    recs = torch.from_numpy(host).to(device)
     env.attach_bank(torch.from_numpy(bank).to(device))
     # initial reset: records = seeded scenes, reset observation rendered on device
     env.attach_bank(recs)
@@ -252,17 +264,18 @@ def start_scene_pool(cfgd, workers, rank, world):
                     action_mode=action_mode, action_profile_id=cfgd["action"])
     rb = LY.Layout.make(LY.Caps(**cfgd["caps"])).record_bytes
     return ScenePool(cfg.model_dump(), cfgd["caps"], cfgd["difficulty"], cfgd["seed0"], rb, workers=workers,
-                     first_gid=2_000_000 + rank, stride=world)
+                     first_gid=2_000_000 + rank, stride=world, batch=16 if cfgd["difficulty"] == "rt_no_traffic_v1" else 4)
 
 
-def fresh_pass(env, pool, one_step, args, world, n, device):
+def fresh_pass(env, pool, one_step, args, world, n, device, seconds=2.0):
     """The canonical loop with the bank refreshed from the host ScenePool while it
-    runs: every 4 steps the finished scenes replace the oldest bank rows (and
-    their cached reset frames are rendered). Reports the pool's scene rate, the
+    runs (at least `seconds` of wall time, so the host rates are measurable):
+    every 8 steps the finished scenes replace the oldest bank rows (and their
+    cached reset frames are rendered). Reports the pool's scene rate, the
     device's reset rate and the share of resets a fresh scene can have served."""
     import torch
     pool.request(4 * pool.batch * pool.workers)
-    pool.poll(timeout=30.0)  # workers up and producing
+    pool.poll(timeout=60.0)  # workers up and producing
     total = args.warmup + args.steps
     for t in range(args.warmup):
         one_step(t, False)
@@ -270,19 +283,24 @@ def fresh_pass(env, pool, one_step, args, world, n, device):
     term0 = env.termination_count()
     d0 = pool.delivered
     slot = 0
+    steps = 0
     t0 = time.perf_counter()
-    for t in range(args.warmup, total):
+    while steps < args.steps or time.perf_counter() - t0 < seconds:
+        t = args.warmup + steps % args.steps
         one_step(t, False)
-        if t % 4 == 0:
+        steps += 1
+        if steps % 8 == 0:
             gids, recs = pool.poll(max_scenes=env.bank.shape[0])
             if len(gids):
                 slot = env.refresh_bank(slot, recs)
                 pool.request(len(gids))
+            if steps % 64 == 0:  # keep the host no more than ~64 steps ahead of the device
+                torch.cuda.current_stream().synchronize()
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     resets = env.termination_count() - term0
     fresh_scenes = pool.delivered - d0
-    return {"workers": pool.workers, "value": round(world * n * args.steps / el, 1),
+    return {"workers": pool.workers, "steps": steps, "seconds": round(el, 3), "value": round(world * n * steps / el, 1),
             "scenes_per_s": round(fresh_scenes / el, 1), "resets_per_s": round(resets / el, 1),
             "fresh_reset_frac": round(min(1.0, fresh_scenes / resets), 4) if resets else 1.0,
             "note": "per rank; resets beyond the fresh scenes reuse bank scenes (recycled)"}
@@ -300,6 +318,7 @@ def main():
     ap.add_argument("--no-wire", action="store_true")
     ap.add_argument("--raster-reps", type=int, default=50, help="back-to-back k_raster launches timed for the roofline")
     ap.add_argument("--dry-run", action="store_true", help="CPU/gloo rehearsal of the N-rank path (no GPU, value null)")
+    ap.add_argument("--scene-cache", default=None, help="directory to keep built scenes in across runs (one box)")
     ap.add_argument("--fresh-workers", type=int, default=4,
                     help="host processes feeding fresh seeded scenes into the reset bank in a last timed pass (0: off)")
     ap.add_argument("--info-mode", default="none", choices=("none", "full"),
@@ -329,7 +348,7 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=device)
     from carlabev_env_amd._lib import check, lib
-    env, host_recs = build_env(cfgd, n, rank, device, args.info_mode)
+    env, host_recs = build_env(cfgd, n, rank, device, args.info_mode, args.scene_cache)
     P = env.params
     total_steps = args.warmup + args.steps
     acts = torch.from_numpy(make_actions(P, n, total_steps, cfgd["act_seed"], rank * n)).to(device)
