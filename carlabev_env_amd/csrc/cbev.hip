@@ -1077,6 +1077,132 @@ __global__ __launch_bounds__(256) void k_actors(KArgs K, uint8_t* __restrict__ r
 }
 
 
+// The output pass at S=256 (measured faster there: 62 vs 68 us per launch at
+// config 5; the 16-byte-store pass below wins at S=128): over one wave's chunks
+// of 1024 output pixels (16 / G rows), a chunk is four 256-pixel dword groups: in group d lane l owns the 4
+// consecutive output pixels 256 d + 4 l .. + 3 of the chunk (row r + d (4 / G)
+// + l / (16 G), columns 4 (l % (16 G)) .. + 3), gathers them one column step
+// apart and packs them into one dword, so each group is ONE 256-byte dword
+// store. Source coordinates are stepped, not recomputed (pygame's rotozoom is
+// affine in the output pixel): per gather one 64-bit add, a 24-bit
+// multiply-add for the LDS byte address, the LDS read, the nibble extract and
+// the pack.
+//   CHECK = false: the rotated surface covers the whole output and every output
+//   pixel samples inside the crop (checked once per env at the four corners;
+//   the map is affine) -> no per-pixel tests.
+//   CHECK = true: compose clipping (black outside the rotated surface) and the
+//   rotozoom background test (bg outside the source), per pixel.
+template <int G, bool R90, bool CHECK, int NW>
+__device__ __forceinline__ void raster_out4(const cbev_params& P, const RotSetup& R, const uint8_t* __restrict__ lds,
+                                           int shift, uint32_t bg, uint8_t* __restrict__ out, int nout,
+                                           int64_t out_stride, int lane, int wave,
+                                           const uint32_t* __restrict__ fov) {
+  constexpr int RPC = 16 / G;  // output rows per chunk
+  constexpr int S = 64 * G;    // == P.size
+  constexpr int LPR = S / 4;   // lanes per output row
+  constexpr int RPD = 4 / G;   // output rows per dword group
+  const int C = P.crop;
+  const uint32_t vmax = (uint32_t)((C << 16) - 1);
+  const int hero_w = P.hero_w;
+  const int hx0 = P.anchor_x - hero_w / 2, hy0 = P.anchor_y - hero_w / 2;
+  const int lrow = lane / LPR, lcol = 4 * (lane % LPR);
+  // this lane's columns: hero byte mask (Hero.draw: black w x w rect at the
+  // anchor, hero.py:26-32) and the compose-clip column test
+  uint32_t hmask = 0, xok = 0;
+#pragma unroll
+  for (int b = 0; b < 4; ++b) {
+    const int u = lcol + b;
+    if (u >= hx0 && u < hx0 + hero_w) hmask |= 0xffu << (8 * b);
+    const int xx = u - R.rx0;
+    if (xx >= 0 && xx < R.nx) xok |= 1u << b;
+  }
+  const uint32_t hblack = hmask & (CBEV_PX_BLACK * 0x01010101u);
+  const int r0 = wave * RPC;
+  const int xx0 = lcol - R.rx0, yy0 = r0 + lrow - R.ry0;
+  // lane state at (output row r0 + lrow, column lcol) of this wave's first chunk
+  int sx = R.dx00 + xx0 * R.icos - yy0 * R.isin;  // 16.16 source x (general)
+  int sy = R.dy00 + xx0 * R.isin + yy0 * R.icos;  // 16.16 source y (general)
+  int sa = R.a00 + shift + xx0 * R.ustep + yy0 * R.vstep;  // LDS texel address (rotate90)
+  // the crop's texel offset rides in the integer part of sx, so the LDS byte is
+  // (sy >> 16) * sb + (sx >> 16) (byte image) or (sy >> 16) * sb + (sx >> 17) with
+  // the nibble (sx >> 16) & 1 (nibble image)
+  sx += shift << 16;
+  const uint8_t* img = lds;
+  const uint32_t sb = 4u * (uint32_t)raster_stride_dwords(S, C);  // LDS bytes per crop row
+  const int chunk_rows = NW * RPC;                // the NW output waves interleave chunks
+  const int nchunks = S / RPC;
+  // general path: (sx, sy) packed in one 64-bit value, so one 64-bit add steps
+  // both coordinates (the low word stays in [0, 2^32): no carry crosses over)
+  uint64_t pxy = ((uint64_t)(uint32_t)sy << 32) | (uint32_t)sx;
+  const uint64_t chunk_step =
+      (uint64_t)(((int64_t)(chunk_rows * R.icos) << 32) + (int64_t)(-chunk_rows * R.isin));
+  // one output row down: (dx, dy) += (-isin, icos); one column right: += (icos, isin)
+  const uint64_t group_step = (uint64_t)(((int64_t)(RPD * R.icos) << 32) + (int64_t)(-RPD * R.isin));
+  const uint64_t col_step = (uint64_t)(((int64_t)R.isin << 32) + (int64_t)R.icos);
+  for (int ch = wave, r = r0; ch < nchunks; ch += NW, r += chunk_rows) {
+    // the frame is written through the uniform base `out` plus a per-lane offset
+    const uint32_t vo = (uint32_t)(r * S + 4 * lane);
+    const bool hero_rows = (unsigned)(r + RPC - 1 - hy0) < (unsigned)(RPC - 1 + hero_w);  // chunk meets the hero rows
+    asm volatile("" : "+v"(pxy), "+v"(sa));  // keep the per-gather offsets as scalar adds
+    uint32_t w[4];
+    uint64_t qg = pxy;  // general path: source coordinates of (row r + d RPD + lrow, column lcol)
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      uint32_t acc = 0;
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        uint32_t v;
+        if (R90) {
+          const int a = sa + d * RPD * R.vstep + b * R.ustep;
+          if (CHECK) {
+            const bool ok = ((xok >> b) & 1u) && (unsigned)(r + d * RPD + lrow - R.ry0) < (unsigned)R.ny;
+            v = ok ? lds_texel(img, ok ? a : 0) : (uint32_t)CBEV_PX_BLACK;
+          } else {
+            v = lds_texel(img, a);
+          }
+        } else {
+          const uint64_t q = b == 0 ? qg : qg + (uint64_t)b * col_step;
+          const uint32_t dx = (uint32_t)q, dy = (uint32_t)(q >> 32);
+          const uint32_t byte = __umul24(dy >> 16, sb) + (dx >> 17);
+          const uint32_t nsh = (dx >> 14) & 4u;
+          if (CHECK) {  // bounds on the unshifted source coordinate
+            const int ux = (int)dx - (shift << 16);
+            const bool ok = ((xok >> b) & 1u) && (unsigned)(r + d * RPD + lrow - R.ry0) < (unsigned)R.ny;
+            const bool in = (uint32_t)ux <= vmax && dy <= vmax;
+            const uint32_t s = (img[(in && ok) ? byte : 0u] >> nsh) & 15u;
+            v = !ok ? (uint32_t)CBEV_PX_BLACK : (in ? s : bg);
+          } else {
+            v = (img[byte] >> nsh) & 15u;
+          }
+        }
+        acc |= v << (8 * b);
+      }
+      w[d] = acc;
+      if (!R90) qg += group_step;
+    }
+    if (hero_rows) {
+#pragma unroll
+      for (int d = 0; d < 4; ++d)
+        if ((unsigned)(r + d * RPD + lrow - hy0) < (unsigned)hero_w) w[d] = (w[d] & ~hmask) | hblack;
+    }
+    if (fov) {  // FovRenderer.apply_mask (fov.py:96-99): black corner triangles (uniform branch)
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        const uint32_t fm = fov[(vo >> 2) + 64 * d];
+        w[d] = (w[d] & ~fm) | (fm & (CBEV_PX_BLACK * 0x01010101u));
+      }
+    }
+    for (int k = 0; k < nout; ++k) {
+      uint8_t* ob = out + (int64_t)k * out_stride;
+#pragma unroll
+      for (int d = 0; d < 4; ++d)  // streamed out: keep the L2 for the map and the records
+        __builtin_nontemporal_store(w[d], (uint32_t*)(ob + (vo + (uint32_t)(256 * d))));
+    }
+    pxy += chunk_step;
+    sa += chunk_rows * R.vstep;
+  }
+}
+
 // Output pass over one wave's chunks of 1024 output pixels (16 / G rows). In a
 // chunk lane l owns the 16 consecutive pixels of row r + l / (4 G), columns
 // 16 (l % (4 G)) .. + 15: it gathers them one column step apart, packs them into
@@ -1198,6 +1324,16 @@ template <int G, int NW = 4>
 __device__ __forceinline__ void raster_out_dispatch(const cbev_params& P, const RotSetup& R, bool fast,
                                                     const uint8_t* lds, int shift, uint32_t bg, uint8_t* out, int nout,
                                                     int64_t out_stride, int lane, int wave, const uint32_t* fov) {
+  if (G >= 4) {
+    if (R.r90) {
+      if (fast) raster_out4<G, true, false, NW>(P, R, lds, shift, bg, out, nout, out_stride, lane, wave, fov);
+      else      raster_out4<G, true, true, NW>(P, R, lds, shift, bg, out, nout, out_stride, lane, wave, fov);
+    } else {
+      if (fast) raster_out4<G, false, false, NW>(P, R, lds, shift, bg, out, nout, out_stride, lane, wave, fov);
+      else      raster_out4<G, false, true, NW>(P, R, lds, shift, bg, out, nout, out_stride, lane, wave, fov);
+    }
+    return;
+  }
   if (R.r90) {
     if (fast) raster_out<G, true, false, NW>(P, R, lds, shift, bg, out, nout, out_stride, lane, wave, fov);
     else      raster_out<G, true, true, NW>(P, R, lds, shift, bg, out, nout, out_stride, lane, wave, fov);
