@@ -232,9 +232,25 @@ __device__ __forceinline__ double lane_value(double v, int k) {
 // the lanes' global stores and loads (same CU); agent scope would also flush L2.
 __device__ __forceinline__ void wave_mem_fence() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup"); }
 
-__device__ __noinline__ void wave_start_retreat(DRec& r, int a, int lane) {
+// Takes the record base and the byte offsets of the groups it touches as plain
+// ints: a DRec (or KArgs) reference makes every k_actors wave spill that struct
+// to scratch at launch (12 KB per wave), retreat or not.
+__device__ __noinline__ void wave_start_retreat(uint8_t* base, int o_ad, int o_ai, int o_aix, int o_aiy, int o_arx,
+                                                int o_ary, int o_acx, int o_acy, int o_acyaw, int A, int RA, int a,
+                                                int lane) {
   wave_mem_fence();  // the owner lane's behaviour stores come first
-  const int RA = r.RA;
+  DRec r{};
+  r.ad = (double*)(base + o_ad);
+  r.ai = (int32_t*)(base + o_ai);
+  r.aix = (double*)(base + o_aix);
+  r.aiy = (double*)(base + o_aiy);
+  r.arx = (double*)(base + o_arx);
+  r.ary = (double*)(base + o_ary);
+  r.acx = (double*)(base + o_acx);
+  r.acy = (double*)(base + o_acy);
+  r.acyaw = (double*)(base + o_acyaw);
+  r.A = A;
+  r.RA = RA;
   const int nrx = RAI(r, CBEV_AI_NRX, a);
   int cur = RAI(r, CBEV_AI_TIDX, a);
   if (cur > nrx - 1) cur = nrx - 1;
@@ -918,6 +934,9 @@ __device__ __forceinline__ void hero_env_render_setup(const KArgs& K, DRec r) {
 // More than 64 actors: d_actor_step per lane.
 // calc_target_index of every live actor of one env (nact <= 64): AW lanes per
 // actor, 64 / AW actors per round; returns lane a's result for actor a
+#ifndef ACTOR_BATCH
+#define ACTOR_BATCH 8
+#endif
 template <int AW>
 __device__ __forceinline__ int actor_search(const DRec& r, int nact, uint64_t livem, double fx, double fy, int nrt,
                                             int lane) {
@@ -932,20 +951,30 @@ __device__ __forceinline__ int actor_search(const DRec& r, int nact, uint64_t li
     const bool glive = aa < nact && ((livem >> (aa & 63)) & 1ull);
     const double* cx = r.acx + (int64_t)(aa & 63) * RA;
     const double* cy = r.acy + (int64_t)(aa & 63) * RA;
-    // pass 1: the smallest squared distance (first index) and the runner-up's
+    // pass 1: the smallest squared distance (first index) and the runner-up's.
+    // ACTOR_BATCH points per lane are loaded at once (index clamped to the last
+    // point, so no lane branches around a load) and folded in order with
+    // selects: one memory round trip per batch instead of one per point.
     double m2 = INFINITY, s2 = INFINITY;
     int i2 = 0x7fffffff;
     if (glive) {
-#pragma unroll 8
-      for (int i = sub; i < gn; i += AW) {
-        const double dx = gfx - cx[i], dy = gfy - cy[i];
-        const double d2 = dx * dx + dy * dy;
-        if (d2 < m2) {
-          s2 = m2;
-          m2 = d2;
-          i2 = i;
-        } else if (d2 < s2) {
-          s2 = d2;
+      for (int i0 = sub; i0 < gn; i0 += ACTOR_BATCH * AW) {
+        double px[ACTOR_BATCH], py[ACTOR_BATCH];
+#pragma unroll
+        for (int u = 0; u < ACTOR_BATCH; ++u) {
+          const int i = i0 + u * AW, ic = i < gn ? i : gn - 1;
+          px[u] = cx[ic];
+          py[u] = cy[ic];
+        }
+#pragma unroll
+        for (int u = 0; u < ACTOR_BATCH; ++u) {
+          const int i = i0 + u * AW;
+          const double dx = gfx - px[u], dy = gfy - py[u];
+          const double d2 = i < gn ? dx * dx + dy * dy : INFINITY;
+          const bool lt = d2 < m2;  // serial order: if (d2 < m2) {...} else if (d2 < s2) s2 = d2
+          s2 = lt ? m2 : (d2 < s2 ? d2 : s2);
+          m2 = lt ? d2 : m2;
+          i2 = lt ? i : i2;
         }
       }
     }
@@ -1000,37 +1029,57 @@ __global__ __launch_bounds__(256) void k_actors(KArgs K, uint8_t* __restrict__ r
   // ---- 1
   const int a = lane;
   bool live = false;
-  int nrt = 0, tid0 = 0;
+  int nrt = 0, tid0 = 0, beh = CBEV_BEH_NONE;
   double s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   double fx = 0.0, fy = 0.0, ts = 0.0;
-  // behaviours; a due retreat rebuilds the actor's route with the whole wave
-  const bool retreat = a < nact && d_behavior<true>(r, a, t);
-  uint64_t rm = __ballot(retreat);
-  if (rm) {
-    if (RA <= 64) {
-      while (rm) {
-        const int k = __builtin_ctzll(rm);
-        rm &= rm - 1;
-        wave_start_retreat(r, k, lane);
-      }
-    } else if (WIDE) {
-      if (retreat) d_start_retreat(r, a);
-      wave_mem_fence();
-    }
-  }
-  if (a < nact) {
+  // the fields the step reads, in one round trip; behaviours may change them,
+  // so a wave with any behaviour reads them again after running those
+  auto load_fields = [&]() {
     ts = RAD(r, CBEV_AD_T_SPEED, a);
-    RAD(r, CBEV_AD_CT_SPEED, a) = ts;
     nrt = RAI(r, CBEV_AI_NROUTE, a);
     tid0 = RAI(r, CBEV_AI_TIDX, a);
-    if (tid0 >= nrt - 1) {
-      RAD(r, CBEV_AD_CT_SPEED, a) = 0.0;  // frozen at route end
-    } else {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) s[k] = RAD(r, CBEV_AD_X + k, a);
+  };
+  if (a < nact) {
+    beh = RAI(r, CBEV_AI_BEH, a);
+    load_fields();
+  }
+  if (__ballot(beh != CBEV_BEH_NONE)) {
+    // behaviours; a due retreat rebuilds the actor's route with the whole wave
+    const bool retreat = beh != CBEV_BEH_NONE && d_behavior<true>(r, a, t);
+    uint64_t rm = __ballot(retreat);
+    if (rm) {
+      if (RA <= 64) {
+        while (rm) {
+          const int k = __builtin_ctzll(rm);
+          rm &= rm - 1;
+          wave_start_retreat(recs + (int64_t)e * K.L.record_bytes, (int)K.L.ad, (int)K.L.ai, (int)K.L.aix,
+                             (int)K.L.aiy, (int)K.L.arx, (int)K.L.ary, (int)K.L.acx, (int)K.L.acy,
+                             (int)K.L.acyaw, r.A, RA, k, lane);
+        }
+      } else if (WIDE) {
+        if (retreat) d_start_retreat(r, a);
+        wave_mem_fence();
+      }
+    }
+    if (a < nact) load_fields();
+  }
+  // the points the Stanley step most likely reads (target index unchanged or
+  // one ahead), fetched under the search
+  double pcx[2] = {0.0, 0.0}, pcy[2] = {0.0, 0.0}, pyaw[2] = {0.0, 0.0};
+  if (a < nact) {
+    // frozen at route end: the controller's target speed is 0
+    RAD(r, CBEV_AD_CT_SPEED, a) = tid0 >= nrt - 1 ? 0.0 : ts;
+    if (tid0 < nrt - 1) {
       live = true;
-      s[0] = RAD(r, CBEV_AD_X, a);
-      s[1] = RAD(r, CBEV_AD_Y, a);
-      s[2] = RAD(r, CBEV_AD_YAW, a);
-      s[3] = RAD(r, CBEV_AD_V, a);
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int64_t o = (int64_t)a * RA + tid0 + k;
+        pcx[k] = r.acx[o];
+        pcy[k] = r.acy[o];
+        pyaw[k] = r.acyaw[o];
+      }
       fx = s[0] + CB_WHEELBASE * cos(s[2]);
       fy = s[1] + CB_WHEELBASE * sin(s[2]);
     }
@@ -1058,9 +1107,12 @@ __global__ __launch_bounds__(256) void k_actors(KArgs K, uint8_t* __restrict__ r
     const double* cyaw = r.acyaw + (int64_t)a * RA;
     const double yaw = s[2];
     const double fa0 = -cos(yaw + CB_PI / 2.0), fa1 = -sin(yaw + CB_PI / 2.0);
-    const double err = (fx - cx[best]) * fa0 + (fy - cy[best]) * fa1;
-    const int cur = tid0 >= best ? tid0 : best;
-    const double theta_e = d_angle_mod(cyaw[cur] - yaw);
+    const int db = best - tid0, cur = tid0 >= best ? tid0 : best;
+    const double bx = db == 0 ? pcx[0] : db == 1 ? pcx[1] : cx[best];
+    const double by = db == 0 ? pcy[0] : db == 1 ? pcy[1] : cy[best];
+    const double cyw = cur == tid0 ? pyaw[0] : cur == tid0 + 1 ? pyaw[1] : cyaw[cur];
+    const double err = (fx - bx) * fa0 + (fy - by) * fa1;
+    const double theta_e = d_angle_mod(cyw - yaw);
     const double theta_d = atan2(2.0 * err, d_pymax(s[3], 1e-3));
     const double max_steer = 30.0 * (CB_PI / 180.0);
     const double di = d_clip(theta_e + theta_d, -max_steer, max_steer);

@@ -3,7 +3,7 @@
 # crash, abort or timeout ends the call.
 set -u
 mkdir -p gpurun_out
-timeout -k 10 ${TEST_LIMIT:-600} python -u -m pytest tests -x -v -m gpu --timeout 180 --timeout-method thread ${PYTEST_ARGS:-} > gpurun_out/pytest_gpu.txt 2>&1
+timeout -k 10 ${TEST_LIMIT:-600} python -u -m pytest tests -x -v -m gpu --timeout 180 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} ${PYTEST_ARGS:-} > gpurun_out/pytest_gpu.txt 2>&1
 rc=$?
 tail -n 40 gpurun_out/pytest_gpu.txt
 [ $rc -ne 0 ] && { echo "pytest rc=$rc"; exit $rc; }
