@@ -934,9 +934,7 @@ __device__ __forceinline__ void hero_env_render_setup(const KArgs& K, DRec r) {
 // More than 64 actors: d_actor_step per lane.
 // calc_target_index of every live actor of one env (nact <= 64): AW lanes per
 // actor, 64 / AW actors per round; returns lane a's result for actor a
-#ifndef ACTOR_BATCH
-#define ACTOR_BATCH 8
-#endif
+constexpr int ACTOR_BATCH = 8;  // route points per lane loaded at once in the target search
 template <int AW>
 __device__ __forceinline__ int actor_search(const DRec& r, int nact, uint64_t livem, double fx, double fy, int nrt,
                                             int lane) {
@@ -1757,16 +1755,20 @@ __global__ __launch_bounds__(256) void k_bank_frames(KArgs K, const uint8_t* __r
 
 // Partial reset from a bank with cached reset frames: records[e] <- bank[b] and
 // bank_frames[b] into every frame-stack slot of env e, for the envs selected by
-// mask. Pure 16-byte copies, split into 4 KB pieces (one per 256-thread pass):
-// RESET_PIECE_F frame pieces (each written to every ring slot) and
-// RESET_PIECE_R record pieces per env. The pieces of the selected envs are
-// dealt round-robin over the workgroups of the env's XCD (env block e / 64 ->
-// XCD (e / 64) % 8, as in the step kernels; workgroup w runs on XCD w % 8), so a
-// reset's copies spread over many CUs instead of one workgroup per env: every
-// workgroup ballots the masks of its XCD's env blocks and counts the selected
-// envs' pieces in env order, taking every WPX-th.
-__host__ __device__ __forceinline__ int reset_pieces_frame(int64_t SS) { return (int)((SS + 4095) / 4096); }
-__host__ __device__ __forceinline__ int reset_pieces_rec(int64_t rb) { return (int)((rb + 4095) / 4096); }
+// mask. Pure 16-byte copies, split into 16 KB pieces: one pass of the 256
+// threads with RESET_PU 16-byte loads each in flight, then the stores. An env's
+// pieces are its frame's (each written to every ring slot), then its record's.
+// The pieces of the selected envs are dealt round-robin over the workgroups of
+// the env's XCD (env block e / 64 -> XCD (e / 64) % 8, as in the step kernels;
+// workgroup w runs on XCD w % 8), so a reset's copies spread over many CUs
+// instead of one workgroup per env: every workgroup ballots the masks of its
+// XCD's env blocks and counts the selected envs' pieces in env order, taking
+// every WPX-th.
+#define RESET_PU 4                      // 16-byte loads per thread in flight
+#define RESET_PIECE (4096 * RESET_PU)   // bytes per piece
+__host__ __device__ __forceinline__ int reset_pieces(int64_t bytes) {
+  return (int)((bytes + RESET_PIECE - 1) / RESET_PIECE);
+}
 
 __global__ __launch_bounds__(256) void k_reset_copy(KArgs K, uint8_t* __restrict__ recs, int n,
                                                     const uint8_t* __restrict__ bank, int n_bank,
@@ -1777,7 +1779,7 @@ __global__ __launch_bounds__(256) void k_reset_copy(KArgs K, uint8_t* __restrict
   const int64_t rb = K.L.record_bytes;
   const int64_t SS = (int64_t)K.P.size * K.P.size;
   const int lane = threadIdx.x & 63;
-  const int pf = reset_pieces_frame(SS), ppe = pf + reset_pieces_rec(rb);
+  const int pf = reset_pieces(SS), ppe = pf + reset_pieces(rb);
   const int myx = blockIdx.x & 7, wpx = gridDim.x >> 3, wk = blockIdx.x >> 3;  // gridDim.x % 8 == 0
   int t = 0;  // pieces of this XCD's selected envs counted so far (uniform)
   for (int base0 = 64 * myx; base0 < n; base0 += 8 * 512) {  // this XCD's env blocks, 8 mask loads in flight
@@ -1802,17 +1804,31 @@ __global__ __launch_bounds__(256) void k_reset_copy(KArgs K, uint8_t* __restrict
       int b = bank_idx ? bank_idx[e] : (int)(((int64_t)e + bank_offset) % n_bank);
       b = b < 0 ? 0 : (b >= n_bank ? n_bank - 1 : b);
       for (int c = first; c < ppe; c += wpx) {
-        if (c < pf) {
-          const int64_t i = (int64_t)c * 256 + threadIdx.x;  // uint4 index in the frame
-          if (i < SS / 16) {
-            const uint4 v = ((const uint4*)(bank_frames + (int64_t)b * SS))[i];
-            for (int f = 0; f < n_frames; ++f) ((uint4*)(ring + ((int64_t)f * n + e) * SS))[i] = v;
-          }
-        } else {
-          const int64_t i = (int64_t)(c - pf) * 256 + threadIdx.x;  // uint4 index in the record
-          if (i < rb / 16) ((uint4*)(recs + (int64_t)e * rb))[i] = ((const uint4*)(bank + (int64_t)b * rb))[i];
-          if (c == pf && threadIdx.x == 0 && K.stats != nullptr) K.stats[e].t0 = (double)wall_clock64();
+        const bool fr = c < pf;  // uniform
+        const uint8_t* src = fr ? bank_frames + (int64_t)b * SS : bank + (int64_t)b * rb;
+        uint8_t* dst = fr ? ring + (int64_t)e * SS : recs + (int64_t)e * rb;
+        const int64_t lim = fr ? SS : rb;
+        const int64_t o0 = (int64_t)(fr ? c : c - pf) * RESET_PIECE + 16 * (int64_t)threadIdx.x;
+        uint4 v[RESET_PU];
+#pragma unroll
+        for (int j = 0; j < RESET_PU; ++j) {
+          const int64_t o = o0 + 4096 * j;
+          v[j] = *(const uint4*)(src + (o < lim ? o : 0));
         }
+        // every load issued before any store (pinned: no sinking under the bounds tests)
+#pragma unroll
+        for (int j = 0; j < RESET_PU; ++j) asm volatile("" ::"v"(v[j].x), "v"(v[j].y), "v"(v[j].z), "v"(v[j].w));
+#pragma unroll
+        for (int j = 0; j < RESET_PU; ++j) {
+          const int64_t o = o0 + 4096 * j;
+          if (o >= lim) continue;
+          if (fr) {
+            for (int f = 0; f < n_frames; ++f) *(uint4*)(dst + (int64_t)f * n * SS + o) = v[j];
+          } else {
+            *(uint4*)(dst + o) = v[j];
+          }
+        }
+        if (c == pf && threadIdx.x == 0 && K.stats != nullptr) K.stats[e].t0 = (double)wall_clock64();
       }
     }
     }
@@ -3283,8 +3299,7 @@ int cbev_reset_frames(cbev_ctx* c, void* records, int n, const void* bank, int n
   if (n <= 0) return CBEV_OK;
   KArgs K = kargs(c);
   // 8 .. RESET_WGS workgroups, a multiple of 8 (k_reset_copy's per-XCD dealing)
-  const int64_t pieces = (int64_t)n * (reset_pieces_frame((int64_t)c->P.size * c->P.size) +
-                                       reset_pieces_rec(c->L.record_bytes));
+  const int64_t pieces = (int64_t)n * (reset_pieces((int64_t)c->P.size * c->P.size) + reset_pieces(c->L.record_bytes));
   // grid cap for masked resets (the canonical reset of the envs that terminated):
   // 1024 measured best (config 2: 6.0 / 6.2 / 6.6 / 7.6 / 10.9 us at 1024 / 256 / 128 / 2048 / 4096)
   const int cap = mask ? RESET_WGS : RESET_WGS;
