@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-$(pwd)}"
 OUT=gpurun_out/prof
 mkdir -p $OUT
 export TMPDIR=/tmp
-ARGS=${BENCH_ARGS:---steps 50 --warmup 5 --no-cpu-baseline --no-wire}
+ARGS=${BENCH_ARGS:---steps 50 --warmup 5 --no-cpu-baseline --no-wire --fresh-workers 0}
 run() {  # name, limit, rocprof args...
   local name=$1 lim=$2; shift 2
   timeout -k 10 "$lim" rocprofv3 "$@" -d $OUT/$name -o $name --output-format csv -- python bench.py $ARGS > $OUT/$name.log 2>&1
@@ -23,4 +23,7 @@ run pmc_sq2 400 --kernel-trace --pmc SQ_WAIT_INST_LDS SQ_BUSY_CYCLES SQ_WAVE_CYC
 run pmc_tcc 400 --kernel-trace --pmc TCC_HIT_sum TCC_MISS_sum
 run pmc_wait 400 --kernel-trace --pmc SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU
 run pmc_lds 400 --kernel-trace --pmc SQ_ACTIVE_INST_LDS SQ_LDS_IDX_ACTIVE SQ_INSTS_VMEM_WR SQ_INSTS_SALU
+# summaries only (the raw traces exceed what gpurun copies back)
+python tools/summarize_profile.py --src $OUT --tag ${TAG:-round2} --config ${CFG:-2} --envs ${ENVS:-4096} --out gpurun_out/psum || exit 1
+rm -rf $OUT
 exit 0

@@ -22,11 +22,12 @@ ap.add_argument("--src", default="gpurun_out/prof")
 ap.add_argument("--tag", default="round1")
 ap.add_argument("--config", type=int, default=2)
 ap.add_argument("--envs", type=int, default=4096)
+ap.add_argument("--out", default="profiles")
 a = ap.parse_args()
 
-os.makedirs("profiles", exist_ok=True)
+os.makedirs(a.out, exist_ok=True)
 stats = os.path.join(a.src, "trace", "trace_kernel_stats.csv")
-shutil.copy(stats, f"profiles/{a.tag}_kernel_stats.csv")
+shutil.copy(stats, f"{a.out}/{a.tag}_kernel_stats.csv")
 pmc = collections.defaultdict(lambda: collections.defaultdict(list))
 for f in sorted(glob.glob(os.path.join(a.src, "pmc_*", "*counter_collection.csv"))):
     for r in csv.DictReader(open(f)):
@@ -38,12 +39,12 @@ for r in csv.DictReader(open(stats)):
     name = r["Name"].split("(")[0].replace("void ", "")
     if name.startswith("k_"):
         dur[name] = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"])}
-json.dump({"kernel_trace": dur, "pmc_mean_per_dispatch": summary}, open(f"profiles/{a.tag}_pmc.json", "w"),
+json.dump({"kernel_trace": dur, "pmc_mean_per_dispatch": summary}, open(f"{a.out}/{a.tag}_pmc.json", "w"),
           indent=1, sort_keys=True)
 rk = next(k for k in summary if k.startswith("k_raster"))
 fetch_kb, write_kb = summary[rk]["FETCH_SIZE"], summary[rk]["WRITE_SIZE"]
 out = {"kernel": rk, "config": a.config, "envs": a.envs, "fetch_kb": fetch_kb, "write_kb": write_kb,
        "hbm_bytes_per_launch": (2 * fetch_kb + write_kb) * 1024,
        "avg_ns": dur.get(rk, {}).get("avg_ns"), "source": f"{a.tag} rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes"}
-json.dump(out, open(f"profiles/pmc_raster_config{a.config}.json", "w"), indent=1)
+json.dump(out, open(f"{a.out}/pmc_raster_config{a.config}.json", "w"), indent=1)
 print(json.dumps(out))
