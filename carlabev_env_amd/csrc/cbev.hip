@@ -1015,23 +1015,14 @@ __global__ __launch_bounds__(256) void k_actors(KArgs K, uint8_t* __restrict__ r
   const int e = xcd_env4_of_wg(blockIdx.x, threadIdx.x >> 6, n);
   if (e >= n) return;
   DRec r = bind_rec(recs + (int64_t)e * K.L.record_bytes, K.L, K.C);
-  const int nact = r.hi[CBEV_HI_NACT];
-  if (nact == 0) return;
-  const double t = r.hd[CBEV_HD_T] + CB_DT;
-  if (WIDE && nact > 64) {
-    for (int a = lane; a < nact; a += 64) d_actor_step(r, a, t);
-    return;
-  }
   const int RA = r.RA;
-  CBEV_STAMPW(6, 0);
-  // ---- 1
   const int a = lane;
   bool live = false;
   int nrt = 0, tid0 = 0, beh = CBEV_BEH_NONE;
   double s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   double fx = 0.0, fy = 0.0, ts = 0.0;
-  // the fields the step reads, in one round trip; behaviours may change them,
-  // so a wave with any behaviour reads them again after running those
+  // the fields the step reads; behaviours may change them, so a wave with any
+  // behaviour reads them again after running those
   auto load_fields = [&]() {
     ts = RAD(r, CBEV_AD_T_SPEED, a);
     nrt = RAI(r, CBEV_AI_NROUTE, a);
@@ -1039,10 +1030,24 @@ __global__ __launch_bounds__(256) void k_actors(KArgs K, uint8_t* __restrict__ r
 #pragma unroll
     for (int k = 0; k < 4; ++k) s[k] = RAD(r, CBEV_AD_X + k, a);
   };
-  if (a < nact) {
+  // read for every actor slot in the same round trip as NACT and the clock
+  // (slots past NACT are not used); pinned here so the loads are not sunk
+  // below the NACT test into a second round trip
+  if (a < r.A) {
     beh = RAI(r, CBEV_AI_BEH, a);
     load_fields();
   }
+  const int nact = r.hi[CBEV_HI_NACT];
+  const double t = r.hd[CBEV_HD_T] + CB_DT;
+  asm volatile("" ::"v"(beh), "v"(nrt), "v"(tid0), "v"(ts), "v"(s[0]), "v"(s[1]), "v"(s[2]), "v"(s[3]));
+  if (nact == 0) return;
+  if (WIDE && nact > 64) {
+    for (int k = lane; k < nact; k += 64) d_actor_step(r, k, t);
+    return;
+  }
+  if (a >= nact) beh = CBEV_BEH_NONE;
+  CBEV_STAMPW(6, 0);
+  // ---- 1
   if (__ballot(beh != CBEV_BEH_NONE)) {
     // behaviours; a due retreat rebuilds the actor's route with the whole wave
     const bool retreat = beh != CBEV_BEH_NONE && d_behavior<true>(r, a, t);
