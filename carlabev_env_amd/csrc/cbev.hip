@@ -1687,8 +1687,13 @@ __global__ __launch_bounds__(raster_threads(64 * G)) __attribute__((amdgpu_waves
   RasterJob J;
   raster_origin<false, G>(K, r, J);
   raster_rot<false, G>(K, r, J);
+  // staging at raised wave priority: the CU's other workgroups are mostly
+  // painting or writing out, and issuing this one's map loads first keeps the
+  // memory pipe busier (raster 25.5 -> 24.9 us at config 2)
+  __builtin_amdgcn_s_setprio(2);
   J.pq = raster_paint_fetch(r);  // in flight under the staging
   stage_all<G, NT>(K, J, lds);
+  __builtin_amdgcn_s_setprio(0);
   __syncthreads();
   CBEV_STAMP(2, 1);
   raster_paint<NT>(K, r, J.pq, J.xmin, J.ymin, J.shift, lds);
