@@ -1438,16 +1438,27 @@ __device__ __forceinline__ PaintPre raster_paint_fetch(const DRec& r) {
 }
 
 // one rect of side sz (rect_from_world_center, transforms.py:46-51) by the 4
-// threads of tid >> 2: thread tq covers columns tq, tq + 4, ...
+// threads of tid >> 2: thread tq covers rows tq, tq + 4, ..., each row's span
+// clipped to the crop and written a whole LDS dword (8 texels) at a time: one
+// and-mask + or-colour pair per dword it touches. Every rect of a paint pass has
+// the same colour, so overlapping rects commute; rows of an LDS image are
+// dword-aligned (rt is a multiple of 8).
 __device__ __forceinline__ void paint_rect4(uint8_t* lds, int rt, int shift, int C, int pad, int xmin, int ymin,
                                             double wx, double wy, int sz, int tq, uint32_t col) {
   const int rx = d_rect_lo(wx, pad, sz) - xmin, ry = d_rect_lo(wy, pad, sz) - ymin;
-  for (int qy = 0; qy < sz; ++qy) {
+  const int x0 = rx > 0 ? rx : 0, x1 = rx + sz < C ? rx + sz : C;
+  if (x0 >= x1) return;
+  uint32_t* l32 = (uint32_t*)lds;
+  const uint32_t colw = col * 0x11111111u;
+  for (int qy = tq; qy < sz; qy += 4) {
     const int py = ry + qy;
     if (py < 0 || py >= C) continue;
-    for (int qx = tq; qx < sz; qx += 4) {
-      const int px = rx + qx;
-      if (px >= 0 && px < C) lds_set_texel(lds, py * rt + shift + px, col);
+    const uint32_t t0 = (uint32_t)(py * rt + shift + x0), t1 = (uint32_t)(py * rt + shift + x1);
+    for (uint32_t w = t0 >> 3; w <= (t1 - 1) >> 3; ++w) {
+      const uint32_t lo = t0 > 8 * w ? t0 - 8 * w : 0u, hi = t1 < 8 * w + 8 ? t1 - 8 * w : 8u;  // nibbles [lo, hi)
+      const uint32_t m = (hi - lo == 8u ? 0xffffffffu : ((1u << (4u * (hi - lo))) - 1u)) << (4u * lo);
+      atomicAnd(l32 + w, ~m);
+      atomicOr(l32 + w, colw & m);
     }
   }
 }
