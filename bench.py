@@ -47,6 +47,7 @@ CONFIGS = {
 }
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip-level parameters (spec)
+BANK_MIN = 4096  # reset-bank rows at least (the seeded start scenes + more seeded scenes)
 
 
 def log(*a):
@@ -84,7 +85,9 @@ def build_env(cfgd, n, rank, device, info_mode="none", cache=None):
     env = CarlaBEVVectorEnv({"env": cfg, "num_envs": n}, device=device, caps=cfgd["caps"], info_mode=info_mode)
     first = rank * n
     t0 = time.time()
-    nb = min(n, 512)
+    # the reset bank: the n seeded scenes the envs start from, then further seeded
+    # scenes up to BANK_MIN rows; terminated envs take its rows in order
+    nb = max(0, BANK_MIN - n)
     key = None
     if cache:  # scenes are a pure function of (config, n, rank): reuse them across runs on one box
         os.makedirs(cache, exist_ok=True)
@@ -108,13 +111,10 @@ def build_env(cfgd, n, rank, device, info_mode="none", cache=None):
         if key:
             np.save(key + "_recs.npy", host)
             np.save(key + "_bank.npy", bank)
-    recs = torch.from_numpy(host).to(device)
-    env.attach_bank(torch.from_numpy(bank).to(device))
-    # initial reset: records = seeded scenes, reset observation rendered on device
-    env.attach_bank(recs)
+    # initial reset: records = seeded scenes (bank rows 0..n-1), reset observation rendered on device
+    env.attach_bank(torch.from_numpy(np.concatenate([host, bank]) if nb else host).to(device))
     env.auto_obs = False
     env.reset_from_bank(mask=None, bank_idx=torch.arange(n, dtype=torch.int32, device=device))
-    env.attach_bank(torch.from_numpy(bank).to(device))
     return env, host
 
 
@@ -170,6 +170,31 @@ def cpu_baseline(cfgd, host_recs, env, seconds):
             "sample": f"{cores} threads x {per} envs of the same workload ({sm} env-steps in {dm:.1f}s); "
                       f"single thread: {blk} envs ({s1} env-steps in {d1:.1f}s). oracle/cbev_oracle.c, "
                       "per-step full padded-map restore as in scene.py:93"}
+
+
+def measure_peaks(env, device, reps=20):
+    """Bandwidth this box reaches on plain streams the size of one step's frames
+    (HIP events on the current stream): a write-only fill (the raster's output
+    floor) and a device-to-device copy (read + write bytes)."""
+    import torch
+    nbytes = int(env.frames().numel())
+    a = torch.empty(nbytes, dtype=torch.uint8, device=device)
+    b = torch.empty_like(a)
+    out = {}
+    for name, fn, traffic in (("write", lambda: a.fill_(7), nbytes), ("copy", lambda: b.copy_(a), 2 * nbytes)):
+        for _ in range(3):
+            fn()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            fn()
+        e1.record()
+        e1.synchronize()
+        out[f"{name}_gbs"] = round(traffic * reps / (e0.elapsed_time(e1) * 1e-3) / 1e9, 1)
+    out["bytes"] = nbytes
+    out["how"] = f"torch fill_ / copy_ of one step's frame bytes, {reps} back-to-back, HIP events"
+    del a, b
+    return out
 
 
 def _free_port() -> int:
@@ -290,9 +315,9 @@ def fresh_pass(env, pool, one_step, args, world, n, device, seconds=2.0):
         one_step(t, False)
         steps += 1
         if steps % 8 == 0:
-            gids, recs = pool.poll(max_scenes=env.bank.shape[0])
+            gids, recs, ctxs = pool.poll(max_scenes=env.bank.shape[0], contexts=True)
             if len(gids):
-                slot = env.refresh_bank(slot, recs)
+                slot = env.refresh_bank(slot, recs, ctxs)
                 pool.request(len(gids))
             if steps % 64 == 0:  # keep the host no more than ~64 steps ahead of the device
                 torch.cuda.current_stream().synchronize()
@@ -321,6 +346,8 @@ def main():
     ap.add_argument("--scene-cache", default=None, help="directory to keep built scenes in across runs (one box)")
     ap.add_argument("--fresh-workers", type=int, default=4,
                     help="host processes feeding fresh seeded scenes into the reset bank in a last timed pass (0: off)")
+    ap.add_argument("--repeats", type=int, default=5,
+                    help="timed passes of exactly --steps steps each (re-seeded between); value = their median")
     ap.add_argument("--info-mode", default="none", choices=("none", "full"),
                     help="full: device episode statistics + a StepInfos per step (not read), as step() returns")
     args = ap.parse_args()
@@ -398,14 +425,10 @@ def main():
             ms3 = [buf[i] / max(cnt.value, 1) for i in range(3)]
         return el, ms3, host_enqueue
 
-    bank = env.bank
-    seeded = torch.from_numpy(host_recs).to(device)
+    start_idx = torch.arange(n, dtype=torch.int32, device=device)
 
-    def reseed():  # back to the seeded scenes, so every pass replays a comparable workload
-        env.attach_bank(seeded)
-        env.reset_from_bank(mask=None, bank_idx=torch.arange(n, dtype=torch.int32, device=device))
-        env.attach_bank(bank)
-        env._bank_cursor = 0
+    def reseed():  # back to the seeded start scenes (bank rows 0..n-1), so every pass replays a comparable workload
+        env.reset_from_bank(mask=None, bank_idx=start_idx)
 
     # The step runs on a stream of its own: launches on HIP's legacy default
     # stream carry implicit synchronisation that costs several us per kernel.
@@ -418,8 +441,16 @@ def main():
             for t in range(min(20, total_steps)):
                 one_step(t, False)
             torch.cuda.synchronize()
-        reseed()
-        el, _, host_enq = timed(False, False)  # headline pass, no instrumentation
+        passes = []
+        rows0 = env.bank_rows_used()
+        for _ in range(max(1, args.repeats)):  # headline passes, no instrumentation
+            reseed()
+            passes.append(timed(False, False))
+        rows_used = env.bank_rows_used() - rows0
+        els = sorted(p[0] for p in passes)
+        el = els[len(els) // 2]
+        host_enq = sorted(p[2] for p in passes)[len(els) // 2]
+        peak = measure_peaks(env, device)
         reseed()
         el_prof, ms3, _ = timed(False, True)  # same workload with HIP events around each kernel (roofline)
         value = world * n * args.steps / el
@@ -476,12 +507,21 @@ def main():
             "config": {"workload": cfgd["workload"], "config_id": args.config, "envs_per_gpu": n,
                        "global_envs": n * world, "obs_size": S, "obs_mode": cfgd["obs_mode"],
                        "parallelism": f"env-sharded x{world}" + (" + RCCL gather" if gather else "")},
+            "repeats": len(els),
+            "ms_per_step_min_max": [round(els[0] / args.steps * 1e3, 4), round(els[-1] / args.steps * 1e3, 4)],
+            "value_min_max": [round(world * n * args.steps / els[-1], 1), round(world * n * args.steps / els[0], 1)],
+            "bank_scenes": int(env.bank.shape[0]),
+            "bank_resets_in_headline_passes": rows_used,
+            # resets take bank rows in order (cursor), so any run of up to B consecutive resets is all distinct
+            "distinct_scenes_per_1k_resets": min(1000, int(env.bank.shape[0])),
             "host_enqueue_ms_per_step": round(host_enq / args.steps * 1e3, 4),
             "ms_per_step_with_kernel_events": round(el_prof / args.steps * 1e3, 4),
             "kernel_ms": {"k_actors": round(ms3[0], 5), "k_ego": round(ms3[1], 5), "k_raster": round(ms3[2], 5)},
             "raster_ms_per_launch": None if burst_ms is None else round(burst_ms, 5),
             "roofline": {"bound": "hbm", "kernel": "k_raster", "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "peak_measured": peak,
+                         "frac_of_measured_write": round(achieved / peak["write_gbs"], 4),
                          "traffic": traffic, "algorithmic_bytes_per_env": algo_bytes,
                          "timing": (f"HIP events around {args.raster_reps} back-to-back launches on the step stream"
                                     if burst_ms is not None else "HIP events around each launch in the timed steps"),

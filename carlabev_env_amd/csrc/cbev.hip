@@ -1786,6 +1786,7 @@ __global__ __launch_bounds__(256) void k_bank_frames(KArgs K, const uint8_t* __r
 // XCD's env blocks and counts the selected envs' pieces in env order, taking
 // every WPX-th.
 #define RESET_PU 4                      // 16-byte loads per thread in flight
+#define RESET_LIST_WGS 512              // k_reset_list's grid cap
 #define RESET_PIECE (4096 * RESET_PU)   // bytes per piece
 __host__ __device__ __forceinline__ int reset_pieces(int64_t bytes) {
   return (int)((bytes + RESET_PIECE - 1) / RESET_PIECE);
@@ -1853,6 +1854,66 @@ __global__ __launch_bounds__(256) void k_reset_copy(KArgs K, uint8_t* __restrict
       }
     }
     }
+  }
+}
+
+// Canonical-loop reset (reset(reset_mask=terminated), tools/debug_env.py:56-132)
+// from the termination list the last k_ego wrote: records[e] <- bank[b] and
+// bank_frames[b] into every frame-stack slot of env e, for the `count` listed
+// envs only (no scan of an n-entry mask). The list is in atomic order, so each
+// env's bank row comes from its rank among the listed env ids: the k-th
+// terminated env in id order takes bank[(cursor + k) % n_bank], which walks the
+// whole bank in order (every reset a distinct scene until it wraps) and does not
+// depend on the order the terminations were appended in. Pieces as in
+// k_reset_copy (16 KB, RESET_PU loads per thread in flight), dealt over the grid.
+__global__ __launch_bounds__(256) void k_reset_list(KArgs K, uint8_t* __restrict__ recs, int n,
+                                                    const uint8_t* __restrict__ bank, int n_bank,
+                                                    const int32_t* __restrict__ list, const uint32_t* __restrict__ count,
+                                                    const unsigned long long* __restrict__ cursor,
+                                                    const uint8_t* __restrict__ bank_frames, uint8_t* __restrict__ ring,
+                                                    int n_frames) {
+  const int cnt = min((int)__builtin_amdgcn_readfirstlane(*count), n);
+  if (cnt == 0) return;
+  const int64_t rb = K.L.record_bytes;
+  const int64_t SS = (int64_t)K.P.size * K.P.size;
+  const int pf = reset_pieces(SS), ppe = pf + reset_pieces(rb);
+  const int total = cnt * ppe;
+  if ((int)blockIdx.x >= total) return;
+  const unsigned long long cur = *cursor;
+  for (int p = blockIdx.x; p < total; p += gridDim.x) {
+    const int slot = p / ppe, c = p - slot * ppe;
+    const int e = list[slot];
+    // rank of e among the listed ids (ids are distinct: one append per terminated env)
+    int rank = 0;
+    for (int j0 = 0; j0 < cnt; j0 += 256) {
+      const int j = j0 + (int)threadIdx.x;
+      rank += __syncthreads_count(j < cnt && list[j] < e);
+    }
+    const int b = (int)((cur + (unsigned long long)rank) % (unsigned long long)n_bank);
+    const bool fr = c < pf;  // uniform
+    const uint8_t* src = fr ? bank_frames + (int64_t)b * SS : bank + (int64_t)b * rb;
+    uint8_t* dst = fr ? ring + (int64_t)e * SS : recs + (int64_t)e * rb;
+    const int64_t lim = fr ? SS : rb;
+    const int64_t o0 = (int64_t)(fr ? c : c - pf) * RESET_PIECE + 16 * (int64_t)threadIdx.x;
+    uint4 v[RESET_PU];
+#pragma unroll
+    for (int j = 0; j < RESET_PU; ++j) {
+      const int64_t o = o0 + 4096 * j;
+      v[j] = *(const uint4*)(src + (o < lim ? o : 0));
+    }
+#pragma unroll
+    for (int j = 0; j < RESET_PU; ++j) asm volatile("" ::"v"(v[j].x), "v"(v[j].y), "v"(v[j].z), "v"(v[j].w));
+#pragma unroll
+    for (int j = 0; j < RESET_PU; ++j) {
+      const int64_t o = o0 + 4096 * j;
+      if (o >= lim) continue;
+      if (fr) {
+        for (int f = 0; f < n_frames; ++f) *(uint4*)(dst + (int64_t)f * n * SS + o) = v[j];
+      } else {
+        *(uint4*)(dst + o) = v[j];
+      }
+    }
+    if (c == pf && threadIdx.x == 0 && K.stats != nullptr) K.stats[e].t0 = (double)wall_clock64();
   }
 }
 
@@ -2251,6 +2312,7 @@ __device__ __forceinline__ void collide_env(const KArgs& K, DRec r, int e, const
   if (terminal) {
     atomicAdd(K.nterm, 1ull);
     if (K.stats != nullptr) d_episode_summary(K, r, e);
+    if (K.tl_list != nullptr) K.tl_list[atomicAdd(K.tl_count, 1u)] = e;  // cbev_reset_terminated's list
   }
   reward_out[e] = reward;
   term_out[e] = (uint8_t)terminal;
@@ -2309,7 +2371,13 @@ __global__ __launch_bounds__(256) void k_ego(KArgs K, uint8_t* __restrict__ recs
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   auto rec = [&](int k) { return bind_ego(lds + k * pk.bytes, recs + (int64_t)(e0 + k) * rb, K, pk); };
-  if (blockIdx.x == 0 && tid == 0 && K.ep_count_next != nullptr) *K.ep_count_next = 0;
+  if (blockIdx.x == 0 && tid == 0) {
+    if (K.ep_count_next != nullptr) *K.ep_count_next = 0;
+    if (K.tl_count_next != nullptr) {  // the previous step's resets took bank rows [cursor, cursor + count)
+      *K.tl_cursor += *K.tl_count_next;
+      *K.tl_count_next = 0;
+    }
+  }
   CBEV_STAMP(0, 0);
   // S0 (wave 0 runs the chain, wave 1 the steering tangent)
   float ag = 0.f, asa = 0.f, ab = 0.f;
@@ -2871,20 +2939,30 @@ struct cbev_ctx {
   int ep_ring, ep_n;
   int64_t step_count;         // cbev_step calls since cbev_set_episode_stats
   double tick_s;
+  // termination list of the last cbev_step (cbev_reset_terminated)
+  int32_t* tl_list_dev;       // [tl_cap]
+  int tl_cap;
+  uint32_t* tl_count_dev;     // [2]: step parity
+  unsigned long long* tl_cursor_dev;
+  int tl_parity;              // counter the next cbev_step appends to
+  int tl_last_n;              // n of the last cbev_step (0: none yet)
 };
 
 // Envs per k_ego workgroup: small groups spread the record staging (LDS-DMA
 // throughput is per CU) and the chains over more CUs; the largest divisor of 64
-// not above CBEV_EGO_NE (default below) whose LDS fits the budget.
+// not above CBEV_EGO_NE (default below) whose LDS fits the budget. Never fewer
+// than 4: the element loops of S2 / S5 give each env 256 / ne threads and reduce
+// them with wave shuffles, which do not cross a 64-lane wave (ne >= 4 keeps an
+// env's threads inside one wave). Returns 0 when 4 envs do not fit.
 static int ego_ne_for(int per_env, int actor_cap) {
   const int budget = 128 * 1024;
   const char* v = getenv("CBEV_EGO_NE");
   // default: 16 envs, fewer when their (env, actor) pairs would need more than one
   // pass of the 256 threads in S5
   int ne = v ? atoi(v) : (actor_cap <= 16 ? 16 : actor_cap <= 32 ? 8 : 4);
-  ne = ne >= 64 ? 64 : ne >= 32 ? 32 : ne >= 16 ? 16 : ne >= 8 ? 8 : ne >= 4 ? 4 : ne >= 2 ? 2 : 1;
-  while (ne > 1 && ne * per_env > budget) ne >>= 1;
-  return ne;
+  ne = ne >= 64 ? 64 : ne >= 32 ? 32 : ne >= 16 ? 16 : ne >= 8 ? 8 : 4;
+  while (ne > 4 && ne * per_env > budget) ne >>= 1;
+  return ne * per_env > budget ? 0 : ne;
 }
 
 static thread_local std::string g_err;
@@ -2973,6 +3051,9 @@ static KArgs kargs(const cbev_ctx* c) {
   K.ep_rows = nullptr;
   K.ep_count = K.ep_count_next = nullptr;
   K.tick_s = c->tick_s;
+  K.tl_list = nullptr;
+  K.tl_count = K.tl_count_next = nullptr;
+  K.tl_cursor = c->tl_cursor_dev;
   return K;
 }
 
@@ -3034,24 +3115,22 @@ int cbev_create(const cbev_params* params, const cbev_caps* caps, int device, cb
     return set_err(CBEV_EINVAL, "bad capacities");
   if (caps->actor_cap > 0 && caps->actor_route_cap < 2) return set_err(CBEV_EINVAL, "actor_route_cap < 2");
   if (raster_lds_bytes(P) > 160 * 1024) return set_err(CBEV_EINVAL, "crop %d needs more LDS than a CU has", P.crop);
+  const cbev_layout lay = cbev_make_layout(*caps);
+  // k_ego LDS per env: packed record ranges + collision scratch + HeroPre + target index
+  const int per_env = ego_pack(lay).bytes + coll_scratch_layout(*caps, lay.vis_words).bytes + (int)sizeof(HeroPre) +
+                      (int)sizeof(int);
+  const int ego_ne = ego_ne_for(per_env, caps->actor_cap);
+  if (ego_ne == 0)
+    return set_err(CBEV_EINVAL, "k_ego stages 4 records per workgroup: %d bytes each do not fit its LDS budget",
+                   per_env);
   HIP_TRY(hipSetDevice(device));
   cbev_ctx* c = (cbev_ctx*)calloc(1, sizeof(cbev_ctx));
   c->P = P;
   c->C = *caps;
-  c->L = cbev_make_layout(*caps);
+  c->L = lay;
   c->device = device;
-  {
-    // k_ego LDS per env: packed record ranges + collision scratch + HeroPre + target index
-    const int per_env = ego_pack(c->L).bytes + coll_scratch_layout(c->C, c->L.vis_words).bytes +
-                        (int)sizeof(HeroPre) + (int)sizeof(int);
-    c->ego_ne = ego_ne_for(per_env, c->C.actor_cap);
-    c->ego_lb = c->ego_ne * per_env;
-    if (c->ego_lb > 160 * 1024) {
-      const int nb = per_env;
-      free(c);
-      return set_err(CBEV_EINVAL, "a record's staged ranges (%d bytes) do not fit LDS", nb);
-    }
-  }
+  c->ego_ne = ego_ne;
+  c->ego_lb = ego_ne * per_env;
   SgTables T;
   build_sg_tables(&T);
   hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(c_sg), &T, sizeof T);
@@ -3060,6 +3139,10 @@ int cbev_create(const cbev_params* params, const cbev_caps* caps, int device, cb
   if (e == hipSuccess) e = hipMemset(c->err_dev, 0, sizeof(int32_t));
   if (e == hipSuccess) e = hipMalloc(&c->nterm_dev, sizeof(unsigned long long));
   if (e == hipSuccess) e = hipMemset(c->nterm_dev, 0, sizeof(unsigned long long));
+  if (e == hipSuccess) e = hipMalloc(&c->tl_count_dev, 2 * sizeof(uint32_t));
+  if (e == hipSuccess) e = hipMemset(c->tl_count_dev, 0, 2 * sizeof(uint32_t));
+  if (e == hipSuccess) e = hipMalloc(&c->tl_cursor_dev, sizeof(unsigned long long));
+  if (e == hipSuccess) e = hipMemset(c->tl_cursor_dev, 0, sizeof(unsigned long long));
   if (e == hipSuccess) {
     int khz = 0;  // wall_clock64() rate
     e = hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device);
@@ -3200,6 +3283,9 @@ void cbev_destroy(cbev_ctx* c) {
   if (c->lut_dev) (void)hipFree(c->lut_dev);
   if (c->err_dev) (void)hipFree(c->err_dev);
   if (c->nterm_dev) (void)hipFree(c->nterm_dev);
+  if (c->tl_list_dev) (void)hipFree(c->tl_list_dev);
+  if (c->tl_count_dev) (void)hipFree(c->tl_count_dev);
+  if (c->tl_cursor_dev) (void)hipFree(c->tl_cursor_dev);
   if (c->area_dev) (void)hipFree(c->area_dev);
   if (c->fov_dev) (void)hipFree(c->fov_dev);
   free(c);
@@ -3237,8 +3323,23 @@ int cbev_step(cbev_ctx* c, void* records, int n, const void* actions, uint8_t* f
     return set_err(CBEV_EINVAL, "null argument");
   if (!c->map_dev) return set_err(CBEV_ESTATE, "cbev_set_map not called");
   if (n <= 0) return CBEV_OK;
+  // every argument check before the first launch, so an error leaves the records untouched
+  if (c->stats && n > c->ep_n) return set_err(CBEV_EINVAL, "n %d exceeds the %d envs of the episode stats", n, c->ep_n);
+  if (n > c->tl_cap) {  // the termination list holds one entry per env (grows once; synchronises)
+    HIP_TRY(hipSetDevice(c->device));
+    if (c->tl_list_dev) HIP_TRY(hipFree(c->tl_list_dev));
+    c->tl_list_dev = nullptr;
+    c->tl_cap = 0;
+    HIP_TRY(hipMalloc(&c->tl_list_dev, (size_t)n * sizeof(int32_t)));
+    c->tl_cap = n;
+  }
   hipStream_t s = (hipStream_t)stream;
   KArgs K = kargs(c);
+  K.tl_list = c->tl_list_dev;
+  K.tl_count = c->tl_count_dev + c->tl_parity;
+  K.tl_count_next = c->tl_count_dev + (c->tl_parity ^ 1);
+  c->tl_parity ^= 1;
+  c->tl_last_n = n;
   const int wg4 = (n + 3) / 4;
   hipEvent_t* ev = nullptr;
   if (c->prof_on && c->prof_n < CBEV_PROF_MAX) ev = c->prof_ev + 4 * c->prof_n++;
@@ -3246,7 +3347,6 @@ int cbev_step(cbev_ctx* c, void* records, int n, const void* actions, uint8_t* f
   if (c->C.actor_cap > 0) hipLaunchKernelGGL(actors_kernel(c->C), dim3(wg4), dim3(256), 0, s, K, (uint8_t*)records, n);
   if (ev) HIP_TRY(hipEventRecord(ev[1], s));
   if (c->stats) {
-    if (n > c->ep_n) return set_err(CBEV_EINVAL, "n %d exceeds the %d envs of the episode stats", n, c->ep_n);
     const int slot = (int)(c->step_count % c->ep_ring), next = (slot + 1) % c->ep_ring;
     K.ep_rows = c->ep_rows + (int64_t)slot * c->ep_n * CBEV_EP_COUNT;
     K.ep_count = c->ep_counts + slot;
@@ -3328,6 +3428,38 @@ int cbev_reset_frames(cbev_ctx* c, void* records, int n, const void* bank, int n
   hipLaunchKernelGGL(k_reset_copy, dim3(grid), dim3(256), 0, (hipStream_t)stream, K, (uint8_t*)records, n,
                      (const uint8_t*)bank, n_bank, mask, bank_idx, bank_offset, bank_frames, frames, n_frames);
   HIP_TRY(hipGetLastError());
+  return CBEV_OK;
+}
+
+int cbev_reset_terminated(cbev_ctx* c, void* records, int n, const void* bank, int n_bank, const uint8_t* bank_frames,
+                          uint8_t* frames, int n_frames, void* stream) {
+  if (!c || !records || !bank || !bank_frames || !frames) return set_err(CBEV_EINVAL, "null argument");
+  if (n_bank <= 0) return set_err(CBEV_EINVAL, "empty bank");
+  if (n_frames < 1) return set_err(CBEV_EINVAL, "n_frames < 1");
+  if (c->tl_last_n == 0) return set_err(CBEV_ESTATE, "cbev_reset_terminated before any cbev_step");
+  if (n != c->tl_last_n) return set_err(CBEV_EINVAL, "n %d != the %d envs of the last cbev_step", n, c->tl_last_n);
+  KArgs K = kargs(c);
+  const int64_t ppe = reset_pieces((int64_t)c->P.size * c->P.size) + reset_pieces(c->L.record_bytes);
+  const int64_t pieces = (int64_t)n * ppe;
+  const int grid = pieces >= RESET_LIST_WGS ? RESET_LIST_WGS : (int)pieces;
+  // the counter the last cbev_step appended to (parity flipped after it)
+  const uint32_t* cnt = c->tl_count_dev + (c->tl_parity ^ 1);
+  hipLaunchKernelGGL(k_reset_list, dim3(grid), dim3(256), 0, (hipStream_t)stream, K, (uint8_t*)records, n,
+                     (const uint8_t*)bank, n_bank, (const int32_t*)c->tl_list_dev, cnt,
+                     (const unsigned long long*)c->tl_cursor_dev, bank_frames, frames, n_frames);
+  HIP_TRY(hipGetLastError());
+  return CBEV_OK;
+}
+
+int cbev_bank_cursor(cbev_ctx* c, int64_t* cursor) {
+  if (!c || !cursor) return set_err(CBEV_EINVAL, "null argument");
+  HIP_TRY(hipSetDevice(c->device));
+  unsigned long long v = 0;
+  HIP_TRY(hipMemcpy(&v, c->tl_cursor_dev, sizeof v, hipMemcpyDeviceToHost));
+  uint32_t cnt[2] = {0, 0};
+  HIP_TRY(hipMemcpy(cnt, c->tl_count_dev, sizeof cnt, hipMemcpyDeviceToHost));
+  // rows taken so far: the folded cursor + the last step's list (taken if it was reset)
+  *cursor = (int64_t)(v + cnt[c->tl_parity ^ 1]);
   return CBEV_OK;
 }
 

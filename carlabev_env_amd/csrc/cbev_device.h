@@ -34,6 +34,14 @@ struct KArgs {
   int32_t* ep_count;          // this step's row count (zeroed by the step before)
   int32_t* ep_count_next;     // the next step's row count, zeroed by this step
   double tick_s;              // seconds per wall_clock64() tick
+  // termination list (cbev_reset_terminated): k_ego appends each env that
+  // terminates to tl_list (tl_count entries); block 0 first folds the previous
+  // step's count into the bank cursor and zeroes it (tl_count_next, the counter
+  // the next step appends to). Null: off.
+  int32_t* tl_list;
+  uint32_t* tl_count;
+  uint32_t* tl_count_next;
+  unsigned long long* tl_cursor;
 };
 
 // class id of padded-map texel (x, y)

@@ -55,13 +55,15 @@ def _worker(cfg_dict, caps, difficulty, seed0, tasks, results):
             return
         gids = task
         out = np.zeros((len(gids), rb), np.uint8)
+        ctxs = []
         try:
             for k, gid in enumerate(gids):
-                builder.build(out[k], None, dict(scene_options(difficulty, gid), scene_seed=seed0 + gid))
+                _, _, ctx = builder.build(out[k], None, dict(scene_options(difficulty, gid), scene_seed=seed0 + gid))
+                ctxs.append(ctx)
         except Exception as exc:  # noqa: BLE001 - reported to the caller by poll()
-            results.put((None, f"{type(exc).__name__}: {exc}"))
+            results.put((None, f"{type(exc).__name__}: {exc}", None))
             continue
-        results.put((gids, out.tobytes()))
+        results.put((gids, out.tobytes(), ctxs))
 
 
 class ScenePool:
@@ -94,25 +96,28 @@ class ScenePool:
             self.requested += k
             n -= k
 
-    def poll(self, max_scenes: int | None = None, timeout: float = 0.0) -> tuple[list, np.ndarray]:
+    def poll(self, max_scenes: int | None = None, timeout: float = 0.0, contexts: bool = False):
         """Finished scenes, without blocking beyond `timeout` seconds for the first
-        batch: (global ids, records uint8[k][record_bytes])."""
-        gids, recs = [], []
+        batch: (global ids, records uint8[k][record_bytes]), plus the scenes'
+        scenario-context dicts when contexts=True (for refresh_bank's CTX_IDs)."""
+        gids, recs, ctxs = [], [], []
         n = 0
         deadline = time.perf_counter() + timeout
         while max_scenes is None or n < max_scenes:
             try:
                 wait = max(0.0, deadline - time.perf_counter()) if not recs else 0.0
-                g, b = self._results.get(timeout=wait) if wait > 0 else self._results.get_nowait()
+                g, b, c = self._results.get(timeout=wait) if wait > 0 else self._results.get_nowait()
             except queue.Empty:
                 break
             if g is None:
                 raise RuntimeError(f"scene pool worker failed: {b}")
             gids.extend(g)
             recs.append(np.frombuffer(b, np.uint8).reshape(len(g), self.rb))
+            ctxs.extend(c)
             n += len(g)
         self.delivered += n
-        return gids, (np.concatenate(recs) if recs else np.zeros((0, self.rb), np.uint8))
+        out = np.concatenate(recs) if recs else np.zeros((0, self.rb), np.uint8)
+        return (gids, out, ctxs) if contexts else (gids, out)
 
     def close(self):
         for _ in self._procs:

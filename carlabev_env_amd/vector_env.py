@@ -238,6 +238,9 @@ class CarlaBEVVectorEnv:
                                            EP_RING), "cbev_set_episode_stats")
         self.bank = None
         self._bank_cursor = 0
+        self._bank_ctx_ids = None  # scenario-context id per bank row set by refresh_bank
+        self._retired_ctx: deque = deque()  # ids of overwritten bank rows, released oldest first
+        self._stepped = False
         self.auto_obs = True  # reset_from_bank also expands the wire observation
         self._closed = False
 
@@ -275,10 +278,19 @@ class CarlaBEVVectorEnv:
         check(lib().cbev_bank_frames(self._ctx, _ptr(self.bank), B, _ptr(self.bank_frames), self._stream()),
               "cbev_bank_frames")
 
-    def refresh_bank(self, slot0: int, records: np.ndarray) -> int:
+    RETIRED_CTX_KEEP = 1 << 16  # contexts of overwritten bank rows kept for envs still running them
+
+    def refresh_bank(self, slot0: int, records: np.ndarray, contexts=None) -> int:
         """Write k fresh scene records (uint8[k][record_bytes], e.g. from a ScenePool)
         into bank rows slot0, slot0 + 1, ... (wrapping) and render their cached reset
-        frames; stream-ordered, no sync. Returns the next slot."""
+        frames; stream-ordered, no sync. Returns the next slot.
+
+        contexts: the k scenes' scenario-context dicts (ScenePool.poll(contexts=True));
+        each gets an id written into its record's CTX_ID, so episodes reset from the
+        row report it in episode_info as the reference merges _scenario_context
+        (carlabev.py:182). The id of an overwritten row is retired: envs may still run
+        that scene, so retired contexts are released only after RETIRED_CTX_KEEP newer
+        ones."""
         if self.bank is None:
             raise RuntimeError("no scene bank attached")
         B, k = self.bank.shape[0], int(records.shape[0])
@@ -286,6 +298,23 @@ class CarlaBEVVectorEnv:
             return slot0
         if records.shape[1] != self.rb or k > B:
             raise ValueError(f"expected at most {B} records of {self.rb} bytes")
+        if contexts is not None:
+            if len(contexts) != k:
+                raise ValueError(f"{len(contexts)} contexts for {k} records")
+            records = np.array(records, copy=True)
+            if self._bank_ctx_ids is None or self._bank_ctx_ids.shape[0] != B:
+                self._bank_ctx_ids = np.zeros(B, dtype=np.int64)
+            ci = LY.HI["CTX_ID"]
+            for j in range(k):
+                row = (slot0 + j) % B
+                old = int(self._bank_ctx_ids[row])
+                if old:
+                    self._retired_ctx.append(old)
+                cid = self._new_ctx_id(contexts[j])
+                self._bank_ctx_ids[row] = cid
+                LY.RecordView(records[j], self.layout).hi[ci] = cid
+            while len(self._retired_ctx) > self.RETIRED_CTX_KEEP:
+                self._ctx_table.pop(self._retired_ctx.popleft(), None)
         src = torch.from_numpy(np.ascontiguousarray(records)).pin_memory()
         done = 0
         s = slot0 % B
@@ -321,11 +350,45 @@ class CarlaBEVVectorEnv:
             LY.RecordView(host[k], self.layout).hi[LY.HI["CTX_ID"]] = self._new_ctx_id(ctx)
         return torch.from_numpy(host).to(self.device)
 
-    def reset_from_bank(self, mask: torch.Tensor | None = None, bank_idx: torch.Tensor | None = None):
-        """Device-only partial reset: env i (mask[i]) <- bank[bank_idx[i]] (default: a rotating
-        offset into the bank), reset frame into every frame-stack slot. One launch, no host sync."""
+    def reset_terminated(self):
+        """The canonical loop's reset(reset_mask=terminated) on the device: the envs the
+        last step terminated (listed by the step kernel, no mask scan) <- the next bank
+        rows in order (bank[(cursor + k) % B] for the k-th of them by env id; the cursor
+        walks the whole bank), reset frame into every frame-stack slot. One launch, no
+        host sync."""
         if self.bank is None:
             raise RuntimeError("no scene bank attached")
+        N, B = self.num_envs, self.bank.shape[0]
+        if self.resize:
+            check(lib().cbev_reset_terminated(self._ctx, _ptr(self.records), N, _ptr(self.bank), B,
+                                              _ptr(self.bank_frames), _ptr(self.full), 1, self._stream()),
+                  "cbev_reset_terminated")
+            self._resize_into_ring(self.term, all_slots=True)
+        else:
+            check(lib().cbev_reset_terminated(self._ctx, _ptr(self.records), N, _ptr(self.bank), B,
+                                              _ptr(self.bank_frames), _ptr(self.ring), self.F, self._stream()),
+                  "cbev_reset_terminated")
+        if not self.auto_obs:
+            return None
+        obs = self._obs()
+        return obs.clone() if self.copy_obs else obs
+
+    def bank_rows_used(self) -> int:
+        """Bank rows reset_terminated() has handed out since the env was created
+        (synchronises); with B rows, resets k .. k + B - 1 all got distinct scenes."""
+        n = ctypes.c_int64()
+        check(lib().cbev_bank_cursor(self._ctx, ctypes.byref(n)), "cbev_bank_cursor")
+        return int(n.value)
+
+    def reset_from_bank(self, mask: torch.Tensor | None = None, bank_idx: torch.Tensor | None = None):
+        """Device-only partial reset: env i (mask[i]) <- bank[bank_idx[i]] (default: a rotating
+        offset into the bank), reset frame into every frame-stack slot. One launch, no host sync.
+        mask = this env's own `term` tensor with no bank_idx is the canonical loop's
+        reset(reset_mask=terminated): served by reset_terminated()."""
+        if self.bank is None:
+            raise RuntimeError("no scene bank attached")
+        if mask is self.term and bank_idx is None and self._stepped:
+            return self.reset_terminated()
         N, B = self.num_envs, self.bank.shape[0]
         offset = 0
         if bank_idx is None:
@@ -445,6 +508,7 @@ class CarlaBEVVectorEnv:
         check(lib().cbev_step(self._ctx, _ptr(self.records), self.num_envs, _ptr(a), _ptr(frames), _ptr(self.reward),
                               _ptr(self.term), _ptr(self.trunc), _ptr(self.cause), _ptr(self.info), self._stream()),
               "cbev_step")
+        self._stepped = True
         if self.resize:
             self._resize_into_ring(None, all_slots=False)
         return a

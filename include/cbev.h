@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define CBEV_ABI_VERSION 2
+#define CBEV_ABI_VERSION 3
 
 typedef struct cbev_ctx cbev_ctx;
 
@@ -118,6 +118,20 @@ int cbev_bank_frames(cbev_ctx* ctx, const void* bank, int n_bank, uint8_t* frame
 int cbev_reset_frames(cbev_ctx* ctx, void* records, int n, const void* bank, int n_bank, const uint8_t* mask,
                       const int32_t* bank_idx, int bank_offset, const uint8_t* bank_frames, uint8_t* frames,
                       int n_frames, void* stream);
+
+/* The canonical loop's reset, `reset(options={"reset_mask": terminated})`
+ * (tools/debug_env.py:56-132 -> SyncVectorEnv.reset -> CarlaBEV.reset,
+ * carlabev.py:96-148), from a bank with cached reset frames: the same records and
+ * ring contents as cbev_reset_frames with mask = the terminations of the last
+ * cbev_step on this context (n must be that step's n), without scanning a mask:
+ * k_ego lists the envs that terminate. Bank rows are taken in order from a
+ * device cursor: the k-th terminated env in env-id order gets
+ * bank[(cursor + k) % n_bank], and the cursor moves past them when the next
+ * cbev_step starts, so consecutive resets walk the whole bank. One launch. */
+int cbev_reset_terminated(cbev_ctx* ctx, void* records, int n, const void* bank, int n_bank,
+                          const uint8_t* bank_frames, uint8_t* frames, int n_frames, void* stream);
+/* Bank rows the terminated-env resets have taken since cbev_create (synchronises). */
+int cbev_bank_cursor(cbev_ctx* ctx, int64_t* cursor);
 
 /* Wrapper stack on the device (wrap_env, envs/__init__.py:62-83). `ring` holds
  * n_frames frames per env (uint8[n_frames][n][h][w], slot `head` the newest;

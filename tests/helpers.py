@@ -11,6 +11,13 @@ from carlabev_env_amd.scene_gen import SceneGenerator
 
 CAPS_FULL = LY.Caps(128, 32, 64, 4)
 
+
+def bench_caps(config: int) -> LY.Caps:
+    """The record capacities bench.py measures configuration `config` with
+    (imported from bench.CONFIGS, not copied)."""
+    import bench
+    return LY.Caps(**bench.CONFIGS[config]["caps"])
+
 _GEN = {}
 
 

@@ -22,7 +22,7 @@ def test_library_loads_and_exports_every_symbol():
     L = _lib.lib()
     for name in _lib.EXPORTED_SYMBOLS:
         assert hasattr(L, name), name
-    assert L.cbev_abi_version() == 2
+    assert L.cbev_abi_version() == 3
     assert L.cbev_params_size() == ctypes.sizeof(CbevParams)
 
 
@@ -141,3 +141,16 @@ def test_oracle_raster_matches_numpy_restatement_mid_episode():
 def test_shaping_reward_rollout_terminates_with_reference_causes():
     recs, frames, causes, layout = _rollout(["rt_easy_v1"], n_envs=3, steps=60, reward="shaping_base_v1")
     assert set(causes) <= {0, 1, 2, 3, 4, 5, 6, 7}
+
+
+def test_create_refuses_records_k_ego_cannot_stage():
+    """k_ego stages at least 4 records per workgroup (its shuffle reductions stay
+    inside a wave): capacities whose staged ranges exceed the LDS budget at 4 envs
+    are refused at cbev_create (no GPU work: the check precedes any launch)."""
+    import ctypes
+    from carlabev_env_amd import layout as LY
+    _, P, _, _, _ = world()
+    L = _lib.lib()
+    ctx = ctypes.c_void_p()
+    rc = L.cbev_create(ctypes.byref(P), ctypes.byref(LY.Caps(4096, 0, 2, 0).c()), 0, ctypes.byref(ctx))
+    assert rc == -1 and b"k_ego" in L.cbev_last_error()

@@ -21,7 +21,7 @@ from carlabev_env_amd import layout as LY
 from carlabev_env_amd._lib import check, lib
 from carlabev_env_amd.semantics import gray_lut, rgb_lut, semantic_lut, rgb_to_semantic_mask_ids, PALETTE
 from carlabev_env_amd.config import RandomNavigationReset, build_random_navigation_options
-from helpers import CAPS_FULL, action_stream, build_records, world
+from helpers import CAPS_FULL, action_stream, bench_caps, build_records, world
 
 pytestmark = pytest.mark.gpu
 
@@ -220,10 +220,12 @@ def test_parity_edge_states_shaping_and_truncation():
     run_parity(["rt_easy_v1"], 10, 4, reward="shaping_base_v1", seed0=4242, edit=edit)
 
 
-@pytest.mark.parametrize("ne", ["1", "4", "64"])
+@pytest.mark.parametrize("ne", ["2", "8", "64"])
 def test_parity_ego_workgroup_shapes(ne, monkeypatch):
-    """k_ego with 1, 4 and the most envs per workgroup the LDS admits (CBEV_EGO_NE,
-    read at cbev_create); odd env counts leave a partial last workgroup."""
+    """k_ego with 4 (CBEV_EGO_NE=2 is raised to the floor of 4 envs, whose 64
+    threads per env stay inside one wave for the shuffle reductions), 8 and the
+    most envs per workgroup the LDS admits (read at cbev_create); odd env counts
+    leave a partial last workgroup."""
     monkeypatch.setenv("CBEV_EGO_NE", ne)
     run_parity(["rt_no_traffic_v1"], 47, 30, seed0=10_000)
     run_parity(["rt_hard_v1"], 31, 30, seed0=20_000, act_seed=7)
@@ -410,15 +412,19 @@ def _sample_envs(n, k=160):
     return np.array(sorted(ids))
 
 
-def run_full_size(kinds, n_envs, size=128, profile="discrete9_v1", seed0=0, steps=16, distinct=160, act_seed=1):
+def run_full_size(kinds, n_envs, size=128, profile="discrete9_v1", seed0=0, steps=16, distinct=160, act_seed=1,
+                  caps=CAPS_FULL):
     """The HIP path at a benchmarked batch size (grid shapes, XCD placement and
     staging batches of the bench) against the oracle on a sampled subset of envs.
     `distinct` seeded scenes are tiled over the batch (env e gets scene e % distinct);
-    every env gets its own action stream, so tiled copies diverge."""
-    cfg, P, padded, layout, builder = world(size, profile, "carl_base_v1", 0.5)
+    every env gets its own action stream, so tiled copies diverge. `caps` are the
+    record capacities: bench.CONFIGS' for the bench configurations, so the kernel
+    shapes the bench line measures (k_actors skipped at actor_cap 0, the k_ego
+    workgroup size, the record layout) are the ones checked here."""
+    cfg, P, padded, layout, builder = world(size, profile, "carl_base_v1", 0.5, caps=caps)
     base, _ = build_records(builder, distinct, kinds, seed0=seed0)
     recs = base[np.arange(n_envs) % distinct].copy()
-    dw = DevWorld(P, padded, CAPS_FULL)
+    dw = DevWorld(P, padded, caps)
     L = lib()
     S = P.size
     rng = np.random.default_rng(act_seed)
@@ -432,7 +438,7 @@ def run_full_size(kinds, n_envs, size=128, profile="discrete9_v1", seed0=0, step
     d_recs = torch.from_numpy(recs).cuda()
     d_frames = torch.zeros((n_envs, S, S), dtype=torch.uint8, device="cuda")
     check(L.cbev_reset(dw.ctx, ptr(d_recs), n_envs, None, 0, None, None, 0, ptr(d_frames), 1, None), "reset")
-    orc = O.Oracle(P, padded, CAPS_FULL.c(), layout.record_bytes)
+    orc = O.Oracle(P, padded, caps.c(), layout.record_bytes)
     h_recs = recs[sample].copy()
     h_frames = np.zeros((len(sample), S, S), np.uint8)
     rew = torch.zeros(n_envs, dtype=torch.float64, device="cuda")
@@ -465,16 +471,98 @@ def run_full_size(kinds, n_envs, size=128, profile="discrete9_v1", seed0=0, step
 
 
 def test_full_size_config2():
-    assert run_full_size(["rt_no_traffic_v1"], 4096, seed0=10_000) >= 128
+    """Config 2 at its bench capacities (actor_cap 0: k_actors is not launched,
+    k_ego runs with empty actor groups and its 16-env workgroups)."""
+    assert run_full_size(["rt_no_traffic_v1"], 4096, seed0=10_000, caps=bench_caps(2)) >= 128
 
 
 def test_full_size_config3():
-    run_full_size(["rt_hard_v1"], 4096, seed0=20_000, act_seed=7)
+    run_full_size(["rt_hard_v1"], 4096, seed0=20_000, act_seed=7, caps=bench_caps(3))
 
 
 def test_full_size_config4_shard():
-    run_full_size(["rt_medium_v1"], 8192, profile="continuous_gsb_v1", seed0=40_000, act_seed=99)
+    run_full_size(["rt_medium_v1"], 8192, profile="continuous_gsb_v1", seed0=40_000, act_seed=99, caps=bench_caps(4))
 
 
 def test_full_size_config5():
-    run_full_size(["mix3"], 2048, size=256, seed0=30_000, steps=12)
+    run_full_size(["mix3"], 2048, size=256, seed0=30_000, steps=12, caps=bench_caps(5))
+
+
+def test_full_size_caps_full():
+    """The test capacities (CAPS_FULL: 32 actor slots, 8-env k_ego workgroups) at a
+    bench batch size, so both workgroup shapes run full-size."""
+    run_full_size(["rt_medium_v1"], 4096, seed0=40_000, act_seed=3, steps=10)
+
+
+@pytest.mark.parametrize("config", [2, 3, 4, 5])
+def test_parity_bench_caps_small(config):
+    """Every step of a small odd-sized batch at each bench configuration's record
+    capacities (bench.CONFIGS), compared whole against the oracle; the odd env
+    counts leave partial k_ego workgroups and k_actors / k_raster tails."""
+    caps = bench_caps(config)
+    if config == 2:
+        run_parity(["rt_no_traffic_v1"], 37, 150, seed0=10_000, caps=caps)
+        run_parity(["rt_no_traffic_v1"], 5, 60, seed0=10_500, act_seed=77, caps=caps)
+    elif config == 3:
+        run_parity(["rt_hard_v1"], 29, 100, seed0=20_000, act_seed=7, caps=caps)
+    elif config == 4:
+        run_parity(["rt_medium_v1"], 23, 100, profile="continuous_gsb_v1", seed0=40_000, act_seed=99, caps=caps)
+    else:
+        run_parity(["mix3"], 19, 80, size=256, seed0=30_000, caps=caps)
+
+
+def test_reset_terminated_matches_masked_reset():
+    """cbev_reset_terminated (the canonical loop's reset from k_ego's termination
+    list) = cbev_reset_frames with mask = that step's terminations and bank rows
+    handed out in env-id order from the cursor: the k-th terminated env gets
+    bank[(cursor + k) % B], and the cursor moves past them at the next step."""
+    cfg, P, padded, layout, builder = world(caps=bench_caps(3))
+    n, B, F = 45, 11, 4
+    recs, _ = build_records(builder, n, ["rt_hard_v1"], seed0=2100)
+    bank, _ = build_records(builder, B, ["rt_hard_v1", "rt_medium_v1"], seed0=2900)
+    dw = DevWorld(P, padded, bench_caps(3))
+    L = lib()
+    S = P.size
+    d_bank = torch.from_numpy(bank.copy()).cuda()
+    bf = torch.zeros((B, S, S), dtype=torch.uint8, device="cuda")
+    check(L.cbev_bank_frames(dw.ctx, ptr(d_bank), B, ptr(bf), None), "bank_frames")
+    d_recs = torch.from_numpy(recs.copy()).cuda()
+    ring = torch.zeros((F, n, S, S), dtype=torch.uint8, device="cuda")
+    check(L.cbev_reset(dw.ctx, ptr(d_recs), n, None, 0, None, None, 0, ptr(ring), F, None), "reset")
+    rew = torch.zeros(n, dtype=torch.float64, device="cuda")
+    term = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    trunc = torch.zeros_like(term)
+    cause = torch.zeros(n, dtype=torch.int32, device="cuda")
+    acts = action_stream(P, n, 12, seed=7)
+    cursor = 0
+    rng = np.random.default_rng(5)
+    total = 0
+    for t in range(12):
+        # push a random subset off the road so every round terminates some envs
+        h = d_recs.cpu().numpy()
+        for e in rng.choice(n, size=int(rng.integers(0, 9)), replace=False):
+            LY.RecordView(h[e], layout).hd[LY.HD["X"]] += 60.0
+        d_recs.copy_(torch.from_numpy(h))
+        a = torch.from_numpy(np.ascontiguousarray(acts[t])).cuda()
+        check(L.cbev_step(dw.ctx, ptr(d_recs), n, ptr(a), ptr(ring[t % F]), ptr(rew), ptr(term), ptr(trunc),
+                          ptr(cause), None, None), "step")
+        torch.cuda.synchronize()
+        m = term.cpu().numpy().astype(bool)
+        ids = np.flatnonzero(m)
+        total += len(ids)
+        bidx = np.zeros(n, np.int32)
+        bidx[ids] = (cursor + np.arange(len(ids))) % B
+        want_r, want_f = d_recs.clone(), ring.clone()
+        check(L.cbev_reset_frames(dw.ctx, ptr(want_r), n, ptr(d_bank), B, ptr(term), ptr(torch.from_numpy(bidx).cuda()),
+                                  0, ptr(bf), ptr(want_f), F, None), "reset_frames")
+        check(L.cbev_reset_terminated(dw.ctx, ptr(d_recs), n, ptr(d_bank), B, ptr(bf), ptr(ring), F, None), "reset_term")
+        torch.cuda.synchronize()
+        assert torch.equal(d_recs, want_r), t
+        assert torch.equal(ring, want_f), t
+        cursor += len(ids)
+        c = ctypes.c_int64()
+        check(L.cbev_bank_cursor(dw.ctx, ctypes.byref(c)), "cursor")
+        assert c.value == cursor, (t, c.value, cursor)
+    assert total > 20
+    # n must match the last step's
+    assert L.cbev_reset_terminated(dw.ctx, ptr(d_recs), n - 1, ptr(d_bank), B, ptr(bf), ptr(ring), F, None) != 0
