@@ -346,6 +346,8 @@ def main():
     ap.add_argument("--scene-cache", default=None, help="directory to keep built scenes in across runs (one box)")
     ap.add_argument("--fresh-workers", type=int, default=4,
                     help="host processes feeding fresh seeded scenes into the reset bank in a last timed pass (0: off)")
+    ap.add_argument("--burn-in", type=int, default=200,
+                    help="canonical-loop steps before the timed passes, which all start from the state they leave")
     ap.add_argument("--repeats", type=int, default=5,
                     help="timed passes of exactly --steps steps each (re-seeded between); value = their median")
     ap.add_argument("--info-mode", default="none", choices=("none", "full"),
@@ -378,12 +380,15 @@ def main():
     env, host_recs = build_env(cfgd, n, rank, device, args.info_mode, args.scene_cache)
     P = env.params
     total_steps = args.warmup + args.steps
-    acts = torch.from_numpy(make_actions(P, n, total_steps, cfgd["act_seed"], rank * n)).to(device)
+    burn = max(0, args.burn_in)
+    # one action stream per env: the burn-in's steps, then the warmup + timed steps of every pass
+    acts_all = torch.from_numpy(make_actions(P, n, burn + total_steps, cfgd["act_seed"], rank * n)).to(device)
+    acts = acts_all[burn:]
     gather = cfgd.get("gather", False) and world > 1
     gatherer = None
     if gather:
         from carlabev_env_amd.sharding import FrameGather
-        gatherer = FrameGather(n, cfgd["size"], device, dst=0)
+        gatherer = FrameGather(n, cfgd["size"], device, dst=0, ctx=env._ctx, stream_fn=env._stream)
 
     env.auto_obs = False
 
@@ -408,6 +413,8 @@ def main():
         for t in range(args.warmup, total_steps):
             one_step(t, wire)
         host_enqueue = time.perf_counter() - t0
+        if gatherer is not None:
+            gatherer.wait()  # the last steps' gathers are part of the timed region
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
@@ -426,9 +433,31 @@ def main():
         return el, ms3, host_enqueue
 
     start_idx = torch.arange(n, dtype=torch.int32, device=device)
+    snap = {}
 
-    def reseed():  # back to the seeded start scenes (bank rows 0..n-1), so every pass replays a comparable workload
+    def reseed():  # back to the steady-state snapshot, so every pass replays a comparable workload
+        if not snap:  # before the burn-in: the seeded start scenes (bank rows 0..n-1)
+            env.reset_from_bank(mask=None, bank_idx=start_idx)
+            return
+        env.records.copy_(snap["records"])
+        env.ring.copy_(snap["ring"])
+        env.head = snap["head"]
+
+    def burn_in():
+        """The canonical loop from the seeded start scenes for `burn` steps, then a
+        snapshot of every env's state and frame stack: the timed passes start from
+        episodes of mixed ages (the steady-state termination and reset rate of the
+        loop) instead of all envs at step 0 of their first episode."""
         env.reset_from_bank(mask=None, bank_idx=start_idx)
+        term0 = env.termination_count()
+        for t in range(burn):
+            env.step_async_only(acts_all[t])
+            env.reset_from_bank(mask=env.term)
+        torch.cuda.synchronize()
+        snap["records"] = env.records.clone()
+        snap["ring"] = env.ring.clone()
+        snap["head"] = env.head
+        return env.termination_count() - term0
 
     # The step runs on a stream of its own: launches on HIP's legacy default
     # stream carry implicit synchronisation that costs several us per kernel.
@@ -441,12 +470,13 @@ def main():
             for t in range(min(20, total_steps)):
                 one_step(t, False)
             torch.cuda.synchronize()
+        burn_resets = burn_in() if burn else 0
         passes = []
-        rows0 = env.bank_rows_used()
+        term0 = env.termination_count()
         for _ in range(max(1, args.repeats)):  # headline passes, no instrumentation
             reseed()
             passes.append(timed(False, False))
-        rows_used = env.bank_rows_used() - rows0
+        pass_resets = env.termination_count() - term0
         els = sorted(p[0] for p in passes)
         el = els[len(els) // 2]
         host_enq = sorted(p[2] for p in passes)[len(els) // 2]
@@ -510,8 +540,12 @@ def main():
             "repeats": len(els),
             "ms_per_step_min_max": [round(els[0] / args.steps * 1e3, 4), round(els[-1] / args.steps * 1e3, 4)],
             "value_min_max": [round(world * n * args.steps / els[-1], 1), round(world * n * args.steps / els[0], 1)],
+            "burn_in_steps": burn,
+            "resets_per_step": round(pass_resets / (max(1, args.repeats) * total_steps), 2),
+            "resets_per_step_note": (f"canonical-loop resets (reset_mask=terminated) per step over the headline "
+                                     f"passes (warmup + timed steps), from a snapshot taken after {burn} burn-in "
+                                     f"steps ({burn_resets} resets)"),
             "bank_scenes": int(env.bank.shape[0]),
-            "bank_resets_in_headline_passes": rows_used,
             # resets take bank rows in order (cursor), so any run of up to B consecutive resets is all distinct
             "distinct_scenes_per_1k_resets": min(1000, int(env.bank.shape[0])),
             "host_enqueue_ms_per_step": round(host_enq / args.steps * 1e3, 4),

@@ -58,6 +58,10 @@ def lib():
     L.cbev_bank_cursor.restype = _I
     L.cbev_expand_obs.argtypes = [_P, _P, _I, _I, _I, _I, _I, _P, _P, _P]
     L.cbev_expand_obs.restype = _I
+    L.cbev_pack_frames.argtypes = [_P, _P, _I, _P, _P]
+    L.cbev_pack_frames.restype = _I
+    L.cbev_unpack_frames.argtypes = [_P, _P, _I, _P, _P]
+    L.cbev_unpack_frames.restype = _I
     L.cbev_vector_obs.argtypes = [_P, _P, _I, _P, _P]
     L.cbev_vector_obs.restype = _I
     L.cbev_set_fov_mask.argtypes = [_P, _P]
@@ -97,6 +101,6 @@ EXPORTED_SYMBOLS = ("cbev_abi_version", "cbev_params_size", "cbev_layout_of", "c
                     "cbev_reset_frames", "cbev_reset_terminated", "cbev_bank_cursor",
                     "cbev_expand_obs", "cbev_vector_obs", "cbev_set_fov_mask", "cbev_set_obs_size", "cbev_resize_obs", "cbev_profile", "cbev_profile_read",
                     "cbev_profile_raster", "cbev_error_flags", "cbev_set_episode_stats", "cbev_episode_slot",
-                    "cbev_wall_clock_hz", "cbev_termination_count")
+                    "cbev_wall_clock_hz", "cbev_termination_count", "cbev_pack_frames", "cbev_unpack_frames")
 
 ERR_ACTION_INDEX = 1  # CBEV_ERR_ACTION_INDEX (include/cbev.h)

@@ -376,7 +376,9 @@ __device__ __noinline__ void wave_start_retreat(uint8_t* base, int o_ad, int o_a
   const int m = nd;
   const double x0 = lane_value(cxv, 0), y0 = lane_value(cyv, 0);
   const double yaw_old = RAD(r, CBEV_AD_YAW, a);
-  const double fx = x0 + CB_WHEELBASE * cos(yaw_old), fy = y0 + CB_WHEELBASE * sin(yaw_old);
+  double syo, cyo;
+  d_sincos(yaw_old, &syo, &cyo);
+  const double fx = x0 + CB_WHEELBASE * cyo, fy = y0 + CB_WHEELBASE * syo;
   const double dxl = fx - cxv, dyl = fy - cyv;
   const double d2 = lane < m ? dxl * dxl + dyl * dyl : INFINITY;
   const double lim = group_min<64>(d2) * (1.0 + 1e-14);
@@ -522,22 +524,38 @@ __device__ __forceinline__ void d_crop_origin(const cbev_params& P, double x, do
 // rect_from_world_center (transforms.py:46-51): centre rounded half-even, x = c - w/2
 __device__ __forceinline__ int d_rect_lo(double w, int pad, int size) { return (int)rint((double)pad + w * 1.0) - size / 2; }
 
-// LDS image of the crop window, nibble-packed like the map: crop row r starts
-// at dword r * sd and holds the packed map bytes from xa = (xmin >> 1) & ~3 on
-// (dword-aligned), so crop pixel (c, r) is texel shift + c of the row (shift =
-// xmin - 2 xa, 0..7), i.e. "nibble address" r * 8 sd + shift + c: byte >> 1 of
-// it, high nibble when odd. sd = the dwords a row needs (7 + C nibbles),
-// rounded up to odd so that successive crop rows start in different LDS banks
-// and gathers along a rotated row spread over the banks at every angle:
-// 182 x 25 dwords = 18.2 KB at S=128. (A byte-per-texel image halves the
-// gather VALU but at S=128 doubles the image, and measured slower: 37 vs 30 us
-// per raster launch at 4096 envs.)
-__host__ __device__ __forceinline__ int raster_stride_dwords(int S, int C) { return ((C + 7 + 7) / 8) | 1; }
+// LDS images of the crop. Two:
+//  * nibble image of the whole crop (every S; the only one at S = 256):
+//    nibble-packed like the map, crop row r starts at dword r * sd and holds the
+//    packed map bytes from xa = (xmin >> 1) & ~3 on, so crop pixel (c, r) is
+//    "nibble address" r * 8 sd + shift + c (shift = xmin - 2 xa, 0..7): byte >> 1
+//    of it, high nibble when odd; sd = the dwords a row needs (7 + C nibbles),
+//    rounded up to odd. 363 x 47 dwords = 68 KB at S=256, 182 x 25 = 18 KB at
+//    S=128; 7.5 VALU instructions per output pixel (address, nibble select).
+//  * byte window (S <= 128, raster8_* below): one palette id per byte, only the
+//    texels the output samples; 3.75 VALU instructions per pixel.
+// The raster is VALU-issue-bound (round 3 PMC: SQ_INSTS_VALU x 4 cycles ~ the
+// launch on every SIMD), hence the byte window wherever it fits.
+// the byte-window path (below, raster8_*) serves S <= 128
+__host__ __device__ constexpr bool raster_win8(int S) {
+#ifdef CBEV_RASTER_NIBBLE
+  return false;
+#else
+  return S <= 128;
+#endif
+}
+__host__ __device__ __forceinline__ int raster_stride_dwords(int S, int C) {
+  return ((C + 7 + 7) / 8) | 1;
+}
 // texels per LDS row (the row stride of texel addresses)
-__host__ __device__ __forceinline__ int raster_row_texels(int S, int C) { return 8 * raster_stride_dwords(S, C); }
-// 16-byte chunks of the packed map per staged row (32 texels each)
-__host__ __device__ __forceinline__ int raster_row_chunks(int S, int C) { return ((C + 7 + 7) / 8 + 3) / 4; }
-// 16 bytes at 4-byte alignment (crop rows start at a dword of the packed map)
+__host__ __device__ __forceinline__ int raster_row_texels(int S, int C) {
+  return 8 * raster_stride_dwords(S, C);
+}
+// 16-byte chunks of the (byte or packed) map per staged row: 16 or 32 texels each
+__host__ __device__ __forceinline__ int raster_row_chunks(int S, int C) {
+  return ((C + 7 + 7) / 8 + 3) / 4;
+}
+// 16 bytes at 4-byte alignment (crop rows start at a dword of the map)
 typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
 __device__ __forceinline__ uint4 load16_a4(const uint8_t* p) {
   const u32x4_a4 t = *(const u32x4_a4*)p;
@@ -553,7 +571,8 @@ __device__ __forceinline__ void lds_set_texel(uint8_t* lds, uint32_t ta, uint32_
   atomicAnd(w, ~(15u << sh));
   atomicOr(w, col << sh);
 }
-__host__ __device__ __forceinline__ int raster_image_bytes(int S, int C) { return C * raster_stride_dwords(S, C) * 4; }
+// + one spare dword after the image (the nibble staging's overhang writes land there)
+__host__ __device__ __forceinline__ int raster_image_bytes(int S, int C);
 
 // Per-env rotation parameters (pygame transform.rotate, 16.16 fixed point;
 // rotate90 for exact multiples of 90 degrees) and the compose placement.
@@ -572,7 +591,10 @@ static_assert(sizeof(cbev_episode_stats) == 1856, "cbev_episode_stats is part of
 __device__ __forceinline__ RotSetup rot_setup(const cbev_params& P, float angle, int sb) {
   RotSetup R;
   const int C = P.crop;
-  R.r90 = fmod((double)angle, (double)90.0f) == 0.0;
+  // fmod(angle, 90) == 0, exactly: a float angle is a multiple of 90 iff its
+  // double quotient by 90 is an integer (a non-multiple misses by >= 2^-24 relative)
+  const double q90 = (double)angle / 90.0;
+  R.r90 = q90 == rint(q90);
   R.nx = C;
   R.ny = C;
   R.isin = R.icos = R.dx00 = R.dy00 = 0;
@@ -591,7 +613,8 @@ __device__ __forceinline__ RotSetup rot_setup(const cbev_params& P, float angle,
     }
   } else {
     double rad = angle * .01745329251994329;
-    double sn = sin(rad), cs = cos(rad);
+    double sn, cs;
+    d_sincos(rad, &sn, &cs);
     double xw = C, yh = C;
     double cxw = cs * xw, cyh = cs * yh, sxw = sn * xw, syh = sn * yh;
     double m1 = fmax(fmax(fmax(fabs(cxw + syh), fabs(cxw - syh)), fabs(-cxw + syh)), fabs(-cxw - syh));
@@ -888,7 +911,11 @@ __device__ __forceinline__ void hero_env_comfort(DRec r) {
   const int has_prev = hi[CBEV_HI_HAS_PREV_COMFORT];
   const double speed_mps = v * CB_MPP, prev_speed_mps = v1 * CB_MPP;
   const double dyaw = yaw - yaw1;
-  const double yr_rad = atan2(sin(dyaw), cos(dyaw)) / CB_DT;
+  // _angle_delta = atan2(sin(dyaw), cos(dyaw)) (comfort.py:13-14,32): dyaw wrapped
+  // into [-pi, pi] by one 2 pi step (yaw and yaw_1 are both angle_mod'ed), equal
+  // to the libm round trip within its last ulps (three transcendentals fewer on
+  // the chain; nothing bit-exact depends on the yaw rate)
+  const double yr_rad = (dyaw > CB_PI ? dyaw - 2.0 * CB_PI : (dyaw < -CB_PI ? dyaw + 2.0 * CB_PI : dyaw)) / CB_DT;
   const double yr_deg = d_degrees(yr_rad);
   const double al = (speed_mps - prev_speed_mps) / CB_DT;
   const double alat = speed_mps * yr_rad;
@@ -1083,8 +1110,10 @@ __global__ __launch_bounds__(256) void k_actors(KArgs K, uint8_t* __restrict__ r
         pcy[k] = r.acy[o];
         pyaw[k] = r.acyaw[o];
       }
-      fx = s[0] + CB_WHEELBASE * cos(s[2]);
-      fy = s[1] + CB_WHEELBASE * sin(s[2]);
+      double sy, cy_;
+      d_sincos(s[2], &sy, &cy_);
+      fx = s[0] + CB_WHEELBASE * cy_;
+      fy = s[1] + CB_WHEELBASE * sy;
     }
   }
   CBEV_STAMPW(6, 1);
@@ -1109,7 +1138,9 @@ __global__ __launch_bounds__(256) void k_actors(KArgs K, uint8_t* __restrict__ r
     const double* cy = r.acy + (int64_t)a * RA;
     const double* cyaw = r.acyaw + (int64_t)a * RA;
     const double yaw = s[2];
-    const double fa0 = -cos(yaw + CB_PI / 2.0), fa1 = -sin(yaw + CB_PI / 2.0);
+    double sp, cp;
+    d_sincos(yaw + CB_PI / 2.0, &sp, &cp);
+    const double fa0 = -cp, fa1 = -sp;
     const int db = best - tid0, cur = tid0 >= best ? tid0 : best;
     const double bx = db == 0 ? pcx[0] : db == 1 ? pcx[1] : cx[best];
     const double by = db == 0 ? pcy[0] : db == 1 ? pcy[1] : cy[best];
@@ -1179,8 +1210,7 @@ __device__ __forceinline__ void raster_out4(const cbev_params& P, const RotSetup
   int sy = R.dy00 + xx0 * R.isin + yy0 * R.icos;  // 16.16 source y (general)
   int sa = R.a00 + shift + xx0 * R.ustep + yy0 * R.vstep;  // LDS texel address (rotate90)
   // the crop's texel offset rides in the integer part of sx, so the LDS byte is
-  // (sy >> 16) * sb + (sx >> 16) (byte image) or (sy >> 16) * sb + (sx >> 17) with
-  // the nibble (sx >> 16) & 1 (nibble image)
+  // (sy >> 16) * sb + (sx >> 17) with the nibble (sx >> 16) & 1
   sx += shift << 16;
   const uint8_t* img = lds;
   const uint32_t sb = 4u * (uint32_t)raster_stride_dwords(S, C);  // LDS bytes per crop row
@@ -1411,7 +1441,7 @@ struct PaintPre {
   double ax, ay;  // actor tid >> 2
   int asz;
   double tx, ty;  // target tid >> 2
-  int tvis;
+  uint32_t tvis;  // its vis_draw word
 };
 
 __device__ __forceinline__ PaintPre raster_paint_fetch(const DRec& r) {
@@ -1430,7 +1460,7 @@ __device__ __forceinline__ PaintPre raster_paint_fetch(const DRec& r) {
     q.asz = RAI(r, CBEV_AI_SIZE, k);
   }
   if (k < q.nt) {
-    q.tvis = (r.vis_draw[k >> 5] >> (k & 31)) & 1u;
+    q.tvis = r.vis_draw[k >> 5];  // the word; its bit is taken at paint time (no wait on the load here)
     q.tx = r.cx[k];
     q.ty = r.cy[k];
   }
@@ -1439,10 +1469,9 @@ __device__ __forceinline__ PaintPre raster_paint_fetch(const DRec& r) {
 
 // one rect of side sz (rect_from_world_center, transforms.py:46-51) by the 4
 // threads of tid >> 2: thread tq covers rows tq, tq + 4, ..., each row's span
-// clipped to the crop and written a whole LDS dword (8 texels) at a time: one
-// and-mask + or-colour pair per dword it touches. Every rect of a paint pass has
-// the same colour, so overlapping rects commute; rows of an LDS image are
-// dword-aligned (rt is a multiple of 8).
+// clipped to the crop, written a whole LDS dword (8 texels) at a time, one and-mask + or-colour pair per dword
+// it touches. Every rect of a paint pass has the same colour, so overlapping
+// rects commute; rows of an LDS image are dword-aligned.
 __device__ __forceinline__ void paint_rect4(uint8_t* lds, int rt, int shift, int C, int pad, int xmin, int ymin,
                                             double wx, double wy, int sz, int tq, uint32_t col) {
   const int rx = d_rect_lo(wx, pad, sz) - xmin, ry = d_rect_lo(wy, pad, sz) - ymin;
@@ -1469,7 +1498,7 @@ __device__ __forceinline__ void lds_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
-template <int NT = 256>
+template <int G, int NT = 256>
 __device__ __forceinline__ void raster_paint(const KArgs& K, const DRec& r, const PaintPre& q, int xmin, int ymin,
                                              int shift, uint8_t* __restrict__ lds) {
   const cbev_params& P = K.P;
@@ -1490,7 +1519,7 @@ __device__ __forceinline__ void raster_paint(const KArgs& K, const DRec& r, cons
     }
     const int nt = q.nt;
     // checkpoints 2x2, goal 4x4 (scenes/utils.py:114-122)
-    if (k < nt && q.tvis)
+    if (k < nt && ((q.tvis >> (k & 31)) & 1u))
       paint_rect4(lds, rt, shift, C, P.pad, xmin, ymin, q.tx, q.ty, k < nt - 1 ? 2 : 4, tq, CBEV_PX_ROUTE);
     for (int i = NT / 4 + k; i < nt; i += NT / 4)
       if ((r.vis_draw[i >> 5] >> (i & 31)) & 1u)
@@ -1529,7 +1558,7 @@ __device__ __forceinline__ void raster_origin(const KArgs& K, const DRec& r, Ras
     J.xmin = r.hi[CBEV_HI_RS_XMIN];
     J.ymin = r.hi[CBEV_HI_RS_YMIN];
   }
-  J.xa = (J.xmin >> 1) & ~3;  // packed byte column (dword aligned)
+  J.xa = (J.xmin >> 1) & ~3;    // packed byte column (dword aligned)
   J.shift = J.xmin - 2 * J.xa;  // texel offset (0..7)
 }
 
@@ -1556,9 +1585,6 @@ __device__ __forceinline__ void raster_rot(const KArgs& K, const DRec& r, Raster
 // the whole crop's, so the gathers are unchanged. Roads are axis-aligned, so
 // most headings sample about a 130 x 130 box of the 182 x 182 crop (S=128).
 #define STAGE_U 5
-struct StageBuf {
-  uint4 v[STAGE_U];
-};
 struct StageWin {
   int y0, ny, c0, nc;  // crop rows [y0, y0 + ny), row chunks [c0, c0 + nc)
 };
@@ -1595,59 +1621,57 @@ __device__ __forceinline__ StageWin stage_window(const cbev_params& P, const Ras
   yh = min(yh, C - 1);
   w.y0 = yl;
   w.ny = yh - yl + 1;
-  w.c0 = (J.shift + xl) >> 5;
-  w.nc = ((J.shift + xh) >> 5) - w.c0 + 1;
+  const int cs = 5;  // 32 texels per 16-byte chunk
+  w.c0 = (J.shift + xl) >> cs;
+  w.nc = ((J.shift + xh) >> cs) - w.c0 + 1;
   return w;
 }
-template <int G, int NT = 256>
-__device__ __forceinline__ void stage_issue(const KArgs& K, const RasterJob& J, const StageWin& W, int q0,
-                                            StageBuf& b) {
-  const int total = W.ny * W.nc;
-  const uint8_t* gbase = K.map + (int64_t)(J.ymin + W.y0) * K.npitch + J.xa + 16 * W.c0;
-  const int dr = NT / W.nc, dj = NT - dr * W.nc;
-  const int q = q0 + (int)threadIdx.x;
-  int r = q / W.nc, c = q - r * W.nc;
-#pragma unroll
-  for (int u = 0; u < STAGE_U; ++u) {
-    if (q + NT * u < total) b.v[u] = load16_a4(gbase + (int64_t)r * K.npitch + 16 * c);
-    r += dr;
-    c += dj;
-    if (c >= W.nc) { c -= W.nc; ++r; }
-  }
-}
-template <int G, int NT = 256>
-__device__ __forceinline__ void stage_commit(const KArgs& K, const StageWin& W, int q0, const StageBuf& b,
-                                             uint8_t* __restrict__ lds) {
-  const int C = K.P.crop;
-  const int sd = raster_stride_dwords(64 * G, C);
-  const int total = W.ny * W.nc;
-  const int dr = NT / W.nc, dj = NT - dr * W.nc;
-  const int q = q0 + (int)threadIdx.x;
-  int row = q / W.nc, jj = q - row * W.nc;
-  uint32_t* l32 = (uint32_t*)lds + W.y0 * sd;
-#pragma unroll
-  for (int u = 0; u < STAGE_U; ++u) {
-    if (q + NT * u < total) {
-      const int j = W.c0 + jj;  // chunk of the row
-      uint32_t* d = l32 + row * sd + 4 * j;
-      d[0] = b.v[u].x;  // the last chunk of a row may overhang the stride
-      if (4 * j + 1 < sd) d[1] = b.v[u].y;
-      if (4 * j + 2 < sd) d[2] = b.v[u].z;
-      if (4 * j + 3 < sd) d[3] = b.v[u].w;
-    }
-    row += dr;
-    jj += dj;
-    if (jj >= W.nc) { jj -= W.nc; ++row; }
-  }
-}
+
+// All STAGE_U loads of a thread are issued back to back, then committed: no
+// branch around a load (a chunk index past the window is clamped to its last
+// chunk, which is then loaded and stored again with the same bytes) and no
+// branch around an LDS store (a row's last chunk overhanging the row stride is
+// redirected to a spare dword after the image). Branches around the loads made
+// the compiler wait for every outstanding load (vmcnt(0)) before each one, so
+// a thread's staging took STAGE_U + 1 dependent memory round trips.
 template <int G, int NT = 256>
 __device__ __forceinline__ void stage_all(const KArgs& K, const RasterJob& J, uint8_t* __restrict__ lds) {
   const StageWin W = stage_window<G>(K.P, J);
-  const int total = W.ny * W.nc;
+  const int C = K.P.crop;
+  const int sd = raster_stride_dwords(64 * G, C);
+  const int nc = W.nc, total = W.ny * nc;
+  const int rl = (total - 1) / nc, cl = (total - 1) - rl * nc;  // the window's last chunk
+  const int dr = NT / nc, dj = NT - dr * nc;
+  const uint8_t* gbase = K.map + (int64_t)(J.ymin + W.y0) * K.npitch + J.xa + 16 * W.c0;
+  uint32_t* l32 = (uint32_t*)lds + W.y0 * sd + 4 * W.c0;
+  uint32_t* spare = (uint32_t*)lds + C * sd;  // raster_image_bytes leaves one dword here
+  const int jlim = sd - 4 * W.c0;              // dwords of a row from the window's first chunk on
   for (int q0 = 0; q0 < total; q0 += NT * STAGE_U) {
-    StageBuf b;
-    stage_issue<G, NT>(K, J, W, q0, b);
-    stage_commit<G, NT>(K, W, q0, b, lds);
+    const int q = q0 + (int)threadIdx.x;
+    int r = q / nc, c = q - r * nc;
+    uint4 v[STAGE_U];
+    int off[STAGE_U], jj[STAGE_U];
+#pragma unroll
+    for (int u = 0; u < STAGE_U; ++u) {
+      const bool ok = q + NT * u < total;
+      const int rr = ok ? r : rl, cc = ok ? c : cl;
+      off[u] = rr * sd + 4 * cc;
+      jj[u] = 4 * cc;  // dword of the row, from the window's first chunk
+      v[u] = load16_a4(gbase + (int64_t)rr * K.npitch + 16 * cc);
+      r += dr;
+      c += dj;
+      if (c >= nc) {
+        c -= nc;
+        ++r;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < STAGE_U; ++u) {
+      l32[off[u]] = v[u].x;
+      *(jj[u] + 1 < jlim ? l32 + off[u] + 1 : spare) = v[u].y;
+      *(jj[u] + 2 < jlim ? l32 + off[u] + 2 : spare) = v[u].z;
+      *(jj[u] + 3 < jlim ? l32 + off[u] + 3 : spare) = v[u].w;
+    }
   }
 }
 
@@ -1662,6 +1686,316 @@ __device__ __forceinline__ void raster_emit(const KArgs& K, const RasterJob& J, 
   raster_out_dispatch<G, NT / 64>(K.P, J.R, J.fast, lds, J.shift, bg, out, nout, out_stride, lane, wave, K.fov);
 }
 
+// ====================================================== byte-image raster (S <= 128)
+__host__ __device__ constexpr int r8_alloc(int S);
+// the raster's dynamic LDS: the byte image's window allocation, or the whole
+// nibble crop + one spare dword (the nibble staging's overhang writes land there)
+__host__ __device__ __forceinline__ int raster_image_bytes(int S, int C) {
+  const int nib = C * raster_stride_dwords(S, C) * 4 + 16;
+  return raster_win8(S) && r8_alloc(S) > nib ? r8_alloc(S) : nib;
+}
+// The byte window holds only the texels of the crop that the output samples
+// (the output -> crop map is affine: the bounding box of the four corners'
+// samples): crop rows [y0, y0 + ny) and the 16-byte chunks [c0, c0 + nc) of the
+// byte map's row from xa = xmin & ~3, one palette id per byte, rows
+// sb = 16 nc + 4 bytes apart (an odd number of dwords). Crop texel (x, y) is LDS
+// byte (y - y0) * sb + ox + x with ox = shift - 16 c0. The allocation is R8_LDS
+// bytes: at S=128 a heading up to about 10 degrees off an axis (roads are
+// axis-aligned) samples <= 24 KB; steeper headings take the nibble image.
+// Measured at config 2 (raster us / launch): nibble only 26.0; windows of 20 KB
+// 25.4, 22 KB 24.6, 24 KB 22.4, 28 KB 22.4, 32 KB 23.7, 36 KB (every heading)
+// 23.2; output bands for windows that do not fit: 60 (the band loop's registers
+// spilled under the 64-VGPR launch bound).
+// A gather is one byte read whose address is two SDWA instructions of the 16.16
+// coordinates; with the coordinate step and the packing, 3.75 VALU instructions
+// per pixel.
+#ifndef CBEV_R8_LDS
+#define CBEV_R8_LDS 24576
+#endif
+__host__ __device__ constexpr int r8_alloc(int S) { return S >= 128 ? CBEV_R8_LDS : 12288; }
+
+struct Win8 {
+  int y0, ny;  // crop rows [y0, y0 + ny)
+  int c0, nc;  // 16-byte chunks of the byte-map row from xa
+  int sb;      // LDS bytes per image row
+  int ox;      // LDS column of crop column 0
+};
+
+// The crop texels output rows [ra, rb) sample: the bounding box of the four
+// corners' source texels (pygame's rotozoom is affine in the output pixel),
+// clamped to the crop (samples outside it are background, no texel needed).
+template <int G>
+__device__ __forceinline__ Win8 win8(const cbev_params& P, const RasterJob& J, int ra, int rb) {
+  constexpr int S = 64 * G;
+  const int C = P.crop;
+  const RotSetup& R = J.R;  // affine form (raster8_affine)
+  int xl = 1 << 30, xh = -(1 << 30), yl = 1 << 30, yh = -(1 << 30);
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const int xx = ((c & 1) ? S - 1 : 0) - R.rx0, yy = ((c & 2) ? rb - 1 : ra) - R.ry0;
+    const int tx = (R.dx00 + xx * R.icos - yy * R.isin) >> 16;
+    const int ty = (R.dy00 + xx * R.isin + yy * R.icos) >> 16;
+    xl = min(xl, tx);
+    xh = max(xh, tx);
+    yl = min(yl, ty);
+    yh = max(yh, ty);
+  }
+  xl = min(max(xl, 0), C - 1);
+  yl = min(max(yl, 0), C - 1);
+  xh = max(min(xh, C - 1), xl);
+  yh = max(min(yh, C - 1), yl);
+  Win8 W;
+  W.y0 = yl;
+  W.ny = yh - yl + 1;
+  W.c0 = (J.shift + xl) >> 4;
+  W.nc = ((J.shift + xh) >> 4) - W.c0 + 1;
+  W.sb = 16 * W.nc + 4;
+  W.ox = J.shift - 16 * W.c0;
+  return W;
+}
+
+// Staging: the window's nc chunks of a row are taken by nc consecutive threads,
+// 256 / nc rows per pass; a thread's rows of all passes are loaded back to back
+// (straight-line code: no branch around a load; rows past the window are its
+// last row again, stored again with the same bytes), then stored.
+template <int U>
+__device__ __forceinline__ void stage8_group(const uint8_t* __restrict__ g, int p8, uint8_t* __restrict__ l, int sb,
+                                             int row, int dr, int last) {
+  uint4 v[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) v[u] = load16_a4(g + (int64_t)min(row + u * dr, last) * p8);
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    uint32_t* d = (uint32_t*)(l + min(row + u * dr, last) * sb);
+    d[0] = v[u].x;
+    d[1] = v[u].y;
+    d[2] = v[u].z;
+    d[3] = v[u].w;
+  }
+}
+__device__ __forceinline__ void stage8(const KArgs& K, const RasterJob& J, const Win8& W, uint8_t* __restrict__ lds) {
+  const int nc = W.nc, dr = 256 / nc;
+  const int t = (int)threadIdx.x;
+  int row = t / nc;
+  const int c = t - row * nc;
+  row = row < dr ? row : dr - 1;  // the 256 % nc leftover threads repeat chunks of the pass's last row
+  const int passes = (W.ny + dr - 1) / dr;
+  const uint8_t* g = K.map8 + (int64_t)(J.ymin + W.y0) * K.p8 + J.xa + 16 * (W.c0 + c);
+  uint8_t* l = lds + 16 * c;
+  // a window of <= R8_LDS bytes takes <= 6 passes at S = 128 (ny <= R8_LDS / (16 nc + 4), 256 / nc rows a pass)
+  if (passes <= 3) {
+    stage8_group<3>(g, K.p8, l, W.sb, row, dr, W.ny - 1);
+  } else {
+    for (int p0 = 0; p0 < passes; p0 += 6) stage8_group<6>(g, K.p8, l, W.sb, row + p0 * dr, dr, W.ny - 1);
+  }
+}
+
+// one rect (rect_from_world_center, transforms.py:46-51) by the 4 threads of
+// tid >> 2, clipped to the crop and the window: byte stores (rects of a pass
+// share their colour, so overlaps commute)
+__device__ __forceinline__ void paint8_rect(uint8_t* lds, const Win8& W, int C, int pad, int xmin, int ymin, double wx,
+                                            double wy, int sz, int tq, uint32_t col) {
+  const int rx = d_rect_lo(wx, pad, sz) - xmin, ry = d_rect_lo(wy, pad, sz) - ymin;
+  // crop columns the window holds: [-ox, -ox + 16 nc)
+  const int x0 = max(max(rx, 0), -W.ox), x1 = min(min(rx + sz, C), -W.ox + 16 * W.nc);
+  if (x0 >= x1) return;
+  for (int qy = tq; qy < sz; qy += 4) {
+    const int py = ry + qy - W.y0;
+    if (py < 0 || py >= W.ny || ry + qy >= C) continue;
+    uint8_t* rowp = lds + py * W.sb + W.ox;
+    for (int x = x0; x < x1; ++x) rowp[x] = (uint8_t)col;
+  }
+}
+
+// Actors, the targets visible before this step's collisions and traffic lights
+// into the window in the reference's draw order (scene.py:93-95,
+// actor_manager.py:121-132): vehicles, pedestrians, targets, traffic lights.
+__device__ __forceinline__ void paint8(const KArgs& K, const DRec& r, const PaintPre& q, const RasterJob& J,
+                                       const Win8& W, uint8_t* __restrict__ lds) {
+  constexpr int NT = 256;
+  const cbev_params& P = K.P;
+  const int C = P.crop;
+  const int k = threadIdx.x >> 2, tq = threadIdx.x & 3;
+  for (int pass = 0; pass < 2; ++pass) {  // vehicles, then pedestrians
+    const int a0 = pass == 0 ? 0 : q.nveh, a1 = pass == 0 ? q.nveh : q.nact;
+    if (a1 <= a0) continue;
+    const uint32_t col = pass == 0 ? CBEV_PX_VEHICLE : CBEV_PX_PEDESTRIAN;
+    if (k >= a0 && k < a1) paint8_rect(lds, W, C, P.pad, J.xmin, J.ymin, q.ax, q.ay, q.asz, tq, col);
+    for (int a = NT / 4 + k; a < a1; a += NT / 4)  // more than NT / 4 actors: fetched here
+      if (a >= a0)
+        paint8_rect(lds, W, C, P.pad, J.xmin, J.ymin, RAD(r, CBEV_AD_X, a), RAD(r, CBEV_AD_Y, a),
+                    RAI(r, CBEV_AI_SIZE, a), tq, col);
+    lds_barrier();
+  }
+  const int nt = q.nt;
+  // checkpoints 2x2, goal 4x4 (scenes/utils.py:114-122)
+  if (k < nt && ((q.tvis >> (k & 31)) & 1u))
+    paint8_rect(lds, W, C, P.pad, J.xmin, J.ymin, q.tx, q.ty, k < nt - 1 ? 2 : 4, tq, CBEV_PX_ROUTE);
+  for (int i = NT / 4 + k; i < nt; i += NT / 4)
+    if ((r.vis_draw[i >> 5] >> (i & 31)) & 1u)
+      paint8_rect(lds, W, C, P.pad, J.xmin, J.ymin, r.cx[i], r.cy[i], i < nt - 1 ? 2 : 4, tq, CBEV_PX_ROUTE);
+  lds_barrier();
+  const int wx0 = -W.ox, wx1 = -W.ox + 16 * W.nc;  // crop columns the window holds
+  for (int t = 0; t < q.ntl; ++t) {  // traffic lights one at a time (colours may differ)
+    const int rx = r.ti[CBEV_TI_RX * r.T + t] - J.xmin, ry = r.ti[CBEV_TI_RY * r.T + t] - J.ymin;
+    const int rw = r.ti[CBEV_TI_RW * r.T + t], rh = r.ti[CBEV_TI_RH * r.T + t];
+    const uint8_t col = (uint8_t)r.ti[CBEV_TI_COLOR * r.T + t];
+    for (int qy = threadIdx.x >> 4; qy < rh; qy += NT / 16)
+      for (int qx = threadIdx.x & 15; qx < rw; qx += 16) {
+        const int px = rx + qx, py = ry + qy;
+        if (px >= 0 && py >= 0 && px < C && py < C && px >= wx0 && px < wx1 && py >= W.y0 && py < W.y0 + W.ny)
+          lds[(py - W.y0) * W.sb + W.ox + px] = col;
+      }
+    lds_barrier();
+  }
+}
+
+// pygame rotate's background: the crop's top-left pixel after painting
+// (fov.py:84-88), which a window need not hold: the map texel there, then the
+// last pass in draw order with a rect over it.
+// (dy >> 16) * sb + (dx >> 16): v_mul_u32_u24 and v_add_u32 with SDWA word selects
+__device__ __forceinline__ uint32_t crop_byte_addr(uint64_t q, uint32_t sb) {
+  uint32_t a;
+  asm("v_mul_u32_u24_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1\n\t"
+      "v_add_u32_sdwa %0, %0, %3 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1"
+      : "=&v"(a)
+      : "s"(sb), "v"((uint32_t)(q >> 32)), "v"((uint32_t)q));
+  return a;
+}
+// a byte of the LDS image at an absolute LDS address (the dynamic LDS starts at
+// 0: k_raster declares no static LDS). A C-level read adds the array's base, one
+// more VALU instruction per pixel; the compiler's wait-count insertion does not
+// see this read, so its users wait for it explicitly (s_waitcnt lgkmcnt(0)
+// naming the registers).
+__device__ __forceinline__ void lds_u8(uint32_t& d, uint32_t a) { asm volatile("ds_read_u8 %0, %1" : "=v"(d) : "v"(a)); }
+
+// Output rows of chunks [0, nch) (RPC rows each, dealt over the NW waves): lane
+// l of a chunk owns the 16 consecutive pixels of row r + l / LPR, columns
+// 16 (l % LPR) .. + 15, gathered one column step apart and written with one
+// 16-byte store. The rotated surface covers the whole output and every output
+// pixel samples inside the window (raster8_env's conditions): no per-pixel tests.
+template <int G, int NW>
+__device__ __forceinline__ void raster_out8(const cbev_params& P, const RotSetup& R, const Win8& W,
+                                            const uint8_t* __restrict__ lds, uint8_t* __restrict__ out, int nout,
+                                            int64_t out_stride, int lane, int wave,
+                                            const uint32_t* __restrict__ fov, int nch) {
+  constexpr int S = 64 * G;     // == P.size
+  constexpr int LPR = S / 16;   // lanes per output row
+  constexpr int RPC = 64 / LPR; // output rows per chunk
+  const int hero_w = P.hero_w;
+  const int hx0 = P.anchor_x - hero_w / 2, hy0 = P.anchor_y - hero_w / 2;
+  const int lrow = lane / LPR, lcol = 16 * (lane % LPR);
+  const int r0 = wave * RPC;
+  const int xx0 = lcol - R.rx0, yy0 = r0 + lrow - R.ry0;
+  // window coordinates (crop coordinates moved by (ox, -y0)) in 16.16, packed in
+  // one 64-bit value so one 64-bit add steps both (the low word stays in
+  // [0, 2^32): no carry crosses over)
+  const int sx = R.dx00 + xx0 * R.icos - yy0 * R.isin + (W.ox << 16);
+  const int sy = R.dy00 + xx0 * R.isin + yy0 * R.icos - (W.y0 << 16);
+  const uint32_t sb = (uint32_t)W.sb;
+  const int chunk_rows = NW * RPC;
+  uint64_t pxy = ((uint64_t)(uint32_t)sy << 32) | (uint32_t)sx;
+  // one output row down: (dx, dy) += (-isin, icos); one column right: += (icos, isin)
+  const uint64_t chunk_step =
+      (uint64_t)(((int64_t)(chunk_rows * R.icos) << 32) + (int64_t)(-chunk_rows * R.isin));
+  const uint64_t col_step = (uint64_t)(((int64_t)R.isin << 32) + (int64_t)R.icos);
+  for (int ch = wave, r = r0; ch < nch; ch += NW, r += chunk_rows) {
+    const int row = r + lrow;
+    const uint32_t vo = (uint32_t)(row * S + lcol);
+    asm volatile("" : "+v"(pxy));
+    uint32_t w[4];
+    uint64_t q = pxy;
+    uint32_t px[16];
+#pragma unroll
+    for (int b = 0; b < 16; ++b) {
+      lds_u8(px[b], crop_byte_addr(q, sb));
+      q += col_step;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)"
+                 : "+v"(px[0]), "+v"(px[1]), "+v"(px[2]), "+v"(px[3]), "+v"(px[4]), "+v"(px[5]), "+v"(px[6]),
+                   "+v"(px[7]), "+v"(px[8]), "+v"(px[9]), "+v"(px[10]), "+v"(px[11]), "+v"(px[12]), "+v"(px[13]),
+                   "+v"(px[14]), "+v"(px[15])
+                 :
+                 : "memory");
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {  // three v_lshl_or_b32 / v_perm_b32 per dword (ids < 16: no masking)
+      const uint32_t x = px[4 * d] | (px[4 * d + 1] << 8), y = px[4 * d + 2] | (px[4 * d + 3] << 8);
+      w[d] = __builtin_amdgcn_perm(y, x, 0x05040100u);
+    }
+    if (fov) {  // FovRenderer.apply_mask (fov.py:96-99): black corner triangles (uniform branch)
+      const uint4 fm = *(const uint4*)(fov + (vo >> 2));
+      w[0] = (w[0] & ~fm.x) | (fm.x & (CBEV_PX_BLACK * 0x01010101u));
+      w[1] = (w[1] & ~fm.y) | (fm.y & (CBEV_PX_BLACK * 0x01010101u));
+      w[2] = (w[2] & ~fm.z) | (fm.z & (CBEV_PX_BLACK * 0x01010101u));
+      w[3] = (w[3] & ~fm.w) | (fm.w & (CBEV_PX_BLACK * 0x01010101u));
+    }
+    // Hero.draw (hero.py:26-32): the black w x w rect at the anchor; its byte
+    // mask is built only in the chunks that meet the hero rows (no registers held)
+    if ((unsigned)(r + RPC - 1 - hy0) < (unsigned)(RPC - 1 + hero_w) && (unsigned)(row - hy0) < (unsigned)hero_w) {
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        uint32_t m = 0;
+#pragma unroll
+        for (int bb = 0; bb < 4; ++bb) {
+          const int u = lcol + 4 * d + bb;
+          if (u >= hx0 && u < hx0 + hero_w) m |= 0xffu << (8 * bb);
+        }
+        w[d] = (w[d] & ~m) | (m & (CBEV_PX_BLACK * 0x01010101u));
+      }
+    }
+    const u32x4_nt v4 = {w[0], w[1], w[2], w[3]};
+    for (int k = 0; k < nout; ++k)  // streamed out: keep the L2 for the map and the records
+      __builtin_nontemporal_store(v4, (u32x4_nt*)(out + (int64_t)k * out_stride + vo));
+    pxy += chunk_step;
+  }
+}
+
+// rotate90 (exact multiples of 90 degrees: pygame's rotate90 transposes) as the
+// affine map it is: k_ego's texel steps (+-1 column or +-rt = a row, per output
+// column / row) become 16.16 steps of +-65536 with sin / cos in {0, +-1}, and the
+// start texel's coordinates sit at +0x8000, so every sample floors to the exact
+// texel and rotate90 takes the general gather (one output pass fewer to compile).
+__device__ __forceinline__ void raster8_affine(RotSetup& R, int rt) {
+  if (!R.r90) return;
+  const int ar = R.a00 / rt, ac = R.a00 - ar * rt;
+  // output column step = (icos, isin) in (column, row); the row step is (-isin, icos)
+  R.icos = R.ustep == 1 ? 65536 : R.ustep == -1 ? -65536 : 0;
+  R.isin = R.ustep == rt ? 65536 : R.ustep == -rt ? -65536 : 0;
+  R.dx00 = (ac << 16) + 0x8000;
+  R.dy00 = (ar << 16) + 0x8000;
+  R.r90 = 0;
+}
+
+// One env's observation by the byte window (whole 256-thread workgroup), when
+// the output samples only inside the crop (J.fast) and the window fits R8_LDS:
+// staged, painted (PAINT: the step's frame; the reset frame draws no actors)
+// and written. Otherwise (headings past about 10 degrees off the axes at S=128,
+// or output beyond the crop) returns false and the caller renders the nibble
+// image of the whole crop.
+template <int G, bool PAINT>
+__device__ __forceinline__ bool raster8_env(const KArgs& K, uint8_t* rec, const RasterJob& J0,
+                                            uint8_t* __restrict__ out, int nout, int64_t out_stride,
+                                            uint8_t* __restrict__ lds) {
+  constexpr int S = 64 * G, LPR = S / 16, RPC = 64 / LPR, NCH = S / RPC;
+  if (!J0.fast) return false;
+  RasterJob J = J0;
+  J.xa = J.xmin & ~3;  // byte-map column (dword aligned)
+  J.shift = J.xmin & 3;
+  raster8_affine(J.R, raster_row_texels(S, K.P.crop));
+  const Win8 W = win8<G>(K.P, J, 0, S);
+  if (W.ny * W.sb > r8_alloc(S)) return false;
+  const DRec r = bind_rec(rec, K.L, K.C);
+  PaintPre pq{};
+  if (PAINT) pq = raster_paint_fetch(r);  // in flight under the staging
+  stage8(K, J, W, lds);
+  __syncthreads();
+  if (PAINT) paint8(K, r, pq, J, W, lds);
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  raster_out8<G, 4>(K.P, J.R, W, lds, out, nout, out_stride, lane, wave, K.fov, NCH);
+  return true;
+}
+
 // BaseMap.reset's observation (theta = 0, nothing painted, world.py:92-100) of
 // one record by a 256-thread workgroup, into `nout` frames out + k*out_stride
 // (every slot of the frame-stack ring on reset).
@@ -1671,6 +2005,9 @@ __device__ __forceinline__ void raster_reset_env(const KArgs& K, const DRec& r, 
   RasterJob J;
   raster_origin<true, G>(K, r, J);
   raster_rot<true, G>(K, r, J);
+  if constexpr (raster_win8(64 * G)) {
+    if (raster8_env<G, false>(K, (uint8_t*)r.hd - K.L.hd, J, out, nout, out_stride, lds)) return;
+  }
   stage_all<G>(K, J, lds);
   __syncthreads();
   raster_emit<G>(K, J, out, nout, out_stride, lds);
@@ -1682,11 +2019,14 @@ __device__ __forceinline__ void raster_reset_env(const KArgs& K, const DRec& r, 
 // 4 waves below, where 8 workgroups share a CU. Measured alternatives (two envs
 // per workgroup with the next env's loads in flight, two crop images per
 // workgroup filled by LDS-DMA while the other is written out, a persistent
-// grid, a column-block lane mapping, a byte image at S=128) are in DESIGN.md §3.
+// grid, a column-block lane mapping, a byte image of the whole crop, output
+// bands for the byte window) are in DESIGN.md §3. The raster kernels declare no
+// static LDS: the byte window's gathers address the LDS absolutely (from 0).
 __host__ __device__ constexpr int raster_threads(int S) { return S >= 256 ? 512 : 256; }
 
 template <int G>
-__global__ __launch_bounds__(raster_threads(64 * G)) __attribute__((amdgpu_waves_per_eu(8))) void k_raster(
+__global__ __launch_bounds__(raster_threads(64 * G)) __attribute__((amdgpu_waves_per_eu(8)))
+void k_raster(
     KArgs K, uint8_t* __restrict__ recs, int n, uint8_t* __restrict__ frames) {
   extern __shared__ __align__(16) uint8_t lds[];
   constexpr int NT = raster_threads(64 * G);
@@ -1698,6 +2038,12 @@ __global__ __launch_bounds__(raster_threads(64 * G)) __attribute__((amdgpu_waves
   RasterJob J;
   raster_origin<false, G>(K, r, J);
   raster_rot<false, G>(K, r, J);
+  if constexpr (raster_win8(64 * G)) {
+    if (raster8_env<G, true>(K, recs + (int64_t)e * K.L.record_bytes, J, frames + (int64_t)e * SS, 1, 0, lds)) {
+      CBEV_STAMP(2, 3);
+      return;
+    }
+  }
   // staging at raised wave priority: the CU's other workgroups are mostly
   // painting or writing out, and issuing this one's map loads first keeps the
   // memory pipe busier (raster 25.5 -> 24.9 us at config 2)
@@ -1707,7 +2053,7 @@ __global__ __launch_bounds__(raster_threads(64 * G)) __attribute__((amdgpu_waves
   __builtin_amdgcn_s_setprio(0);
   __syncthreads();
   CBEV_STAMP(2, 1);
-  raster_paint<NT>(K, r, J.pq, J.xmin, J.ymin, J.shift, lds);
+  raster_paint<G, NT>(K, r, J.pq, J.xmin, J.ymin, J.shift, lds);
   CBEV_STAMP(2, 2);
   raster_emit<G, NT>(K, J, frames + (int64_t)e * SS, 1, 0, lds);
   CBEV_STAMP(2, 3);
@@ -2403,8 +2749,7 @@ __global__ __launch_bounds__(256) void k_ego(KArgs K, uint8_t* __restrict__ recs
   if (lane < ne_eff) {
     const double* hd = (const double*)(lds + lane * pk.bytes + K.L.hd);
     if (wave == 0) {
-      pre[lane].cyaw = cos(hd[CBEV_HD_YAW]);
-      pre[lane].syaw = sin(hd[CBEV_HD_YAW]);
+      d_sincos(hd[CBEV_HD_YAW], &pre[lane].syaw, &pre[lane].cyaw);
     } else if (wave == 1) {
       const double max_steer = 30.0 * (CB_PI / 180.0);
       pre[lane].tdelta = tan(d_clip(d_hero_delta(hd[CBEV_HD_V], asa), -max_steer, max_steer));
@@ -2473,8 +2818,7 @@ __global__ __launch_bounds__(256) void k_ego(KArgs K, uint8_t* __restrict__ recs
       hero_env_render_setup(K, rec(lane));
     } else if (wave == 3) {  // the updated yaw's cos / sin for the actors' TTCs (S5)
       const double yaw = ((const double*)(lds + lane * pk.bytes + K.L.hd))[CBEV_HD_YAW];
-      pre[lane].cyaw = cos(yaw);
-      pre[lane].syaw = sin(yaw);
+      d_sincos(yaw, &pre[lane].syaw, &pre[lane].cyaw);
     } else if (wave == 0) {
       const DRec r = rec(lane);
       const double x = r.hd[CBEV_HD_X], y = r.hd[CBEV_HD_Y];
@@ -2596,7 +2940,9 @@ __global__ __launch_bounds__(256) void k_ego(KArgs K, uint8_t* __restrict__ recs
         const double hvx_m = hv_m * cyaw, hvy_m = hv_m * syaw;
         const double hvx = v * cyaw, hvy = v * syaw;
         const double av = mine ? pav : RAD(r, CBEV_AD_V, a), ayaw = mine ? payaw : RAD(r, CBEV_AD_YAW, a);
-        const double avx = av * cos(ayaw), avy = av * sin(ayaw);
+        double say, cay;
+        d_sincos(ayaw, &say, &cay);
+        const double avx = av * cay, avy = av * say;
         {  // compute_ttc_raw (reward_signals.py:46-94)
           double rx_ = ax * CB_MPP - hx_m, ry_ = ay * CB_MPP - hy_m;
           double rvx = avx * CB_MPP - hvx_m, rvy = avy * CB_MPP - hvy_m;
@@ -2784,6 +3130,38 @@ __global__ __launch_bounds__(256) void k_expand_rgb(const uint8_t* __restrict__ 
   }
 }
 
+// Palette-id frames <-> nibble-packed frames (ids are <= 15): byte j of a packed
+// frame holds pixel 2j in its low nibble and pixel 2j + 1 in its high nibble.
+// The wire format of the multi-GPU frame gather (sharding.FrameGather): half
+// the bytes of the uint8 frames. 16 pixels per thread, one 16-byte load and one
+// 8-byte store (pack) or the reverse (unpack), streamed (non-temporal).
+typedef uint32_t nt_u2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t pack8(uint32_t a, uint32_t b) {  // 8 ids (two dwords) -> 8 nibbles
+  const uint32_t x = (a & 0x0f0f0f0fu) | ((a >> 4) & 0xf0f0f0f0u);    // bytes 0|1<<4 in byte 0, 2|3<<4 in byte 2
+  const uint32_t y = (b & 0x0f0f0f0fu) | ((b >> 4) & 0xf0f0f0f0u);
+  return (x & 0xffu) | ((x >> 8) & 0xff00u) | ((y & 0xffu) << 16) | ((y << 8) & 0xff000000u);
+}
+__device__ __forceinline__ uint32_t unpack4(uint32_t h) {  // 4 packed bytes (low half of the dword's ids) -> ids
+  const uint32_t b0 = h & 0xffu, b1 = (h >> 8) & 0xffu;
+  return (b0 & 15u) | ((b0 >> 4) << 8) | ((b1 & 15u) << 16) | ((b1 >> 4) << 24);
+}
+__global__ __launch_bounds__(256) void k_pack_frames(const uint8_t* __restrict__ ids, int64_t n16,
+                                                     uint8_t* __restrict__ packed) {
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n16; i += (int64_t)gridDim.x * 256) {
+    const uint4 v = *(const uint4*)(ids + 16 * i);
+    const nt_u2 o = {pack8(v.x, v.y), pack8(v.z, v.w)};
+    __builtin_nontemporal_store(o, (nt_u2*)(packed + 8 * i));
+  }
+}
+__global__ __launch_bounds__(256) void k_unpack_frames(const uint8_t* __restrict__ packed, int64_t n16,
+                                                       uint8_t* __restrict__ ids) {
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n16; i += (int64_t)gridDim.x * 256) {
+    const uint2 h = *(const uint2*)(packed + 8 * i);
+    const nt_u4 o = {unpack4(h.x), unpack4(h.x >> 16), unpack4(h.y), unpack4(h.y >> 16)};
+    __builtin_nontemporal_store(o, (nt_u4*)(ids + 16 * i));
+  }
+}
+
 // obs_mode "vector" (carlabev.py:237-244): float32 [x, y, yaw, v] of the hero
 // (State.state, state.py:53-60) + set_point [cx, cy, cyaw][target_idx]
 // (stanley_controller.py:140-148), one thread per env.
@@ -2920,6 +3298,8 @@ struct cbev_ctx {
   int device;
   uint8_t* map_dev;
   int64_t map_bytes;
+  uint8_t* map8_dev;  // byte map (byte-image raster staging)
+  int p8;
   uint32_t* lut_dev;  // 16 entries
   int prof_on;
   int64_t prof_n;
@@ -3044,6 +3424,8 @@ static KArgs kargs(const cbev_ctx* c) {
   K.L = c->L;
   K.map = c->map_dev;
   K.npitch = c->npitch;
+  K.map8 = c->map8_dev;
+  K.p8 = c->p8;
   K.fov = (const uint32_t*)c->fov_dev;
   K.err = c->err_dev;
   K.nterm = c->nterm_dev;
@@ -3072,6 +3454,15 @@ static const void* reset_kernel(int size) {
   return size == 64 ? (const void*)k_reset<1> : size == 128 ? (const void*)k_reset<2> : (const void*)k_reset<4>;
 }
 static size_t raster_lds_bytes(const cbev_params& P) { return (size_t)raster_image_bytes(P.size, P.crop); }
+// One step's observation for n records: one workgroup per env.
+static void launch_raster(const cbev_ctx* c, const KArgs& K, void* records, int n, uint8_t* frames, hipStream_t s) {
+  const size_t lb = raster_lds_bytes(c->P);
+  switch (c->P.size) {
+    case 64: hipLaunchKernelGGL(k_raster<1>, dim3(n), dim3(raster_threads(64)), lb, s, K, (uint8_t*)records, n, frames); break;
+    case 128: hipLaunchKernelGGL(k_raster<2>, dim3(n), dim3(raster_threads(128)), lb, s, K, (uint8_t*)records, n, frames); break;
+    default: hipLaunchKernelGGL(k_raster<4>, dim3(n), dim3(raster_threads(256)), lb, s, K, (uint8_t*)records, n, frames); break;
+  }
+}
 
 
 extern "C" {
@@ -3162,6 +3553,16 @@ int cbev_create(const cbev_params* params, const cbev_caps* caps, int device, cb
   if (e == hipSuccess)
     e = hipFuncSetAttribute(bank_frames_kernel(P.size), hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)raster_lds_bytes(P));
+  // the byte-image gathers address the LDS absolutely: the crop image must be the
+  // first thing in the workgroup's LDS (no static segment before it)
+  for (const void* kf : {raster_kernel(P.size), reset_kernel(P.size), bank_frames_kernel(P.size)}) {
+    hipFuncAttributes fa;
+    if (e == hipSuccess) e = hipFuncGetAttributes(&fa, kf);
+    if (e == hipSuccess && fa.sharedSizeBytes != 0) {
+      free(c);
+      return set_err(CBEV_EINVAL, "cbev_create: raster kernel declares %zu bytes of static LDS", fa.sharedSizeBytes);
+    }
+  }
   if (e != hipSuccess) {
     free(c);
     return set_err(CBEV_EHIP, "cbev_create: %s", hipGetErrorString(e));
@@ -3248,19 +3649,11 @@ int cbev_profile_raster(cbev_ctx* c, void* records, int n, uint8_t* frames, int 
   HIP_TRY(hipSetDevice(c->device));
   hipStream_t s = (hipStream_t)stream;
   const KArgs K = kargs(c);
-  const size_t lb = raster_lds_bytes(c->P);
-  const int rg = n;
   hipEvent_t ev[2];
   HIP_TRY(hipEventCreate(&ev[0]));
   HIP_TRY(hipEventCreate(&ev[1]));
   HIP_TRY(hipEventRecord(ev[0], s));
-  for (int i = 0; i < reps; ++i) {
-    switch (c->P.size) {
-      case 64: hipLaunchKernelGGL(k_raster<1>, dim3(rg), dim3(raster_threads(64)), lb, s, K, (uint8_t*)records, n, frames); break;
-      case 128: hipLaunchKernelGGL(k_raster<2>, dim3(rg), dim3(raster_threads(128)), lb, s, K, (uint8_t*)records, n, frames); break;
-      default: hipLaunchKernelGGL(k_raster<4>, dim3(rg), dim3(raster_threads(256)), lb, s, K, (uint8_t*)records, n, frames); break;
-    }
-  }
+  for (int i = 0; i < reps; ++i) launch_raster(c, K, records, n, frames, s);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipEventRecord(ev[1], s));
   HIP_TRY(hipEventSynchronize(ev[1]));
@@ -3280,6 +3673,7 @@ void cbev_destroy(cbev_ctx* c) {
     free(c->prof_ev);
   }
   if (c->map_dev) (void)hipFree(c->map_dev);
+  if (c->map8_dev) (void)hipFree(c->map8_dev);
   if (c->lut_dev) (void)hipFree(c->lut_dev);
   if (c->err_dev) (void)hipFree(c->err_dev);
   if (c->nterm_dev) (void)hipFree(c->nterm_dev);
@@ -3314,6 +3708,17 @@ int cbev_set_map(cbev_ctx* c, const uint8_t* map_host, int64_t bytes) {
   HIP_TRY(hipMemcpy(c->map_dev, packed.data(), nbytes, hipMemcpyHostToDevice));
   c->map_bytes = nbytes;
   c->npitch = np;
+  // byte map for the byte-image raster: a 16-byte staging chunk of a crop row
+  // may start up to 3 bytes before xmin and end up to ~16 bytes past the crop
+  const int p8 = (W + 64 + 63) & ~63;
+  std::vector<uint8_t> map8((size_t)p8 * H, 0);
+  for (int y = 0; y < H; ++y) memcpy(map8.data() + (size_t)y * p8, map_host + (size_t)y * pitch, W);
+  if (c->map8_dev) HIP_TRY(hipFree(c->map8_dev));
+  c->map8_dev = nullptr;
+  HIP_TRY(hipMalloc(&c->map8_dev, (size_t)p8 * H + 4096));
+  HIP_TRY(hipMemset(c->map8_dev, 0, (size_t)p8 * H + 4096));
+  HIP_TRY(hipMemcpy(c->map8_dev, map8.data(), (size_t)p8 * H, hipMemcpyHostToDevice));
+  c->p8 = p8;
   return CBEV_OK;
 }
 
@@ -3356,15 +3761,7 @@ int cbev_step(cbev_ctx* c, void* records, int n, const void* actions, uint8_t* f
   hipLaunchKernelGGL(k_ego, dim3((n + c->ego_ne - 1) / c->ego_ne), dim3(256), (size_t)c->ego_lb, s, K,
                      (uint8_t*)records, n, actions, reward, term, trunc, cause, info, c->ego_ne);
   if (ev) HIP_TRY(hipEventRecord(ev[2], s));
-  {
-    const size_t lb = raster_lds_bytes(c->P);
-    const int rg = n;
-    switch (c->P.size) {
-      case 64: hipLaunchKernelGGL(k_raster<1>, dim3(rg), dim3(raster_threads(64)), lb, s, K, (uint8_t*)records, n, frames); break;
-      case 128: hipLaunchKernelGGL(k_raster<2>, dim3(rg), dim3(raster_threads(128)), lb, s, K, (uint8_t*)records, n, frames); break;
-      default: hipLaunchKernelGGL(k_raster<4>, dim3(rg), dim3(raster_threads(256)), lb, s, K, (uint8_t*)records, n, frames); break;
-    }
-  }
+  launch_raster(c, K, records, n, frames, s);
   if (ev) HIP_TRY(hipEventRecord(ev[3], s));
   HIP_TRY(hipGetLastError());
   return CBEV_OK;
@@ -3555,6 +3952,26 @@ static void area_tab(int ssize, int dsize, double scale, std::vector<int32_t>& o
     }
   }
   off[dsize] = (int32_t)si.size();
+}
+
+int cbev_pack_frames(cbev_ctx* c, const uint8_t* frames, int n, uint8_t* packed, void* stream) {
+  if (!c || !frames || !packed) return set_err(CBEV_EINVAL, "null argument");
+  if (n <= 0) return CBEV_OK;
+  const int64_t n16 = (int64_t)n * c->P.size * c->P.size / 16;  // S is a multiple of 64
+  const int grid = (int)std::min<int64_t>((n16 + 255) / 256, 8192);
+  hipLaunchKernelGGL(k_pack_frames, dim3(grid), dim3(256), 0, (hipStream_t)stream, frames, n16, packed);
+  HIP_TRY(hipGetLastError());
+  return CBEV_OK;
+}
+
+int cbev_unpack_frames(cbev_ctx* c, const uint8_t* packed, int n, uint8_t* frames, void* stream) {
+  if (!c || !frames || !packed) return set_err(CBEV_EINVAL, "null argument");
+  if (n <= 0) return CBEV_OK;
+  const int64_t n16 = (int64_t)n * c->P.size * c->P.size / 16;
+  const int grid = (int)std::min<int64_t>((n16 + 255) / 256, 8192);
+  hipLaunchKernelGGL(k_unpack_frames, dim3(grid), dim3(256), 0, (hipStream_t)stream, packed, n16, frames);
+  HIP_TRY(hipGetLastError());
+  return CBEV_OK;
 }
 
 int cbev_vector_obs(cbev_ctx* c, const void* records, int n, float* out, void* stream) {

@@ -25,6 +25,8 @@ struct KArgs {
   const uint8_t* map;  // padded class map, nibble-packed: render_h rows x npitch bytes,
                        // texel x of a row in byte x >> 1, high nibble when x is odd
   int npitch;
+  const uint8_t* map8;  // the same map, one palette id per byte (p8 bytes per row): the byte-image raster stages it
+  int p8;
   const uint32_t* fov;  // FOV corner mask, S*S bytes (0xff = black), or null (fov_masked off)
   int32_t* err;         // device error word (CBEV_ERR_* bits, read by cbev_error_flags)
   unsigned long long* nterm;  // terminations since cbev_create (cbev_termination_count)
@@ -106,8 +108,16 @@ __device__ __forceinline__ DRec bind_rec(uint8_t* base, const cbev_layout& L, co
 
 // ---------------------------------------------------------------- NumPy semantics
 // npy_remainder: Python-style modulo (sign of the divisor)
+// fmod(a, b) for b > 0: a - trunc(a / b) * b, which is exact. For |a| < 2b the
+// quotient is -1, 0 or 1 and a -/+ b is exact (Sterbenz: b <= |a| < 2b), so the
+// common case (angles a few radians from the range) skips the library's loop.
+__device__ __forceinline__ double d_fmod_pos(double a, double b) {
+  const double aa = fabs(a);
+  if (!(aa < 2.0 * b)) return fmod(a, b);  // also NaN / inf
+  return aa < b ? a : (a > 0 ? a - b : a + b);
+}
 __device__ __forceinline__ double d_remainder(double a, double b) {
-  double m = fmod(a, b);
+  double m = b > 0 ? d_fmod_pos(a, b) : fmod(a, b);
   if (m != 0.0) {
     if ((b < 0) != (m < 0)) m += b;
   } else {
@@ -124,6 +134,9 @@ __device__ __forceinline__ double d_clip(double a, double lo, double hi) {
 }
 __device__ __forceinline__ double d_pymax(double a, double b) { return (b > a) ? b : a; }
 __device__ __forceinline__ double d_degrees(double r) { return r * (180.0 / CB_PI); }
+// sin and cos of one argument with one argument reduction (ocml's sincos runs
+// the same reduction and kernels as sin and cos)
+__device__ __forceinline__ void d_sincos(double x, double* s, double* c) { sincos(x, s, c); }
 __device__ __forceinline__ double d_radians(double d) { return d * (CB_PI / 180.0); }
 
 // ---------------------------------------------------------------- wave reductions
@@ -229,8 +242,10 @@ __device__ __forceinline__ void d_state_update(double* s, double acc, double del
   s[5] = s[1];
   s[6] = s[2];
   s[7] = s[3];
-  s[0] += s[3] * cos(s[2]) * CB_DT;
-  s[1] += s[3] * sin(s[2]) * CB_DT;
+  double sn, cs;
+  d_sincos(s[2], &sn, &cs);
+  s[0] += s[3] * cs * CB_DT;
+  s[1] += s[3] * sn * CB_DT;
   s[2] += s[3] / CB_WHEELBASE * tan(delta) * CB_DT;
   s[3] += acc * CB_DT;
   s[2] = d_angle_mod(s[2]);
@@ -240,8 +255,10 @@ __device__ __forceinline__ void d_state_update(double* s, double acc, double del
 // Controller.calc_target_index on one lane (serial over the route)
 __device__ __forceinline__ int d_target_index_serial(double x, double y, double yaw, const double* cx,
                                                      const double* cy, int n, double* err) {
-  double fx = x + CB_WHEELBASE * cos(yaw);
-  double fy = y + CB_WHEELBASE * sin(yaw);
+  double sy, cy_;
+  d_sincos(yaw, &sy, &cy_);
+  double fx = x + CB_WHEELBASE * cy_;
+  double fy = y + CB_WHEELBASE * sy;
   // argmin of hypot (first on ties) in two passes: the squared distance
   // dx*dx + dy*dy is within a few ulp of hypot^2, so every index whose hypot
   // can reach the minimum has a squared distance within (1 + 1e-14) of the
@@ -270,7 +287,9 @@ __device__ __forceinline__ int d_target_index_serial(double x, double y, double 
     }
   }
   if (err) {
-    double fa0 = -cos(yaw + CB_PI / 2.0), fa1 = -sin(yaw + CB_PI / 2.0);
+    double sp, cp;
+    d_sincos(yaw + CB_PI / 2.0, &sp, &cp);
+    double fa0 = -cp, fa1 = -sp;
     *err = (fx - cx[best]) * fa0 + (fy - cy[best]) * fa1;
   }
   return best;

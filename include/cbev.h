@@ -159,6 +159,14 @@ int cbev_expand_obs(cbev_ctx* ctx, const uint8_t* ring, int n, int n_frames, int
  * target_idx (stanley_controller.py:140-148), from the records as they are now. */
 int cbev_vector_obs(cbev_ctx* ctx, const void* records, int n, float* out, void* stream);
 
+/* The multi-GPU frame gather's wire format (palette ids are
+ * <= 15): packed = uint8[n][S*S/2], byte j of env e = frames[e][2j] |
+ * frames[e][2j + 1] << 4. cbev_unpack_frames is the inverse. The reference has
+ * no multi-process path (SyncVectorEnv, envs/__init__.py:116-119): this halves
+ * the bytes the gather of the compact observation moves over xGMI. */
+int cbev_pack_frames(cbev_ctx* ctx, const uint8_t* frames, int n, uint8_t* packed, void* stream);
+int cbev_unpack_frames(cbev_ctx* ctx, const uint8_t* packed, int n, uint8_t* frames, void* stream);
+
 /* EnvConfig.fov_masked: FovRenderer's static corner mask (envs/fov.py:46-68,96-99)
  * applied by the raster (step and reset frames) after compose, before the ego
  * overlay. mask_host = uint8[S][S], 0xff where the output is blacked out, 0

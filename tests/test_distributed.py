@@ -97,7 +97,18 @@ def test_bench_launcher_dry_run_two_ranks():
     rec = json.loads(lines[0])
     assert rec["n_gpus"] == 2 and rec["dry_run"] and rec["gather_ok"]
     from carlabev_env_amd.sharding import payload_bytes
-    assert rec["gather_bytes_per_step"] == payload_bytes(4, 128)
+    assert rec["gather_bytes_per_step"] == payload_bytes(4, 128)  # nibble-packed frames
+    assert payload_bytes(4, 128) == (4 * 128 * 128 // 2 + 14 * 4 + 15) // 16 * 16
+
+
+def test_pack_frames_roundtrip_cpu():
+    from carlabev_env_amd.sharding import pack_frames, unpack_frames
+    fr = torch.randint(0, 16, (3, 64, 64), dtype=torch.uint8)
+    pk = pack_frames(fr)
+    assert pk.shape == (3, 2048)
+    f0 = fr.reshape(3, -1)
+    assert torch.equal(pk, f0[:, 0::2] | (f0[:, 1::2] << 4))
+    assert torch.equal(unpack_frames(pk, 64), fr)
 
 
 def _packed_worker(rank, world, port, q):
@@ -106,25 +117,29 @@ def _packed_worker(rank, world, port, q):
     try:
         from carlabev_env_amd.sharding import FrameGather
         n, S = 5, 16
-        g = FrameGather(n, S, "cpu")
-        send_ptr = g.send.data_ptr()
-        for step in range(3):  # buffers are reused across steps
+        g = FrameGather(n, S, "cpu")  # nibble-packed frames, two buffers used in turn
+        send_ptrs = [b.data_ptr() for b in g.send]
+        for step in range(5):  # buffers are reused across steps
             gen = torch.Generator().manual_seed(100 * rank + step)
-            fr = torch.randint(0, 10, (n, S, S), dtype=torch.uint8, generator=gen)
+            fr = torch.randint(0, 16, (n, S, S), dtype=torch.uint8, generator=gen)
             rew = torch.randn(n, dtype=torch.float64, generator=gen)
             term = (torch.rand(n, generator=gen) < 0.5).to(torch.uint8)
             trunc = (torch.rand(n, generator=gen) < 0.5).to(torch.uint8)
             cause = torch.randint(-1, 6, (n,), dtype=torch.int32, generator=gen)
             g.gather(fr, rew, term, trunc, cause)
-            assert g.send.data_ptr() == send_ptr
+            assert [b.data_ptr() for b in g.send] == send_ptrs
             if rank == 0:
                 q.put((step, tuple(t.clone().numpy() for t in g.gathered())))
+        g.wait()
         dist.barrier()
     finally:
         dist.destroy_process_group()
 
 
 def test_packed_gather_all_fields():
+    """The nibble-packed, double-buffered asynchronous gather (sharding.FrameGather)
+    round-trips every palette id 0..15 and the reward / cause / flag fields of
+    both ranks over five steps, reusing its two send buffers."""
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -132,7 +147,7 @@ def test_packed_gather_all_fields():
     procs = [ctx.Process(target=_packed_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    got = [q.get(timeout=240) for _ in range(3)]
+    got = [q.get(timeout=240) for _ in range(5)]
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -140,7 +155,7 @@ def test_packed_gather_all_fields():
     for step, (fr, rew, cause, term, trunc) in got:
         for r in range(world):
             gen = torch.Generator().manual_seed(100 * r + step)
-            e_fr = torch.randint(0, 10, (n, S, S), dtype=torch.uint8, generator=gen).numpy()
+            e_fr = torch.randint(0, 16, (n, S, S), dtype=torch.uint8, generator=gen).numpy()
             e_rew = torch.randn(n, dtype=torch.float64, generator=gen).numpy()
             e_term = (torch.rand(n, generator=gen) < 0.5).to(torch.uint8).numpy()
             e_trunc = (torch.rand(n, generator=gen) < 0.5).to(torch.uint8).numpy()
