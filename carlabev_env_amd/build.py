@@ -15,8 +15,12 @@ DEPS = [SRC, os.path.join(HERE, "csrc", "cbev_device.h"), os.path.join(REPO, "in
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 # -ffp-contract=off: hipcc contracts a*b+c into FMA by default, which changes
 # rounding relative to the reference's (and the oracle's) float64 arithmetic.
+# -amdgpu-kernarg-preload-count=16: the leading scalar kernel arguments (up to 16
+# dwords; k_ego puts its staging scalars there) arrive in SGPRs at wave start
+# instead of through a cold kernarg-segment load (cbev.hip, EgoStage).
 FLAGS = ["--offload-arch=gfx950", "-O3", "-fPIC", "-shared", "-std=c++17", "-ffp-contract=off",
-         "-fno-fast-math", "-Wall", "-Wno-unused-function", f"-I{os.path.join(REPO, 'include')}"]
+         "-fno-fast-math", "-Wall", "-Wno-unused-function", "-mllvm", "-amdgpu-kernarg-preload-count=16",
+         f"-I{os.path.join(REPO, 'include')}"]
 
 
 def needs_build() -> bool:

@@ -34,6 +34,7 @@
 
 #include <algorithm>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/cbev.h"
@@ -691,13 +692,15 @@ __device__ unsigned g_hwid[CBEV_NSTAMP][4096];                   // HW_ID (SE / 
 #endif
 
 // ---- record staging for k_ego. A workgroup owns `ne` envs (a divisor of 64,
-// so a 64-env block stays on one XCD) and copies the record ranges its float64
-// chains and element loops read into LDS with LDS-DMA (16-byte lane-linear
-// pieces, all in flight at once), packed per env as
-//   [HD, HI, cx, cy] [raw_x, raw_y] [vis, vis_draw]
-// (EgoPack). Everything read at one index only (cyaw at the target index,
-// raw_cum at two segments) or by a few lanes (actor fields) is read from the
-// record in HBM; the fields the kernel changes are copied back at the end.
+// so a 64-env block stays on one XCD) and copies the record prefix its float64
+// chains and element loops read -- HD, HI, cx, cy, cyaw, raw_x, raw_y, raw_cum,
+// vis, vis_draw, contiguous in the layout -- into LDS with LDS-DMA (16-byte
+// lane-linear pieces, all in flight at once), at the record's own offsets
+// (EgoPack). Only the actor groups (read by a few lanes) stay in HBM. Staging
+// cyaw and raw_cum too (1 KB more per env at route_cap 64) takes the HBM loads
+// of cyaw[target] and raw_cum[segment] out of the S3 / S5 / S6 chains, each a
+// dependent ~1 us latency. The fields the kernel changes (HD, HI, the vis group)
+// are copied back at the end.
 __device__ __forceinline__ int staged_env0(int w, int ne, int n) {
   const int n512 = n & ~511;
   if (w * ne >= n512) return w * ne;
@@ -706,52 +709,51 @@ __device__ __forceinline__ int staged_env0(int w, int ne, int n) {
 }
 
 struct EgoPack {
-  int n0, n1, n2;        // 16-byte pieces of the three ranges
-  int raw_off, vis_off;  // byte offsets of the second and third range in the packed image
-  int bytes;             // packed bytes per env
+  int n;            // 16-byte pieces of the staged prefix
+  int vis_c, nvis;  // the vis group's first piece and piece count
+  int bytes;        // staged bytes per env
 };
 __host__ __device__ __forceinline__ EgoPack ego_pack(const cbev_layout& L) {
   EgoPack p;
-  p.n0 = (int)(L.cyaw / 16);                   // HD, HI, cx, cy (the record's prefix)
-  p.n1 = (int)((L.raw_cum - L.raw_x) / 16);    // raw_x, raw_y
-  p.n2 = (int)((8 * L.vis_words + 15) / 16);   // vis, vis_draw
-  p.raw_off = 16 * p.n0;
-  p.vis_off = 16 * (p.n0 + p.n1);
-  p.bytes = 16 * (p.n0 + p.n1 + p.n2);
+  const int64_t end = L.vis + 8 * (int64_t)L.vis_words;  // vis, vis_draw
+  p.n = (int)((end + 15) / 16);
+  p.vis_c = (int)(L.vis / 16);
+  p.nvis = p.n - p.vis_c;
+  p.bytes = 16 * p.n;
   return p;
 }
 
-// DRec of a staged env: the packed ranges in LDS, every other group in HBM
-__device__ __forceinline__ DRec bind_ego(uint8_t* l, uint8_t* g, const KArgs& K, const EgoPack& p) {
+// DRec of a staged env: the prefix in LDS, the actor groups in HBM
+__device__ __forceinline__ DRec bind_ego(uint8_t* l, uint8_t* g, const KArgs& K) {
   DRec r = bind_rec(g, K.L, K.C);
-  r.hd = (double*)(l + K.L.hd);
-  r.hi = (int32_t*)(l + K.L.hi);
-  r.cx = (double*)(l + K.L.cx);
-  r.cy = (double*)(l + K.L.cy);
-  r.raw_x = (int32_t*)(l + p.raw_off);
-  r.raw_y = (int32_t*)(l + p.raw_off + (K.L.raw_y - K.L.raw_x));
-  r.vis = (uint32_t*)(l + p.vis_off);
-  r.vis_draw = r.vis + K.L.vis_words;
+  const DRec s = bind_rec(l, K.L, K.C);
+  r.hd = s.hd;
+  r.hi = s.hi;
+  r.cx = s.cx;
+  r.cy = s.cy;
+  r.cyaw = s.cyaw;
+  r.raw_x = s.raw_x;
+  r.raw_y = s.raw_y;
+  r.raw_cum = s.raw_cum;
+  r.vis = s.vis;
+  r.vis_draw = s.vis_draw;
   return r;
 }
 
-// record byte offset of packed piece c
-__device__ __forceinline__ int ego_src(const cbev_layout& L, const EgoPack& p, int c) {
-  return c < p.n0 ? 16 * c : c < p.n0 + p.n1 ? (int)L.raw_x + 16 * (c - p.n0) : (int)L.vis + 16 * (c - p.n0 - p.n1);
-}
-
-// LDS-DMA: piece q of the workgroup lands at LDS byte 16 q (lane-linear per wave)
-__device__ __forceinline__ void ego_stage_in(uint8_t* lds, const uint8_t* __restrict__ recs, int e0, int ne,
-                                             const KArgs& K, const EgoPack& p) {
-  const int nch = p.bytes >> 4, total = ne * nch;
+// LDS-DMA: piece c of env k (record byte 16 c) lands at LDS byte 16 (k n + c),
+// lane-linear per wave. rb, n: passed as leading kernel arguments, which the
+// launch preloads into SGPRs (kernarg preloading, -amdgpu-kernarg-preload-count),
+// so the first load is issued at wave start.
+__device__ __forceinline__ void ego_stage_in(uint8_t* lds, const uint8_t* __restrict__ recs, int e0, int ne, int rb,
+                                             int n) {
+  const int total = ne * n;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int64_t rb = K.L.record_bytes;
   for (int b = wave * 64; b < total; b += 256) {
     const int q = b + lane;
     if (q < total) {
-      const int k = q / nch, c = q - k * nch;
-      __builtin_amdgcn_global_load_lds((const void*)(recs + (int64_t)(e0 + k) * rb + ego_src(K.L, p, c)),
+      const int k = q / n, c = q - k * n;
+      __builtin_amdgcn_global_load_lds((const void*)(recs + (int64_t)(e0 + k) * rb + 16 * c),
                                        (__attribute__((address_space(3))) void*)(lds + 16 * b), 16, 0, 0);
     }
   }
@@ -760,12 +762,12 @@ __device__ __forceinline__ void ego_stage_in(uint8_t* lds, const uint8_t* __rest
 // the changed ranges back: HD + HI (the first pieces) and the vis group
 __device__ __forceinline__ void ego_stage_out(const uint8_t* lds, uint8_t* __restrict__ recs, int e0, int ne,
                                               const KArgs& K, const EgoPack& p) {
-  const int nhh = (int)(K.L.cx / 16), nout = nhh + p.n2;
+  const int nhh = (int)(K.L.cx / 16), nout = nhh + p.nvis;
   const int64_t rb = K.L.record_bytes;
   for (int q = threadIdx.x; q < ne * nout; q += 256) {
     const int k = q / nout, j = q - k * nout;
-    const int c = j < nhh ? j : p.n0 + p.n1 + (j - nhh);
-    *(uint4*)(recs + (int64_t)(e0 + k) * rb + ego_src(K.L, p, c)) = *(const uint4*)(lds + k * p.bytes + 16 * c);
+    const int c = j < nhh ? j : p.vis_c + (j - nhh);
+    *(uint4*)(recs + (int64_t)(e0 + k) * rb + 16 * c) = *(const uint4*)(lds + k * p.bytes + 16 * c);
   }
 }
 
@@ -1989,7 +1991,11 @@ __device__ __forceinline__ bool raster8_env(const KArgs& K, uint8_t* rec, const 
   if (PAINT) pq = raster_paint_fetch(r);  // in flight under the staging
   stage8(K, J, W, lds);
   __syncthreads();
-  if (PAINT) paint8(K, r, pq, J, W, lds);
+  if (PAINT) {
+    CBEV_STAMP(2, 1);
+    paint8(K, r, pq, J, W, lds);
+    CBEV_STAMP(2, 2);
+  }
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   raster_out8<G, 4>(K.P, J.R, W, lds, out, nout, out_stride, lane, wave, K.fov, NCH);
@@ -2030,9 +2036,14 @@ void k_raster(
     KArgs K, uint8_t* __restrict__ recs, int n, uint8_t* __restrict__ frames) {
   extern __shared__ __align__(16) uint8_t lds[];
   constexpr int NT = raster_threads(64 * G);
+  CBEV_STAMP(2, 0);
+#ifdef CBEV_RASTER_KTOUCH
+  // the kernel arguments of the render set-up and the staging in one round of
+  // scalar loads (left to itself the compiler fetches them branch by branch)
+  asm volatile("" ::"s"(n), "s"(recs), "s"(K.L.record_bytes), "s"(K.L.hi), "s"(K.map8), "s"(K.p8), "s"(K.P.crop));
+#endif
   const int e = xcd_env_of_wg(blockIdx.x, n);
   if (e >= n) return;
-  CBEV_STAMP(2, 0);
   const int64_t SS = (int64_t)K.P.size * K.P.size;
   const DRec r = bind_rec(recs + (int64_t)e * K.L.record_bytes, K.L, K.C);
   RasterJob J;
@@ -2677,12 +2688,45 @@ __device__ __forceinline__ void collide_env(const KArgs& K, DRec r, int e, const
   CBEV_STAMP(4, 3);
 }
 
+// ---- butterfly reductions over the tpe lanes of an env (tpe a power of two,
+// groups aligned to tpe). Partner at level OFF: DPP inside a row of 16 lanes for
+// OFF = 1, 2 (quad_perm [1,0,3,2], [2,3,0,1]), 4 (row_half_mirror: lane l of a
+// group of 8 with 7 - l) and 8 (row_mirror: l with 15 - l) -- after levels 1 and
+// 2 every lane of a quad holds the quad's result and after 4 every lane of an 8,
+// so a mirror pairs complementary partials as an xor would -- then ds_bpermute
+// (__shfl_xor) across rows. The combines are commutative and associative
+// (minimum with a lowest-index tie-break), so the pairing order does not matter.
+// A DPP move is one VALU instruction; __shfl_xor is an LDS round trip each.
+template <int OFF>
+__device__ __forceinline__ int peer_i32(int v) {
+  if constexpr (OFF == 1) return __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xF, 0xF, false);
+  else if constexpr (OFF == 2) return __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xF, 0xF, false);
+  else if constexpr (OFF == 4) return __builtin_amdgcn_update_dpp(0, v, 0x141, 0xF, 0xF, false);
+  else if constexpr (OFF == 8) return __builtin_amdgcn_update_dpp(0, v, 0x140, 0xF, 0xF, false);
+  else return __shfl_xor(v, OFF, 64);
+}
+template <int OFF>
+__device__ __forceinline__ double peer_f64(double v) {
+  const int lo = peer_i32<OFF>(__double2loint(v)), hi = peer_i32<OFF>(__double2hiint(v));
+  return __hiloint2double(hi, lo);
+}
+// f(std::integral_constant<int, OFF>) for OFF = 1, 2, 4, ... < tpe (uniform tpe <= 64)
+template <class F>
+__device__ __forceinline__ void butterfly(int tpe, F&& f) {
+  if (tpe > 1) f(std::integral_constant<int, 1>{});
+  if (tpe > 2) f(std::integral_constant<int, 2>{});
+  if (tpe > 4) f(std::integral_constant<int, 4>{});
+  if (tpe > 8) f(std::integral_constant<int, 8>{});
+  if (tpe > 16) f(std::integral_constant<int, 16>{});
+  if (tpe > 32) f(std::integral_constant<int, 32>{});
+}
+
 // ============================================================== k_ego
 // The ego half of CarlaBEV.step() (scene.py:90-140, carlabev.py:159-185) for
 // `ne` envs per 256-thread workgroup, in one launch after k_actors and before
 // k_raster:
-//   S0  actions decoded; HD, HI, cx, cy, raw_x, raw_y and the vis words of the
-//       ne records staged into LDS (ego_stage_in)
+//   S0  the ne records' prefixes (HD .. vis_draw) staged into LDS
+//       (ego_stage_in), then the actions decoded
 //   S1  cos / sin of the yaw (wave 0) beside tan(clip(delta)) (wave 1)
 //   S2  Controller.calc_target_index over (env, route point) pairs: squared
 //       distances, then hypot for the candidates within (1 + 1e-14) of the
@@ -2699,24 +2743,30 @@ __device__ __forceinline__ void collide_env(const KArgs& K, DRec r, int e, const
 //   S7  HD, HI and the vis group back to the records
 // k_raster reads only what this kernel wrote (RS_* set-up, poses, vis_draw),
 // so collision no longer has to wait for the frame.
-__global__ __launch_bounds__(256) void k_ego(KArgs K, uint8_t* __restrict__ recs, int n,
+__global__ __launch_bounds__(256) void k_ego(uint8_t* __restrict__ recs, int n, int ne, int st_rb, int st_n, KArgs K,
                                              const void* __restrict__ actions, double* __restrict__ reward_out,
                                              uint8_t* __restrict__ term_out, uint8_t* __restrict__ trunc_out,
-                                             int32_t* __restrict__ cause_out, float* __restrict__ info_out, int ne) {
+                                             int32_t* __restrict__ cause_out, float* __restrict__ info_out) {
   extern __shared__ __align__(16) uint8_t lds[];
+  CBEV_STAMP(0, 0);
   const int e0 = staged_env0(blockIdx.x, ne, n);
   const int ne_eff = min(ne, n - e0);
-  if (ne_eff <= 0) return;
+  // S0: the staging first (it depends on nothing loaded, and its scalars are
+  // preloaded), then the action loads and the actor prefetch, whose latency
+  // overlaps the staging's
+  ego_stage_in(lds, recs, e0, ne_eff > 0 ? ne_eff : 0, st_rb, st_n);
+  CBEV_STAMP(3, 0);
   const cbev_params& P = K.P;
   const EgoPack pk = ego_pack(K.L);
-  const CollScratchLayout SL = coll_scratch_layout(K.C, K.L.vis_words);
   const int64_t rb = K.L.record_bytes;
+  if (ne_eff <= 0) return;
+  const CollScratchLayout SL = coll_scratch_layout(K.C, K.L.vis_words);
   uint8_t* scr = lds + ne * pk.bytes;          // [ne] collision scratch
   HeroPre* pre = (HeroPre*)(scr + ne * SL.bytes);  // [ne]
   int* best = (int*)(pre + ne);                   // [ne] target search result
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  auto rec = [&](int k) { return bind_ego(lds + k * pk.bytes, recs + (int64_t)(e0 + k) * rb, K, pk); };
+  auto rec = [&](int k) { return bind_ego(lds + k * pk.bytes, recs + (int64_t)(e0 + k) * rb, K); };
   if (blockIdx.x == 0 && tid == 0) {
     if (K.ep_count_next != nullptr) *K.ep_count_next = 0;
     if (K.tl_count_next != nullptr) {  // the previous step's resets took bank rows [cursor, cursor + count)
@@ -2724,8 +2774,7 @@ __global__ __launch_bounds__(256) void k_ego(KArgs K, uint8_t* __restrict__ recs
       *K.tl_count_next = 0;
     }
   }
-  CBEV_STAMP(0, 0);
-  // S0 (wave 0 runs the chain, wave 1 the steering tangent)
+  // wave 0 runs the chain, wave 1 the steering tangent
   float ag = 0.f, asa = 0.f, ab = 0.f;
   if (wave <= 1 && lane < ne_eff) d_decode_action(K, actions, e0 + lane, &ag, &asa, &ab);
   // the (env, actor) pair of S5 this thread takes first: its actor's fields are
@@ -2742,7 +2791,6 @@ __global__ __launch_bounds__(256) void k_ego(KArgs K, uint8_t* __restrict__ recs
     pav = RAD(g, CBEV_AD_V, a);
     pasz = RAI(g, CBEV_AI_SIZE, a);
   }
-  ego_stage_in(lds, recs, e0, ne_eff, K, pk);
   __syncthreads();
   CBEV_STAMP(0, 1);
   // S1
@@ -2756,6 +2804,7 @@ __global__ __launch_bounds__(256) void k_ego(KArgs K, uint8_t* __restrict__ recs
     }
   }
   __syncthreads();
+  CBEV_STAMP(3, 1);
   // S2
   {
     const int tpe = 256 / ne, k = tid / tpe, sub = tid - k * tpe;
@@ -2774,10 +2823,11 @@ __global__ __launch_bounds__(256) void k_ego(KArgs K, uint8_t* __restrict__ recs
         const double d2 = dx * dx + dy * dy;
         m2 = d2 < m2 ? d2 : m2;
       }
-      for (int o = tpe >> 1; o > 0; o >>= 1) {
-        const double t = __shfl_xor(m2, o, tpe);
+      butterfly(tpe, [&](auto off) {
+        const double t = peer_f64<decltype(off)::value>(m2);
         m2 = t < m2 ? t : m2;
-      }
+      });
+      CBEV_STAMP(3, 2);
       const double lim = m2 * (1.0 + 1e-14);
       double bd = INFINITY;
       int bi = 0x7fffffff;
@@ -2791,17 +2841,19 @@ __global__ __launch_bounds__(256) void k_ego(KArgs K, uint8_t* __restrict__ recs
           }
         }
       }
-      for (int o = tpe >> 1; o > 0; o >>= 1) {  // smallest hypot, lowest index on ties
-        const double qd = __shfl_xor(bd, o, tpe);
-        const int qi = __shfl_xor(bi, o, tpe);
+      butterfly(tpe, [&](auto off) {  // smallest hypot, lowest index on ties
+        constexpr int O = decltype(off)::value;
+        const double qd = peer_f64<O>(bd);
+        const int qi = peer_i32<O>(bi);
         if (qd < bd || (qd == bd && qi < bi)) {
           bd = qd;
           bi = qi;
         }
-      }
+      });
       if (sub == 0) best[k] = bi == 0x7fffffff ? 0 : bi;
     }
   }
+  CBEV_STAMP(3, 3);
   __syncthreads();
   CBEV_STAMP(0, 2);
   // S3
@@ -2864,6 +2916,7 @@ __global__ __launch_bounds__(256) void k_ego(KArgs K, uint8_t* __restrict__ recs
           bi = i;
         }
       }
+      CBEV_STAMP(5, 0);
       const int tidx = r.hi[CBEV_HI_TIDX];
       const int nw = d_next_wps(tidx, r.hi[CBEV_HI_NROUTE]);
       double lk = INFINITY, le = INFINITY;
@@ -2876,21 +2929,23 @@ __global__ __launch_bounds__(256) void k_ego(KArgs K, uint8_t* __restrict__ recs
           li = i;
         }
       }
-      for (int off = tpe >> 1; off > 0; off >>= 1) {
-        const double ob = __shfl_xor(bd, off, 64);
-        const int obi = __shfl_xor(bi, off, 64);
+      CBEV_STAMP(5, 1);
+      butterfly(tpe, [&](auto off) {
+        constexpr int O = decltype(off)::value;
+        const double ob = peer_f64<O>(bd);
+        const int obi = peer_i32<O>(bi);
         if (ob < bd || (ob == bd && obi < bi)) {
           bd = ob;
           bi = obi;
         }
-        const double ok = __shfl_xor(lk, off, 64), oe = __shfl_xor(le, off, 64);
-        const int oli = __shfl_xor(li, off, 64);
+        const double ok = peer_f64<O>(lk), oe = peer_f64<O>(le);
+        const int oli = peer_i32<O>(li);
         if (ok < lk || (ok == lk && oli < li)) {
           lk = ok;
           le = oe;
           li = oli;
         }
-      }
+      });
       if (sub == 0) {
         double* red = (double*)(sk + SL.segd);
         const bool any = bd < 1e9;
@@ -2899,6 +2954,7 @@ __global__ __launch_bounds__(256) void k_ego(KArgs K, uint8_t* __restrict__ recs
         red[2] = le;
         ((int*)(sk + SL.ints))[CS_BSEG] = any ? bi : 0;
       }
+      CBEV_STAMP(5, 2);
       // visible targets vs the hero rect (target.py:37-44)
       int* I = (int*)(sk + SL.ints);
       const int hrx = I[3], hry = I[4];
@@ -2913,6 +2969,7 @@ __global__ __launch_bounds__(256) void k_ego(KArgs K, uint8_t* __restrict__ recs
           atomicMax(&I[CS_TGT_LAST], i);
         }
       }
+      CBEV_STAMP(5, 3);
     }
     // vehicles / pedestrians (fields read from HBM, field-major over the actor
     // slots): rect hit, actors_state entry and both TTCs (scene.py:110-140,
@@ -3511,6 +3568,10 @@ int cbev_create(const cbev_params* params, const cbev_caps* caps, int device, cb
   const int per_env = ego_pack(lay).bytes + coll_scratch_layout(*caps, lay.vis_words).bytes + (int)sizeof(HeroPre) +
                       (int)sizeof(int);
   const int ego_ne = ego_ne_for(per_env, caps->actor_cap);
+  // k_ego stages the record prefix HD .. vis_draw as one range (EgoPack)
+  if (!(lay.hd < lay.hi && lay.hi < lay.cx && lay.cx < lay.cy && lay.cy < lay.cyaw && lay.cyaw < lay.raw_x &&
+        lay.raw_x < lay.raw_y && lay.raw_y < lay.raw_cum && lay.raw_cum < lay.vis && lay.vis % 16 == 0))
+    return set_err(CBEV_EINVAL, "record layout: the k_ego prefix is not contiguous");
   if (ego_ne == 0)
     return set_err(CBEV_EINVAL, "k_ego stages 4 records per workgroup: %d bytes each do not fit its LDS budget",
                    per_env);
@@ -3758,8 +3819,9 @@ int cbev_step(cbev_ctx* c, void* records, int n, const void* actions, uint8_t* f
     K.ep_count_next = c->ep_counts + next;
     c->step_count += 1;
   }
-  hipLaunchKernelGGL(k_ego, dim3((n + c->ego_ne - 1) / c->ego_ne), dim3(256), (size_t)c->ego_lb, s, K,
-                     (uint8_t*)records, n, actions, reward, term, trunc, cause, info, c->ego_ne);
+  hipLaunchKernelGGL(k_ego, dim3((n + c->ego_ne - 1) / c->ego_ne), dim3(256), (size_t)c->ego_lb, s,
+                     (uint8_t*)records, n, c->ego_ne, (int)c->L.record_bytes, ego_pack(c->L).n, K, actions, reward,
+                     term, trunc, cause, info);
   if (ev) HIP_TRY(hipEventRecord(ev[2], s));
   launch_raster(c, K, records, n, frames, s);
   if (ev) HIP_TRY(hipEventRecord(ev[3], s));

@@ -4,8 +4,8 @@ set -eu
 mkdir -p tools/micro/ab
 for v in "$@"; do
   name=${v%%:*}; flags=${v#*:}
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -shared -std=c++17 -ffp-contract=off -fno-fast-math \
-    -Wno-unused-function -Iinclude $flags -o tools/micro/ab/libcbev_$name.so carlabev_env_amd/csrc/cbev.hip &
+  /opt/rocm/bin/hipcc $(python -c "from carlabev_env_amd import build as B; print(' '.join(B.FLAGS))") \
+    $flags -o tools/micro/ab/libcbev_$name.so carlabev_env_amd/csrc/cbev.hip &
 done
 wait
 ls tools/micro/ab

@@ -23,9 +23,10 @@ ap.add_argument("--reset", action="store_true", help="canonical loop: reset the 
 a = ap.parse_args()
 so = os.path.join(REPO, "gpurun_out", "libcbev_timing.so")
 os.makedirs(os.path.dirname(so), exist_ok=True)
-subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-fPIC", "-shared", "-std=c++17",
-                "-ffp-contract=off", "-fno-fast-math", f"-I{REPO}/include", "-DCBEV_TIMING", *a.defs.split(),
-                "-o", so, f"{REPO}/carlabev_env_amd/csrc/cbev.hip"], check=True)
+sys.path.insert(0, REPO)
+from carlabev_env_amd import build as B  # noqa: E402
+
+subprocess.run([B.HIPCC, *B.FLAGS, "-DCBEV_TIMING", *a.defs.split(), "-o", so, B.SRC], check=True)
 os.environ["CBEV_LIB"] = so
 sys.path.insert(0, REPO)
 import torch  # noqa: E402
@@ -55,7 +56,7 @@ xcc = buf[2 * NS * 4096 * 4:].reshape(NS, 4096).astype(np.int64)
 hwid = xcc >> 32
 xcc = xcc & 0xFFFFFFFF
 buf = buf[:2 * NS * 4096 * 4].reshape(2, NS, 4096, 4)
-for k, name in enumerate(("k_ego A: stage-in / S1+S2 search / S3 chain + S4", "k_ego B: S5 collision pre-pass / S6 collide chain / stage-out", "k_raster", "-", "collide_env(thread0)", "-", "k_actors: behaviour / search / stanley+update (per wave)")):
+for k, name in enumerate(("k_ego A: stage-in / S1+S2 search / S3 chain + S4", "k_ego B: S5 collision pre-pass / S6 collide chain / stage-out", "k_raster", "k_ego wave 0: DMA issued / S1 done / S2 min / S2 done", "collide_env(thread0)", "k_ego S5 (wave 0): segs / lateral / reduce / targets", "k_actors: behaviour / search / stanley+update (per wave)")):
     if not (buf[0, k, :, 0] > 0).any():
         continue
     st = buf[0, k].astype(np.int64)
@@ -66,6 +67,10 @@ for k, name in enumerate(("k_ego A: stage-in / S1+S2 search / S3 chain + S4", "k
           f"WG mean {(rt[:, 3] - rt[:, 0]).mean() / 100:.2f} us, first start->last start "
           f"{(rt[:, 0].max() - rt[:, 0].min()) / 100:.2f} us; clock {((st[:, 3] - st[:, 0]).sum() / max((rt[:, 3] - rt[:, 0]).sum(), 1)) / 100:.2f} GHz")
     d = np.diff(st, axis=1)
+    if k in (3, 5):  # cycles since the start of k_ego A (3) / B (5) in the same workgroup
+        ref = buf[0, 0 if k == 3 else 1].astype(np.int64)[used][:, 0]
+        print(f"{name}: cycles since the phase start: {[round(float((st[:, j] - ref).mean())) for j in range(4)]}")
+        continue
     print(f"{name}: {used.sum()} WGs; cycles mean phase1 {d[:, 0].mean():.0f} (max {d[:, 0].max():.0f})  phase2 {d[:, 1].mean():.0f} "
           f"(max {d[:, 1].max():.0f})  phase3 {d[:, 2].mean():.0f}; WG total mean {(st[:, 3] - st[:, 0]).mean():.0f}; "
           )
