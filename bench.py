@@ -234,6 +234,18 @@ def launch_ranks(n: int) -> int:
     return rc
 
 
+def gather_budget(config: int, ranks: int = 8, link_gbs: float = 153.0, links: int = 7) -> dict:
+    """Per-rank gather payload of `config` at its bench size, nibble-packed (as
+    FrameGather sends it) and unpacked, and rank 0's ingress time for `ranks`
+    ranks over `links` point-to-point xGMI links of `link_gbs` GB/s."""
+    from carlabev_env_amd.sharding import payload_bytes
+    cfgd = CONFIGS[config]
+    packed, plain = payload_bytes(cfgd["envs"], cfgd["size"]), payload_bytes(cfgd["envs"], cfgd["size"], packed=False)
+    ingress = lambda b: round((ranks - 1) * b / (links * link_gbs * 1e9) * 1e3, 3)  # noqa: E731
+    return {"envs_per_rank": cfgd["envs"], "bytes_packed": packed, "bytes_unpacked": plain, "ranks": ranks,
+            "rank0_ingress_ms_packed": ingress(packed), "rank0_ingress_ms_unpacked": ingress(plain)}
+
+
 def dry_run(args, world, rank):
     """CPU rehearsal of the N-rank path (gloo): rendezvous, the packed frame
     gather of config 4 (FrameGather on CPU tensors), barrier-bracketed timing and
@@ -271,6 +283,7 @@ def dry_run(args, world, rank):
                           "unit": "env-steps/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
                           "ms_per_step": round(el / max(args.steps, 1) * 1e3, 4), "dry_run": True,
                           "gather_ok": ok, "gather_bytes_per_step": None if g is None else g.bytes_per_step,
+                          "at_config_size": gather_budget(args.config),
                           "config": {"config_id": args.config, "envs_per_gpu": n, "global_envs": n * world}}),
               flush=True)
     if world > 1:

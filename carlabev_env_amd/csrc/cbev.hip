@@ -740,8 +740,8 @@ __device__ __forceinline__ DRec bind_ego(uint8_t* l, uint8_t* g, const KArgs& K)
   return r;
 }
 
-// LDS-DMA: piece c of env k (record byte 16 c) lands at LDS byte 16 (k n + c),
-// lane-linear per wave. rb, n: passed as leading kernel arguments, which the
+// LDS-DMA by waves 2 and 3: piece c of env k (record byte 16 c) lands at LDS
+// byte 16 (k n + c), lane-linear per wave. rb, n: passed as leading kernel arguments, which the
 // launch preloads into SGPRs (kernarg preloading, -amdgpu-kernarg-preload-count),
 // so the first load is issued at wave start.
 __device__ __forceinline__ void ego_stage_in(uint8_t* lds, const uint8_t* __restrict__ recs, int e0, int ne, int rb,
@@ -749,7 +749,8 @@ __device__ __forceinline__ void ego_stage_in(uint8_t* lds, const uint8_t* __rest
   const int total = ne * n;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  for (int b = wave * 64; b < total; b += 256) {
+  if (wave < 2) return;  // waves 0 and 1 run S1 meanwhile (k_ego)
+  for (int b = (wave - 2) * 64; b < total; b += 128) {
     const int q = b + lane;
     if (q < total) {
       const int k = q / n, c = q - k * n;
@@ -2727,10 +2728,10 @@ __device__ __forceinline__ void butterfly(int tpe, F&& f) {
 // k_raster:
 //   S0  the ne records' prefixes (HD .. vis_draw) staged into LDS
 //       (ego_stage_in), then the actions decoded
-//   S1  cos / sin of the yaw (wave 0) beside tan(clip(delta)) (wave 1)
-//   S2  Controller.calc_target_index over (env, route point) pairs: squared
-//       distances, then hypot for the candidates within (1 + 1e-14) of the
-//       smallest, first minimum (stanley_controller.py:51-62)
+//   S1  cos / sin of the yaw (wave 0) beside tan(clip(delta)) (wave 1), from
+//       the record in HBM while waves 2 and 3 stage it
+//   S2  Controller.calc_target_index over (env, route point) pairs: hypot, the
+//       first minimum (stanley_controller.py:51-62)
 //   S3  the ego chain, one thread per env (BaseAgent.physics_step, hero.py:88-138)
 //   S4  comfort + dist2goal (wave 1) | render set-up of this step's observation
 //       (wave 2) | collision prologue (wave 0): ego tile load, hero rect, and the
@@ -2774,9 +2775,20 @@ __global__ __launch_bounds__(256) void k_ego(uint8_t* __restrict__ recs, int n, 
       *K.tl_count_next = 0;
     }
   }
-  // wave 0 runs the chain, wave 1 the steering tangent
+  // S1 under the staging (waves 0 and 1 issue none of it): the actions, and
+  // from the record's yaw and speed cos / sin of the yaw (wave 0, which runs the
+  // chain) beside tan(clip(delta)) (wave 1)
   float ag = 0.f, asa = 0.f, ab = 0.f;
-  if (wave <= 1 && lane < ne_eff) d_decode_action(K, actions, e0 + lane, &ag, &asa, &ab);
+  if (wave <= 1 && lane < ne_eff) {
+    d_decode_action(K, actions, e0 + lane, &ag, &asa, &ab);
+    const double* ghd = (const double*)(recs + (int64_t)(e0 + lane) * rb + K.L.hd);
+    if (wave == 0) {
+      d_sincos(ghd[CBEV_HD_YAW], &pre[lane].syaw, &pre[lane].cyaw);
+    } else {
+      const double max_steer = 30.0 * (CB_PI / 180.0);
+      pre[lane].tdelta = tan(d_clip(d_hero_delta(ghd[CBEV_HD_V], asa), -max_steer, max_steer));
+    }
+  }
   // the (env, actor) pair of S5 this thread takes first: its actor's fields are
   // loaded now, in flight under S0-S4 (slots past NACT hold zeros and are skipped)
   const int A = K.C.actor_cap;
@@ -2793,17 +2805,6 @@ __global__ __launch_bounds__(256) void k_ego(uint8_t* __restrict__ recs, int n, 
   }
   __syncthreads();
   CBEV_STAMP(0, 1);
-  // S1
-  if (lane < ne_eff) {
-    const double* hd = (const double*)(lds + lane * pk.bytes + K.L.hd);
-    if (wave == 0) {
-      d_sincos(hd[CBEV_HD_YAW], &pre[lane].syaw, &pre[lane].cyaw);
-    } else if (wave == 1) {
-      const double max_steer = 30.0 * (CB_PI / 180.0);
-      pre[lane].tdelta = tan(d_clip(d_hero_delta(hd[CBEV_HD_V], asa), -max_steer, max_steer));
-    }
-  }
-  __syncthreads();
   CBEV_STAMP(3, 1);
   // S2
   {
@@ -2816,31 +2817,18 @@ __global__ __launch_bounds__(256) void k_ego(uint8_t* __restrict__ recs, int n, 
       const int nr = ((const int32_t*)(base + K.L.hi))[CBEV_HI_NROUTE];
       const double fx = hd[CBEV_HD_X] + CB_WHEELBASE * pre[k].cyaw;
       const double fy = hd[CBEV_HD_Y] + CB_WHEELBASE * pre[k].syaw;
-      double m2 = INFINITY;
-#pragma unroll 4
-      for (int i = sub; i < nr; i += tpe) {
-        const double dx = fx - cx[i], dy = fy - cy[i];
-        const double d2 = dx * dx + dy * dy;
-        m2 = d2 < m2 ? d2 : m2;
-      }
-      butterfly(tpe, [&](auto off) {
-        const double t = peer_f64<decltype(off)::value>(m2);
-        m2 = t < m2 ? t : m2;
-      });
-      CBEV_STAMP(3, 2);
-      const double lim = m2 * (1.0 + 1e-14);
+      // np.argmin(np.hypot(dx, dy)): the first smallest hypot, in one pass
       double bd = INFINITY;
       int bi = 0x7fffffff;
+#pragma unroll 4
       for (int i = sub; i < nr; i += tpe) {
-        const double dx = fx - cx[i], dy = fy - cy[i];
-        if (dx * dx + dy * dy <= lim) {
-          const double h = hypot(dx, dy);
-          if (h < bd) {  // first minimum within this thread's (increasing) indices
-            bd = h;
-            bi = i;
-          }
+        const double h = hypot(fx - cx[i], fy - cy[i]);
+        if (h < bd) {  // first minimum within this thread's (increasing) indices; NaN never wins
+          bd = h;
+          bi = i;
         }
       }
+      CBEV_STAMP(3, 2);
       butterfly(tpe, [&](auto off) {  // smallest hypot, lowest index on ties
         constexpr int O = decltype(off)::value;
         const double qd = peer_f64<O>(bd);

@@ -99,6 +99,12 @@ def test_bench_launcher_dry_run_two_ranks():
     from carlabev_env_amd.sharding import payload_bytes
     assert rec["gather_bytes_per_step"] == payload_bytes(4, 128)  # nibble-packed frames
     assert payload_bytes(4, 128) == (4 * 128 * 128 // 2 + 14 * 4 + 15) // 16 * 16
+    # config 4 at its bench size (8192 envs per rank): the packed payload is half
+    # the unpacked one, and rank 0's ingress at 8 ranks over 7 xGMI links halves
+    b = rec["at_config_size"]
+    assert b["envs_per_rank"] == 8192 and b["bytes_packed"] == payload_bytes(8192, 128)
+    assert abs(b["bytes_unpacked"] - 2 * b["bytes_packed"]) <= 14 * 8192
+    assert 0.43 < b["rank0_ingress_ms_packed"] < 0.45 and 0.87 < b["rank0_ingress_ms_unpacked"] < 0.89
 
 
 def test_pack_frames_roundtrip_cpu():
