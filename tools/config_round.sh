@@ -24,6 +24,6 @@ run pmc_fetch --kernel-trace --pmc FETCH_SIZE
 run pmc_write --kernel-trace --pmc WRITE_SIZE
 # summaries only (the raw traces exceed what gpurun copies back)
 ENVS=$(python -c "import json; print(json.loads(open('gpurun_out/bench_cfg$CFG.json').read().strip().splitlines()[-1])['config']['envs_per_gpu'])")
-python tools/summarize_profile.py --src $OUT --tag round2_config$CFG --config $CFG --envs $ENVS --out gpurun_out/psum || exit 1
+python tools/summarize_profile.py --src $OUT --tag ${TAG:-round3}_config$CFG --config $CFG --envs $ENVS --out gpurun_out/psum || exit 1
 rm -rf $OUT
 exit 0
