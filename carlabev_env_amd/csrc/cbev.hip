@@ -2224,20 +2224,22 @@ __global__ __launch_bounds__(256) void k_reset_copy(KArgs K, uint8_t* __restrict
 // whole bank in order (every reset a distinct scene until it wraps) and does not
 // depend on the order the terminations were appended in. Pieces as in
 // k_reset_copy (16 KB, RESET_PU loads per thread in flight), dealt over the grid.
-__global__ __launch_bounds__(256) void k_reset_list(KArgs K, uint8_t* __restrict__ recs, int n,
-                                                    const uint8_t* __restrict__ bank, int n_bank,
-                                                    const int32_t* __restrict__ list, const uint32_t* __restrict__ count,
-                                                    const unsigned long long* __restrict__ cursor,
+// The leading scalar arguments are preloaded into SGPRs by the launch (kernarg
+// preloading): the count load is issued at wave start.
+__global__ __launch_bounds__(256) void k_reset_list(const uint32_t* __restrict__ count,
+                                                    const int32_t* __restrict__ list,
+                                                    const unsigned long long* __restrict__ cursor, int n, int n_bank,
+                                                    int rb, int SS, int n_frames, uint8_t* __restrict__ recs,
+                                                    const uint8_t* __restrict__ bank,
                                                     const uint8_t* __restrict__ bank_frames, uint8_t* __restrict__ ring,
-                                                    int n_frames) {
+                                                    KArgs K) {
+  const unsigned long long cur = *cursor;
   const int cnt = min((int)__builtin_amdgcn_readfirstlane(*count), n);
+  asm volatile("" ::"s"(cur), "s"(cnt));  // the cursor loaded beside the count (one wait)
   if (cnt == 0) return;
-  const int64_t rb = K.L.record_bytes;
-  const int64_t SS = (int64_t)K.P.size * K.P.size;
   const int pf = reset_pieces(SS), ppe = pf + reset_pieces(rb);
   const int total = cnt * ppe;
   if ((int)blockIdx.x >= total) return;
-  const unsigned long long cur = *cursor;
   for (int p = blockIdx.x; p < total; p += gridDim.x) {
     const int slot = p / ppe, c = p - slot * ppe;
     const int e = list[slot];
@@ -3891,9 +3893,9 @@ int cbev_reset_terminated(cbev_ctx* c, void* records, int n, const void* bank, i
   const int grid = pieces >= RESET_LIST_WGS ? RESET_LIST_WGS : (int)pieces;
   // the counter the last cbev_step appended to (parity flipped after it)
   const uint32_t* cnt = c->tl_count_dev + (c->tl_parity ^ 1);
-  hipLaunchKernelGGL(k_reset_list, dim3(grid), dim3(256), 0, (hipStream_t)stream, K, (uint8_t*)records, n,
-                     (const uint8_t*)bank, n_bank, (const int32_t*)c->tl_list_dev, cnt,
-                     (const unsigned long long*)c->tl_cursor_dev, bank_frames, frames, n_frames);
+  hipLaunchKernelGGL(k_reset_list, dim3(grid), dim3(256), 0, (hipStream_t)stream, cnt, (const int32_t*)c->tl_list_dev,
+                     (const unsigned long long*)c->tl_cursor_dev, n, n_bank, (int)c->L.record_bytes,
+                     c->P.size * c->P.size, n_frames, (uint8_t*)records, (const uint8_t*)bank, bank_frames, frames, K);
   HIP_TRY(hipGetLastError());
   return CBEV_OK;
 }
