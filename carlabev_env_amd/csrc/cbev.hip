@@ -692,15 +692,15 @@ __device__ unsigned g_hwid[CBEV_NSTAMP][4096];                   // HW_ID (SE / 
 #endif
 
 // ---- record staging for k_ego. A workgroup owns `ne` envs (a divisor of 64,
-// so a 64-env block stays on one XCD) and copies the record prefix its float64
-// chains and element loops read -- HD, HI, cx, cy, cyaw, raw_x, raw_y, raw_cum,
-// vis, vis_draw, contiguous in the layout -- into LDS with LDS-DMA (16-byte
-// lane-linear pieces, all in flight at once), at the record's own offsets
-// (EgoPack). Only the actor groups (read by a few lanes) stay in HBM. Staging
-// cyaw and raw_cum too (1 KB more per env at route_cap 64) takes the HBM loads
-// of cyaw[target] and raw_cum[segment] out of the S3 / S5 / S6 chains, each a
-// dependent ~1 us latency. The fields the kernel changes (HD, HI, the vis group)
-// are copied back at the end.
+// so a 64-env block stays on one XCD) and copies the record ranges its float64
+// chains and element loops read into LDS with LDS-DMA (16-byte lane-linear
+// pieces, all in flight at once), packed per env as two ranges of the layout:
+//   [HD, HI, cx, cy] [raw_x, raw_y, raw_cum, vis, vis_draw]
+// (EgoPack). cyaw (read at one index, by the shaping reward only) and the
+// actor groups (read by a few lanes) stay in HBM. raw_cum is staged: its reads
+// at the arg-min segment (S5) and the route end (S6) sat inside the chains, a
+// dependent HBM latency each. The fields the kernel changes (HD, HI, the vis
+// group) are copied back at the end.
 __device__ __forceinline__ int staged_env0(int w, int ne, int n) {
   const int n512 = n & ~511;
   if (w * ne >= n512) return w * ne;
@@ -709,43 +709,49 @@ __device__ __forceinline__ int staged_env0(int w, int ne, int n) {
 }
 
 struct EgoPack {
-  int n;            // 16-byte pieces of the staged prefix
-  int vis_c, nvis;  // the vis group's first piece and piece count
+  int n0, n;        // 16-byte pieces of the first range, of both
+  int raw_x;        // record offset of the second range (its LDS offset is 16 n0)
+  int vis_c, nvis;  // the vis group's first packed piece and piece count
   int bytes;        // staged bytes per env
 };
 __host__ __device__ __forceinline__ EgoPack ego_pack(const cbev_layout& L) {
   EgoPack p;
-  const int64_t end = L.vis + 8 * (int64_t)L.vis_words;  // vis, vis_draw
-  p.n = (int)((end + 15) / 16);
-  p.vis_c = (int)(L.vis / 16);
+  p.n0 = (int)(L.cyaw / 16);                              // HD, HI, cx, cy (the record's prefix)
+  const int64_t end = L.vis + 8 * (int64_t)L.vis_words;  // raw_x .. vis_draw
+  p.n = p.n0 + (int)((end - L.raw_x + 15) / 16);
+  p.raw_x = (int)L.raw_x;
+  p.vis_c = p.n0 + (int)((L.vis - L.raw_x) / 16);
   p.nvis = p.n - p.vis_c;
   p.bytes = 16 * p.n;
   return p;
 }
 
-// DRec of a staged env: the prefix in LDS, the actor groups in HBM
-__device__ __forceinline__ DRec bind_ego(uint8_t* l, uint8_t* g, const KArgs& K) {
+// DRec of a staged env: the two ranges in LDS, cyaw and the actor groups in HBM
+__device__ __forceinline__ DRec bind_ego(uint8_t* l, uint8_t* g, const KArgs& K, const EgoPack& p) {
   DRec r = bind_rec(g, K.L, K.C);
-  const DRec s = bind_rec(l, K.L, K.C);
+  const DRec s = bind_rec(l, K.L, K.C);  // the first range at the record's offsets
   r.hd = s.hd;
   r.hi = s.hi;
   r.cx = s.cx;
   r.cy = s.cy;
-  r.cyaw = s.cyaw;
-  r.raw_x = s.raw_x;
-  r.raw_y = s.raw_y;
-  r.raw_cum = s.raw_cum;
-  r.vis = s.vis;
-  r.vis_draw = s.vis_draw;
+  uint8_t* l1 = l + 16 * p.n0 - K.L.raw_x;  // the second range: record offset o at l1 + o
+  r.raw_x = (int32_t*)(l1 + K.L.raw_x);
+  r.raw_y = (int32_t*)(l1 + K.L.raw_y);
+  r.raw_cum = (double*)(l1 + K.L.raw_cum);
+  r.vis = (uint32_t*)(l1 + K.L.vis);
+  r.vis_draw = r.vis + K.L.vis_words;
   return r;
 }
 
-// LDS-DMA by waves 2 and 3: piece c of env k (record byte 16 c) lands at LDS
-// byte 16 (k n + c), lane-linear per wave. rb, n: passed as leading kernel arguments, which the
-// launch preloads into SGPRs (kernarg preloading, -amdgpu-kernarg-preload-count),
-// so the first load is issued at wave start.
+// record byte offset of packed piece c
+__device__ __forceinline__ int ego_src(int n0, int raw_x, int c) { return c < n0 ? 16 * c : raw_x + 16 * (c - n0); }
+
+// LDS-DMA by waves 2 and 3: packed piece c of env k lands at LDS byte
+// 16 (k n + c), lane-linear per wave. rb, n0, n, raw_x: passed as leading kernel
+// arguments, which the launch preloads into SGPRs (kernarg preloading,
+// -amdgpu-kernarg-preload-count), so the first load is issued at wave start.
 __device__ __forceinline__ void ego_stage_in(uint8_t* lds, const uint8_t* __restrict__ recs, int e0, int ne, int rb,
-                                             int n) {
+                                             int n0, int n, int raw_x) {
   const int total = ne * n;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -754,7 +760,7 @@ __device__ __forceinline__ void ego_stage_in(uint8_t* lds, const uint8_t* __rest
     const int q = b + lane;
     if (q < total) {
       const int k = q / n, c = q - k * n;
-      __builtin_amdgcn_global_load_lds((const void*)(recs + (int64_t)(e0 + k) * rb + 16 * c),
+      __builtin_amdgcn_global_load_lds((const void*)(recs + (int64_t)(e0 + k) * rb + ego_src(n0, raw_x, c)),
                                        (__attribute__((address_space(3))) void*)(lds + 16 * b), 16, 0, 0);
     }
   }
@@ -768,7 +774,7 @@ __device__ __forceinline__ void ego_stage_out(const uint8_t* lds, uint8_t* __res
   for (int q = threadIdx.x; q < ne * nout; q += 256) {
     const int k = q / nout, j = q - k * nout;
     const int c = j < nhh ? j : p.vis_c + (j - nhh);
-    *(uint4*)(recs + (int64_t)(e0 + k) * rb + 16 * c) = *(const uint4*)(lds + k * p.bytes + 16 * c);
+    *(uint4*)(recs + (int64_t)(e0 + k) * rb + ego_src(p.n0, p.raw_x, c)) = *(const uint4*)(lds + k * p.bytes + 16 * c);
   }
 }
 
@@ -1953,6 +1959,7 @@ __device__ __forceinline__ void raster_out8(const cbev_params& P, const RotSetup
   }
 }
 
+
 // rotate90 (exact multiples of 90 degrees: pygame's rotate90 transposes) as the
 // affine map it is: k_ego's texel steps (+-1 column or +-rt = a row, per output
 // column / row) become 16.16 steps of +-65536 with sin / cos in {0, +-1}, and the
@@ -2508,7 +2515,7 @@ __device__ __forceinline__ void collide_env(const KArgs& K, DRec r, int e, const
 
   // scene_info / controller_info (scene.py:206-225, stanley_controller.py:125-163)
   const int tidx = hi[CBEV_HI_TIDX];
-  const double spx = r.cx[tidx], spy = r.cy[tidx], spyaw = r.cyaw[tidx];
+  const double spx = r.cx[tidx], spy = r.cy[tidx];
   double dist2wp;
   {
     double dx = x - spx, dy = y - spy;
@@ -2622,6 +2629,7 @@ __device__ __forceinline__ void collide_env(const KArgs& K, DRec r, int e, const
       } else {
         double rr = 0.0;
         const double yaw1 = hd[CBEV_HD_YAW1], v1 = hd[CBEV_HD_V1];
+        const double spyaw = r.cyaw[tidx];  // HBM (k_ego does not stage cyaw)
         double yaw_error = atan2(sin(spyaw - yaw), cos(spyaw - yaw));
         double align = cos(yaw_error);
         double d2r = pre.have_sd ? pre.d2r : d_lateral_error(x, y, r.cx + tidx, r.cy + tidx, nw);
@@ -2746,7 +2754,8 @@ __device__ __forceinline__ void butterfly(int tpe, F&& f) {
 //   S7  HD, HI and the vis group back to the records
 // k_raster reads only what this kernel wrote (RS_* set-up, poses, vis_draw),
 // so collision no longer has to wait for the frame.
-__global__ __launch_bounds__(256) void k_ego(uint8_t* __restrict__ recs, int n, int ne, int st_rb, int st_n, KArgs K,
+__global__ __launch_bounds__(256) void k_ego(uint8_t* __restrict__ recs, int n, int ne, int st_rb, int st_n0, int st_n,
+                                             int st_raw_x, KArgs K,
                                              const void* __restrict__ actions, double* __restrict__ reward_out,
                                              uint8_t* __restrict__ term_out, uint8_t* __restrict__ trunc_out,
                                              int32_t* __restrict__ cause_out, float* __restrict__ info_out) {
@@ -2757,7 +2766,7 @@ __global__ __launch_bounds__(256) void k_ego(uint8_t* __restrict__ recs, int n, 
   // S0: the staging first (it depends on nothing loaded, and its scalars are
   // preloaded), then the action loads and the actor prefetch, whose latency
   // overlaps the staging's
-  ego_stage_in(lds, recs, e0, ne_eff > 0 ? ne_eff : 0, st_rb, st_n);
+  ego_stage_in(lds, recs, e0, ne_eff > 0 ? ne_eff : 0, st_rb, st_n0, st_n, st_raw_x);
   CBEV_STAMP(3, 0);
   const cbev_params& P = K.P;
   const EgoPack pk = ego_pack(K.L);
@@ -2769,7 +2778,7 @@ __global__ __launch_bounds__(256) void k_ego(uint8_t* __restrict__ recs, int n, 
   int* best = (int*)(pre + ne);                   // [ne] target search result
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  auto rec = [&](int k) { return bind_ego(lds + k * pk.bytes, recs + (int64_t)(e0 + k) * rb, K); };
+  auto rec = [&](int k) { return bind_ego(lds + k * pk.bytes, recs + (int64_t)(e0 + k) * rb, K, pk); };
   if (blockIdx.x == 0 && tid == 0) {
     if (K.ep_count_next != nullptr) *K.ep_count_next = 0;
     if (K.tl_count_next != nullptr) {  // the previous step's resets took bank rows [cursor, cursor + count)
@@ -3560,8 +3569,9 @@ int cbev_create(const cbev_params* params, const cbev_caps* caps, int device, cb
   const int ego_ne = ego_ne_for(per_env, caps->actor_cap);
   // k_ego stages the record prefix HD .. vis_draw as one range (EgoPack)
   if (!(lay.hd < lay.hi && lay.hi < lay.cx && lay.cx < lay.cy && lay.cy < lay.cyaw && lay.cyaw < lay.raw_x &&
-        lay.raw_x < lay.raw_y && lay.raw_y < lay.raw_cum && lay.raw_cum < lay.vis && lay.vis % 16 == 0))
-    return set_err(CBEV_EINVAL, "record layout: the k_ego prefix is not contiguous");
+        lay.raw_x < lay.raw_y && lay.raw_y < lay.raw_cum && lay.raw_cum < lay.vis && lay.vis % 16 == 0 &&
+        lay.cyaw % 16 == 0 && lay.raw_x % 16 == 0))
+    return set_err(CBEV_EINVAL, "record layout: the k_ego staging ranges are not contiguous");
   if (ego_ne == 0)
     return set_err(CBEV_EINVAL, "k_ego stages 4 records per workgroup: %d bytes each do not fit its LDS budget",
                    per_env);
@@ -3810,8 +3820,8 @@ int cbev_step(cbev_ctx* c, void* records, int n, const void* actions, uint8_t* f
     c->step_count += 1;
   }
   hipLaunchKernelGGL(k_ego, dim3((n + c->ego_ne - 1) / c->ego_ne), dim3(256), (size_t)c->ego_lb, s,
-                     (uint8_t*)records, n, c->ego_ne, (int)c->L.record_bytes, ego_pack(c->L).n, K, actions, reward,
-                     term, trunc, cause, info);
+                     (uint8_t*)records, n, c->ego_ne, (int)c->L.record_bytes, ego_pack(c->L).n0, ego_pack(c->L).n,
+                     (int)c->L.raw_x, K, actions, reward, term, trunc, cause, info);
   if (ev) HIP_TRY(hipEventRecord(ev[2], s));
   launch_raster(c, K, records, n, frames, s);
   if (ev) HIP_TRY(hipEventRecord(ev[3], s));
