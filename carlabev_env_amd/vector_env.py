@@ -188,6 +188,13 @@ class CarlaBEVVectorEnv:
         self.trunc = torch.zeros(N, dtype=torch.uint8, device=dev)
         self.cause = torch.zeros(N, dtype=torch.int32, device=dev)
         self.info = torch.zeros((N, 16), dtype=torch.float32, device=dev)
+        # device addresses of the per-step buffers (allocated once here): the step's
+        # host path passes them as plain ints instead of re-reading tensor metadata
+        self._p_step = tuple(t.data_ptr() for t in (self.records, self.reward, self.term, self.trunc, self.cause,
+                                                      self.info))
+        self._p_ring, self._slot_bytes = self.ring.data_ptr(), N * h * w
+        self._p_full = self.full.data_ptr() if self.full is not None else None
+        self._dev_index = dev.index if dev.index is not None else torch.cuda.current_device()
         # spaces (envs/spaces.py:27-61 + wrapper spaces)
         aspec = get_action_profile_spec(self.cfg.action_profile_id)
         self.discrete = aspec["action_mode"] == "discrete"
@@ -246,7 +253,8 @@ class CarlaBEVVectorEnv:
 
     # ------------------------------------------------------------------ helpers
     def _stream(self):
-        return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+        # the caller's current stream on the env's device (raw handle: no Stream object per call)
+        return ctypes.c_void_p(torch._C._cuda_getCurrentRawStream(self._dev_index))
 
     def _new_record_buffer(self, n: int) -> np.ndarray:
         return np.zeros((n, self.rb), dtype=np.uint8)
@@ -275,6 +283,7 @@ class CarlaBEVVectorEnv:
         # reset observations of the bank, rendered once; reset_from_bank then only copies
         B, S = self.bank.shape[0], self.S
         self.bank_frames = torch.empty((B, S, S), dtype=torch.uint8, device=self.device)
+        self._p_bank, self._p_bank_frames = self.bank.data_ptr(), self.bank_frames.data_ptr()
         check(lib().cbev_bank_frames(self._ctx, _ptr(self.bank), B, _ptr(self.bank_frames), self._stream()),
               "cbev_bank_frames")
 
@@ -359,15 +368,14 @@ class CarlaBEVVectorEnv:
         if self.bank is None:
             raise RuntimeError("no scene bank attached")
         N, B = self.num_envs, self.bank.shape[0]
+        rec = self._p_step[0]
         if self.resize:
-            check(lib().cbev_reset_terminated(self._ctx, _ptr(self.records), N, _ptr(self.bank), B,
-                                              _ptr(self.bank_frames), _ptr(self.full), 1, self._stream()),
-                  "cbev_reset_terminated")
+            check(lib().cbev_reset_terminated(self._ctx, rec, N, self._p_bank, B, self._p_bank_frames, self._p_full, 1,
+                                              self._stream()), "cbev_reset_terminated")
             self._resize_into_ring(self.term, all_slots=True)
         else:
-            check(lib().cbev_reset_terminated(self._ctx, _ptr(self.records), N, _ptr(self.bank), B,
-                                              _ptr(self.bank_frames), _ptr(self.ring), self.F, self._stream()),
-                  "cbev_reset_terminated")
+            check(lib().cbev_reset_terminated(self._ctx, rec, N, self._p_bank, B, self._p_bank_frames, self._p_ring,
+                                              self.F, self._stream()), "cbev_reset_terminated")
         if not self.auto_obs:
             return None
         obs = self._obs()
@@ -504,10 +512,10 @@ class CarlaBEVVectorEnv:
             self._flush_pending()
             self._ep_step += 1
         self.head = (self.head + 1) % self.F
-        frames = self.full if self.resize else self.ring[self.head]
-        check(lib().cbev_step(self._ctx, _ptr(self.records), self.num_envs, _ptr(a), _ptr(frames), _ptr(self.reward),
-                              _ptr(self.term), _ptr(self.trunc), _ptr(self.cause), _ptr(self.info), self._stream()),
-              "cbev_step")
+        frames = self._p_full if self.resize else self._p_ring + self.head * self._slot_bytes
+        rec, rew, term, trunc, cause, info = self._p_step
+        check(lib().cbev_step(self._ctx, rec, self.num_envs, a.data_ptr(), frames, rew, term, trunc, cause, info,
+                              self._stream()), "cbev_step")
         self._stepped = True
         if self.resize:
             self._resize_into_ring(None, all_slots=False)
