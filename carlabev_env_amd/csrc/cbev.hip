@@ -2053,11 +2053,6 @@ void k_raster(
   extern __shared__ __align__(16) uint8_t lds[];
   constexpr int NT = raster_threads(64 * G);
   CBEV_STAMP(2, 0);
-#ifdef CBEV_RASTER_KTOUCH
-  // the kernel arguments of the render set-up and the staging in one round of
-  // scalar loads (left to itself the compiler fetches them branch by branch)
-  asm volatile("" ::"s"(n), "s"(recs), "s"(K.L.record_bytes), "s"(K.L.hi), "s"(K.map8), "s"(K.p8), "s"(K.P.crop));
-#endif
   const int e = xcd_env_of_wg(blockIdx.x, n);
   if (e >= n) return;
   const int64_t SS = (int64_t)K.P.size * K.P.size;
