@@ -191,6 +191,11 @@ __device__ __noinline__ void d_start_retreat(DRec& r, int a) {
   const double* cx = r.acx + (int64_t)a * RA;
   const double* cy = r.acy + (int64_t)a * RA;
   const double* cyaw = r.acyaw + (int64_t)a * RA;
+  float* cf = r.acf + 2 * (int64_t)a * RA;  // the search's float32 copy follows the route
+  for (int i = 0; i < m; ++i) {
+    cf[2 * i] = (float)cx[i];
+    cf[2 * i + 1] = (float)cy[i];
+  }
   double v0 = RAD(r, CBEV_AD_V, a);
   RAD(r, CBEV_AD_X, a) = cx[0];
   RAD(r, CBEV_AD_Y, a) = cy[0];
@@ -237,8 +242,8 @@ __device__ __forceinline__ void wave_mem_fence() { __builtin_amdgcn_fence(__ATOM
 // ints: a DRec (or KArgs) reference makes every k_actors wave spill that struct
 // to scratch at launch (12 KB per wave), retreat or not.
 __device__ __noinline__ void wave_start_retreat(uint8_t* base, int o_ad, int o_ai, int o_aix, int o_aiy, int o_arx,
-                                                int o_ary, int o_acx, int o_acy, int o_acyaw, int A, int RA, int a,
-                                                int lane) {
+                                                int o_ary, int o_acx, int o_acy, int o_acyaw, int o_acf, int A, int RA,
+                                                int a, int lane) {
   wave_mem_fence();  // the owner lane's behaviour stores come first
   DRec r{};
   r.ad = (double*)(base + o_ad);
@@ -371,6 +376,9 @@ __device__ __noinline__ void wave_start_retreat(uint8_t* base, int o_ad, int o_a
     cx[lane] = cxv;
     cy[lane] = cyv;
     cyaw[lane] = yawv;
+    float* cf = (float*)(base + o_acf) + 2 * ((int64_t)a * RA + lane);  // the search's float32 copy
+    cf[0] = (float)cxv;
+    cf[1] = (float)cyv;
   }
   // ---- Actor.set_route_surface / Controller.set_route(jitter_start=False): pose at the
   // smoothed start, target index from there (calc_target_index), heading cyaw[idx]
@@ -970,6 +978,11 @@ __device__ __forceinline__ void hero_env_render_setup(const KArgs& K, DRec r) {
 // More than 64 actors: d_actor_step per lane.
 // calc_target_index of every live actor of one env (nact <= 64): AW lanes per
 // actor, 64 / AW actors per round; returns lane a's result for actor a
+#ifdef CBEV_ACTOR_F64_ONLY  // A/B switch: the float64 scan alone
+constexpr bool kActorF32 = false;
+#else
+constexpr bool kActorF32 = true;
+#endif
 constexpr int ACTOR_BATCH = 8;  // route points per lane loaded at once in the target search
 template <int AW>
 __device__ __forceinline__ int actor_search(const DRec& r, int nact, uint64_t livem, double fx, double fy, int nrt,
@@ -985,13 +998,62 @@ __device__ __forceinline__ int actor_search(const DRec& r, int nact, uint64_t li
     const bool glive = aa < nact && ((livem >> (aa & 63)) & 1ull);
     const double* cx = r.acx + (int64_t)(aa & 63) * RA;
     const double* cy = r.acy + (int64_t)(aa & 63) * RA;
-    // pass 1: the smallest squared distance (first index) and the runner-up's.
-    // ACTOR_BATCH points per lane are loaded at once (index clamped to the last
-    // point, so no lane branches around a load) and folded in order with
-    // selects: one memory round trip per batch instead of one per point.
+    // pass 1: the smallest squared distance (first index) and the runner-up's,
+    // exactly as a serial float64 scan finds them -- from the float32 copy of
+    // the route first (8 instead of 16 bytes a point: the search is bound by
+    // the route bytes, 105 MB per launch at config 3). Each lane keeps its three
+    // smallest float32 distances; the float64 scan then runs over the points
+    // within 3 eps of the group's float32 minimum distance only: |d_f32 - d| <=
+    // eps = 0.05 px for coordinates below 4096 px (float32 rounding of both
+    // points and of the squares, about 2e-3 px), so the exact arg-min is among
+    // them, and every other point lies more than eps beyond it (its squared
+    // distance exceeds the (1 + 1e-14) tolerance of pass 2: the runner-up test
+    // is unchanged). A lane with three or more such points scans all its points
+    // in float64.
     double m2 = INFINITY, s2 = INFINITY;
     int i2 = 0x7fffffff;
-    if (glive) {
+    float f1 = INFINITY, f2 = INFINITY, f3 = INFINITY;
+    int j1 = -1, j2 = -1;
+    if (glive && kActorF32) {
+      const float2* cf = (const float2*)r.acf + (int64_t)(aa & 63) * RA;
+      const float ffx = (float)gfx, ffy = (float)gfy;
+      for (int i0 = sub; i0 < gn; i0 += ACTOR_BATCH * AW) {
+        float2 p[ACTOR_BATCH];
+#pragma unroll
+        for (int u = 0; u < ACTOR_BATCH; ++u) {
+          const int i = i0 + u * AW;
+          p[u] = cf[i < gn ? i : gn - 1];
+        }
+#pragma unroll
+        for (int u = 0; u < ACTOR_BATCH; ++u) {
+          const int i = i0 + u * AW;
+          const float dx = ffx - p[u].x, dy = ffy - p[u].y;
+          const float d = i < gn ? dx * dx + dy * dy : INFINITY;
+          const bool l1 = d < f1, l2 = d < f2;
+          f3 = l2 ? f2 : (d < f3 ? d : f3);
+          f2 = l1 ? f1 : (l2 ? d : f2);
+          j2 = l1 ? j1 : (l2 ? i : j2);
+          f1 = l1 ? d : f1;
+          j1 = l1 ? i : j1;
+        }
+      }
+    }
+    float mf = f1;
+#pragma unroll
+    for (int off = AW / 2; off > 0; off >>= 1) {
+      const float o = __shfl_xor(mf, off, 64);
+      mf = o < mf ? o : mf;
+    }
+    const float tf = sqrtf(mf) + 0.15f, thr = tf * tf;  // 3 eps
+    auto exact = [&](int i) {  // one point of the serial float64 scan, in index order
+      const double dx = gfx - cx[i], dy = gfy - cy[i];
+      const double d2 = dx * dx + dy * dy;
+      const bool lt = d2 < m2;
+      s2 = lt ? m2 : (d2 < s2 ? d2 : s2);
+      m2 = lt ? d2 : m2;
+      i2 = lt ? i : i2;
+    };
+    if (glive && (!kActorF32 || f3 <= thr)) {  // three or more candidates in this lane: the float64 scan
       for (int i0 = sub; i0 < gn; i0 += ACTOR_BATCH * AW) {
         double px[ACTOR_BATCH], py[ACTOR_BATCH];
 #pragma unroll
@@ -1011,6 +1073,15 @@ __device__ __forceinline__ int actor_search(const DRec& r, int nact, uint64_t li
           i2 = lt ? i : i2;
         }
       }
+    } else if (glive) {
+      int c1 = f1 <= thr ? j1 : -1, c2 = f2 <= thr ? j2 : -1;
+      if (c1 > c2) {  // index order (-1: none)
+        const int t = c1;
+        c1 = c2;
+        c2 = t;
+      }
+      if (c1 >= 0) exact(c1);
+      if (c2 >= 0) exact(c2);
     }
     group_min2<AW>(m2, i2, s2);
     const double lim = m2 * (1.0 + 1e-14);
@@ -1095,7 +1166,7 @@ __global__ __launch_bounds__(256) void k_actors(KArgs K, uint8_t* __restrict__ r
           rm &= rm - 1;
           wave_start_retreat(recs + (int64_t)e * K.L.record_bytes, (int)K.L.ad, (int)K.L.ai, (int)K.L.aix,
                              (int)K.L.aiy, (int)K.L.arx, (int)K.L.ary, (int)K.L.acx, (int)K.L.acy,
-                             (int)K.L.acyaw, r.A, RA, k, lane);
+                             (int)K.L.acyaw, (int)K.L.acf, r.A, RA, k, lane);
         }
       } else if (WIDE) {
         if (retreat) d_start_retreat(r, a);

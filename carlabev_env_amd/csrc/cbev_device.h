@@ -71,6 +71,7 @@ struct DRec {
   double* ad;
   int32_t* ai;
   double *acx, *acy, *acyaw, *aix, *aiy, *arx, *ary;
+  float* acf;  // [A][RA][2]: acx / acy as float32
   int32_t* ti;
   int A, RA, T;
 };
@@ -92,6 +93,7 @@ __device__ __forceinline__ DRec bind_rec(uint8_t* base, const cbev_layout& L, co
   r.acx = (double*)(base + L.acx);
   r.acy = (double*)(base + L.acy);
   r.acyaw = (double*)(base + L.acyaw);
+  r.acf = (float*)(base + L.acf);
   r.aix = (double*)(base + L.aix);
   r.aiy = (double*)(base + L.aiy);
   r.arx = (double*)(base + L.arx);

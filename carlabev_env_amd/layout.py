@@ -67,7 +67,7 @@ class CbevCaps(ctypes.Structure):
 class CbevLayout(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int64) for n in (
         "hd", "hi", "cx", "cy", "cyaw", "raw_x", "raw_y", "raw_cum", "vis", "ad", "ai",
-        "acx", "acy", "acyaw", "aix", "aiy", "arx", "ary", "ti", "record_bytes")] + [
+        "acx", "acy", "acyaw", "aix", "aiy", "arx", "ary", "ti", "acf", "record_bytes")] + [
         ("vis_words", ctypes.c_int32), ("pad", ctypes.c_int32)]
 
 
@@ -119,6 +119,7 @@ class Layout:
         for n in ("acx", "acy", "acyaw", "aix", "aiy", "arx", "ary"):
             put(n, 8 * A * RA)
         put("ti", 4 * len(TI) * T)
+        put("acf", 8 * A * RA)  # acx / acy as float32 pairs (the actor target search's first pass)
         return Layout(caps, off, _align(o, 256), vis_words)
 
 
@@ -154,6 +155,7 @@ class RecordView:
         self.arx = v("arx", np.float64, (A, RA))
         self.ary = v("ary", np.float64, (A, RA))
         self.ti = v("ti", np.int32, (len(TI), T))
+        self.acf = v("acf", np.float32, (A, RA, 2))
 
     def h(self, name):
         return self.hd[HD[name]]

@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define CBEV_ABI_VERSION 3
+#define CBEV_ABI_VERSION 4
 
 typedef struct cbev_ctx cbev_ctx;
 

@@ -163,6 +163,8 @@ typedef struct cbev_layout {
   int64_t aix, aiy;                     /* double[A][RA] initial raw route */
   int64_t arx, ary;                     /* double[A][RA] current raw route */
   int64_t ti;                           /* int32[TI][T] */
+  int64_t acf;                          /* float[A][RA][2]: acx / acy rounded to float32,
+                                           the actor target search's first pass */
   int64_t record_bytes;                 /* multiple of 256 */
   int32_t vis_words;
   int32_t pad;
@@ -196,6 +198,7 @@ static inline cbev_layout cbev_make_layout(cbev_caps c) {
   L.arx = o;     o = cbev__align(o + 8 * A * RA, 64);
   L.ary = o;     o = cbev__align(o + 8 * A * RA, 64);
   L.ti = o;      o = cbev__align(o + 4 * (int64_t)CBEV_TI_COUNT * T, 64);
+  L.acf = o;     o = cbev__align(o + 8 * A * RA, 64);
   L.record_bytes = cbev__align(o, 256);
   L.pad = 0;
   return L;

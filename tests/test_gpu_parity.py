@@ -77,6 +77,10 @@ def compare_records(a: np.ndarray, b: np.ndarray, layout, tag=""):
             mk = k if arr in ("arx", "ary") else m
             assert np.allclose(getattr(va, arr)[a, :mk], getattr(vb, arr)[a, :mk], rtol=1e-9, atol=1e-9), (tag, arr, a)
         assert angles_close(va.acyaw[a, :m], vb.acyaw[a, :m]), (tag, "acyaw", a)
+        # a: the device record; its float32 route copy (the target search's first
+        # pass) follows every rebuild of the smoothed route
+        assert np.array_equal(va.acf[a, :m, 0], va.acx[a, :m].astype(np.float32)), (tag, "acf x", a)
+        assert np.array_equal(va.acf[a, :m, 1], va.acy[a, :m].astype(np.float32)), (tag, "acf y", a)
 
 
 def info_of(v, cause):

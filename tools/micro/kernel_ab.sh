@@ -4,7 +4,7 @@ mkdir -p gpurun_out/kab
 export TMPDIR=/tmp
 for so in "$@"; do
   n=$(basename $so .so)
-  CBEV_LIB=$so timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/kab/$n -o run --output-format csv -- python bench.py --steps 50 --warmup 10 --no-cpu-baseline --no-wire --fresh-workers 0 > gpurun_out/kab/$n.log 2>&1 || { echo "$n failed"; tail -5 gpurun_out/kab/$n.log; exit 1; }
+  CBEV_LIB=$so timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/kab/$n -o run --output-format csv -- python bench.py ${BENCH_ARGS:-} --steps 50 --warmup 10 --no-cpu-baseline --no-wire --fresh-workers 0 > gpurun_out/kab/$n.log 2>&1 || { echo "$n failed"; tail -5 gpurun_out/kab/$n.log; exit 1; }
   f=$(find gpurun_out/kab/$n -name "*kernel_stats.csv" | head -1)
   python - "$f" "$n" <<'PY'
 import csv, sys
