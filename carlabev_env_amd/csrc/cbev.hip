@@ -2126,6 +2126,13 @@ void k_raster(
   CBEV_STAMP(2, 0);
   const int e = xcd_env_of_wg(blockIdx.x, n);
   if (e >= n) return;
+#ifdef CBEV_RASTER_STAGGER
+  {  // experiment: offset the first round's resident slots so phases de-synchronise
+    const int slot = (int)blockIdx.x / 256;
+    if (slot < 6)
+      for (int i = 0; i < (slot % CBEV_RASTER_SLOTS) * CBEV_RASTER_STAGGER; ++i) __builtin_amdgcn_s_sleep(8);
+  }
+#endif
   const int64_t SS = (int64_t)K.P.size * K.P.size;
   const DRec r = bind_rec(recs + (int64_t)e * K.L.record_bytes, K.L, K.C);
   RasterJob J;
