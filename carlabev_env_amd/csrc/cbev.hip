@@ -2076,13 +2076,7 @@ __device__ __forceinline__ bool raster8_env(const KArgs& K, uint8_t* rec, const 
   const DRec r = bind_rec(rec, K.L, K.C);
   PaintPre pq{};
   if (PAINT) pq = raster_paint_fetch(r);  // in flight under the staging
-#ifdef CBEV_R8_PRIO
-  __builtin_amdgcn_s_setprio(2);
-#endif
   stage8(K, J, W, lds);
-#ifdef CBEV_R8_PRIO
-  __builtin_amdgcn_s_setprio(0);
-#endif
   __syncthreads();
   if (PAINT) {
     CBEV_STAMP(2, 1);
@@ -2320,35 +2314,21 @@ __global__ __launch_bounds__(256) void k_reset_list(const uint32_t* __restrict__
                                                     const uint8_t* __restrict__ bank,
                                                     const uint8_t* __restrict__ bank_frames, uint8_t* __restrict__ ring,
                                                     KArgs K) {
-  const int pf = reset_pieces(SS), ppe = pf + reset_pieces(rb);
-  // the first piece's list entry and the first 256 list entries (for the rank)
-  // are loaded beside the cursor and the count, before the count is known: the
-  // list holds n entries, so the indices are in bounds and entries past the
-  // count are masked below (one dependent round trip fewer)
-  const int e_first = list[min((int)blockIdx.x / ppe, n - 1)];
-  const int l_first = (int)threadIdx.x < n ? list[threadIdx.x] : 0x7fffffff;
   const unsigned long long cur = *cursor;
   const int cnt = min((int)__builtin_amdgcn_readfirstlane(*count), n);
   asm volatile("" ::"s"(cur), "s"(cnt));  // the cursor loaded beside the count (one wait)
   if (cnt == 0) return;
+  const int pf = reset_pieces(SS), ppe = pf + reset_pieces(rb);
   const int total = cnt * ppe;
   if ((int)blockIdx.x >= total) return;
   for (int p = blockIdx.x; p < total; p += gridDim.x) {
     const int slot = p / ppe, c = p - slot * ppe;
-#ifdef CBEV_RESET_NOPREFETCH
     const int e = list[slot];
-#else
-    const int e = p == (int)blockIdx.x ? e_first : list[slot];
-#endif
     // rank of e among the listed ids (ids are distinct: one append per terminated env)
     int rank = 0;
     for (int j0 = 0; j0 < cnt; j0 += 256) {
       const int j = j0 + (int)threadIdx.x;
-#ifdef CBEV_RESET_NOPREFETCH
       rank += __syncthreads_count(j < cnt && list[j] < e);
-#else
-      rank += __syncthreads_count(j < cnt && (j0 == 0 ? l_first : list[j]) < e);
-#endif
     }
     const int b = (int)((cur + (unsigned long long)rank) % (unsigned long long)n_bank);
     const bool fr = c < pf;  // uniform
