@@ -1115,9 +1115,17 @@ __device__ __forceinline__ int actor_search(const DRec& r, int nact, uint64_t li
 // WIDE: the context's capacities allow more than 64 actors or more than 64
 // actor route points, which take the serial per-lane paths (d_actor_step,
 // d_start_retreat). Contexts within 64 / 64 launch k_actors<false>, which
-// compiles without them: 106 instead of 229 VGPRs, 4 waves per SIMD instead of 2.
+// compiles without them: 134 instead of 246 VGPRs, 3 waves per SIMD instead of 2
+// (asking for 4 waves per SIMD, amdgpu_waves_per_eu(4), still leaves 130 VGPRs
+// and spills 12).
+#ifdef CBEV_ACTORS_WPE
+template <bool WIDE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIDE ? 1 : CBEV_ACTORS_WPE)))
+void k_actors(KArgs K, uint8_t* __restrict__ recs, int n) {
+#else
 template <bool WIDE>
 __global__ __launch_bounds__(256) void k_actors(KArgs K, uint8_t* __restrict__ recs, int n) {
+#endif
   const int lane = threadIdx.x & 63;
   const int e = xcd_env4_of_wg(blockIdx.x, threadIdx.x >> 6, n);
   if (e >= n) return;
@@ -2118,7 +2126,14 @@ __device__ __forceinline__ void raster_reset_env(const KArgs& K, const DRec& r, 
 __host__ __device__ constexpr int raster_threads(int S) { return S >= 256 ? 512 : 256; }
 
 template <int G>
-__global__ __launch_bounds__(raster_threads(64 * G)) __attribute__((amdgpu_waves_per_eu(8)))
+// waves per EU the register allocation targets: the LDS image already caps a CU
+// at 6 workgroups of 4 waves at S <= 128 (2 of 8 at S = 256), so asking for 6
+// instead of 8 costs no residency and leaves the compiler 80 VGPRs: SGPR spills
+// to VGPR lanes 96 -> 59, config 2 24.68 -> 23.99 us, config 3 25.66 -> 24.94
+#ifndef CBEV_RASTER_WPE
+#define CBEV_RASTER_WPE 6
+#endif
+__global__ __launch_bounds__(raster_threads(64 * G)) __attribute__((amdgpu_waves_per_eu(CBEV_RASTER_WPE)))
 void k_raster(
     KArgs K, uint8_t* __restrict__ recs, int n, uint8_t* __restrict__ frames) {
   extern __shared__ __align__(16) uint8_t lds[];
