@@ -1118,14 +1118,8 @@ __device__ __forceinline__ int actor_search(const DRec& r, int nact, uint64_t li
 // compiles without them: 134 instead of 246 VGPRs, 3 waves per SIMD instead of 2
 // (asking for 4 waves per SIMD, amdgpu_waves_per_eu(4), still leaves 130 VGPRs
 // and spills 12).
-#ifdef CBEV_ACTORS_WPE
-template <bool WIDE>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIDE ? 1 : CBEV_ACTORS_WPE)))
-void k_actors(KArgs K, uint8_t* __restrict__ recs, int n) {
-#else
 template <bool WIDE>
 __global__ __launch_bounds__(256) void k_actors(KArgs K, uint8_t* __restrict__ recs, int n) {
-#endif
   const int lane = threadIdx.x & 63;
   const int e = xcd_env4_of_wg(blockIdx.x, threadIdx.x >> 6, n);
   if (e >= n) return;
