@@ -40,14 +40,16 @@ CONFIGS = {
             workload="random traffic (rt_hard_v1, 25 vehicles), 4096 envs/GPU, 128x128 RGB->gray 4-stack"),
     4: dict(envs=8192, size=128, obs_mode="bev_semantic", difficulty="rt_medium_v1", action="continuous_gsb_v1",
             seed0=40_000, act_seed=99, caps=dict(route_cap=64, actor_cap=16, actor_route_cap=64, tl_cap=0),
-            gather=True, workload="rt_medium_v1, continuous, 8192 envs/GPU, RCCL frame gather to rank 0"),
+            gather=True, workload="rt_medium_v1, continuous, 8192 envs/GPU, RCCL frame gather to rank 0",
+            workload_n1="rt_medium_v1, continuous, 8192 envs/GPU (one shard; no gather at N=1)"),
     5: dict(envs=2048, size=256, obs_mode="bev_semantic", difficulty="mix3", action="discrete9_v1",
             seed0=30_000, act_seed=1234, caps=dict(route_cap=64, actor_cap=4, actor_route_cap=64, tl_cap=4),
             workload="lead_brake/jaywalk/red_light_runner mix, 2048 envs/GPU, 256x256 semantic, comfort export"),
 }
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip-level parameters (spec)
-BANK_MIN = 4096  # reset-bank rows at least (the seeded start scenes + more seeded scenes)
+BANK_MIN = 4096  # reset-bank rows at least; the bank holds max(BANK_MIN, 2 n) scenes
+BANK_GID0 = 1_000_000  # bank scenes: global ids 1e6 + rank * B + i, distinct from every start scene (id < 1e6)
 
 
 def log(*a):
@@ -72,50 +74,57 @@ def make_actions(P, n, steps, seed0, offset):
     return out
 
 
-def build_env(cfgd, n, rank, device, info_mode="none", cache=None):
-    """Vector env with every env reset to its seeded scene (host scene-gen)."""
+def env_config(cfgd):
     from carlabev_env_amd.config import EnvConfig
-    from carlabev_env_amd.host_reset import HostResetBuilder
-    from carlabev_env_amd.vector_env import CarlaBEVVectorEnv
-    import torch
     S = cfgd["size"]
     action_mode = "continuous" if cfgd["action"].startswith("continuous") else "discrete"
-    cfg = EnvConfig(size=S, obs_size=(S, S), obs_mode=cfgd["obs_mode"], render_mode="rgb_array",
-                    action_mode=action_mode, action_profile_id=cfgd["action"])
-    env = CarlaBEVVectorEnv({"env": cfg, "num_envs": n}, device=device, caps=cfgd["caps"], info_mode=info_mode)
-    first = rank * n
-    t0 = time.time()
-    # the reset bank: the n seeded scenes the envs start from, then further seeded
-    # scenes up to BANK_MIN rows; terminated envs take its rows in order
-    nb = max(0, BANK_MIN - n)
+    return EnvConfig(size=S, obs_size=(S, S), obs_mode=cfgd["obs_mode"], render_mode="rgb_array",
+                     action_mode=action_mode, action_profile_id=cfgd["action"])
+
+
+def build_scene_sets(cfgd, n, rank, cache=None):
+    """The n seeded start scenes (global ids rank*n + i, scene_seed = seed0 + id)
+    and the reset bank of B = max(BANK_MIN, 2 n) further seeded scenes (global ids
+    BANK_GID0 + rank*B + j: no bank scene is a start scene), built by host worker
+    processes before the GPU is touched (scene generation stays on the host,
+    SURVEY §8). Scenes are a pure function of (config, n, rank): `cache` keeps them
+    across runs on one box."""
+    from carlabev_env_amd import layout as LY
+    from carlabev_env_amd.scene_pool import build_scenes
+    rb = LY.Layout.make(LY.Caps(**cfgd["caps"])).record_bytes
+    B = max(BANK_MIN, 2 * n)
     key = None
-    if cache:  # scenes are a pure function of (config, n, rank): reuse them across runs on one box
+    if cache:
         os.makedirs(cache, exist_ok=True)
-        key = os.path.join(cache, f"cfg{cfgd['seed0']}_{cfgd['difficulty']}_{n}_{rank}_{env.rb}")
-    if key and os.path.exists(key + "_recs.npy"):
-        host = np.load(key + "_recs.npy")
-        bank = np.load(key + "_bank.npy")
-        log(f"[rank {rank}] loaded {n} scenes + {nb} bank scenes from {cache}")
-    else:
-        host = np.zeros((n, env.rb), np.uint8)
-        for i in range(n):
-            gid = first + i
-            opts = dict(scene_options(cfgd, gid), scene_seed=cfgd["seed0"] + gid)
-            env.builder.build(host[i], None, opts)
-        # bank of further seeded scenes for the canonical reset-on-termination loop
-        bank = np.zeros((nb, env.rb), np.uint8)
-        for i in range(nb):
-            gid = 1_000_000 + first + i
-            env.builder.build(bank[i], None, dict(scene_options(cfgd, gid), scene_seed=cfgd["seed0"] + gid))
-        log(f"[rank {rank}] built {n} scenes + {nb} bank scenes in {time.time() - t0:.1f}s")
-        if key:
-            np.save(key + "_recs.npy", host)
-            np.save(key + "_bank.npy", bank)
-    # initial reset: records = seeded scenes (bank rows 0..n-1), reset observation rendered on device
-    env.attach_bank(torch.from_numpy(np.concatenate([host, bank]) if nb else host).to(device))
+        key = os.path.join(cache, f"v4_cfg{cfgd['seed0']}_{cfgd['difficulty']}_{n}_{B}_{rank}_{rb}")
+    if key and os.path.exists(key + "_bank.npy"):
+        log(f"[rank {rank}] loaded {n} start scenes + {B} bank scenes from {cache}")
+        return np.load(key + "_recs.npy"), np.load(key + "_bank.npy")
+    t0 = time.time()
+    workers = max(1, min(16, len(os.sched_getaffinity(0))))
+    args = (env_config(cfgd).model_dump(), cfgd["caps"], cfgd["difficulty"], cfgd["seed0"], rb)
+    host = build_scenes(*args, [rank * n + i for i in range(n)], workers=workers)
+    bank = build_scenes(*args, [BANK_GID0 + rank * B + j for j in range(B)], workers=workers)
+    log(f"[rank {rank}] built {n} start scenes + {B} bank scenes on {workers} workers in {time.time() - t0:.1f}s")
+    if key:
+        np.save(key + "_recs.npy", host)
+        np.save(key + "_bank.npy", bank)
+    return host, bank
+
+
+def build_env(cfgd, n, rank, device, info_mode="full", scenes=None):
+    """Vector env with every env reset to its seeded start scene and the reset
+    bank attached (terminated envs take its rows in order)."""
+    from carlabev_env_amd.vector_env import CarlaBEVVectorEnv
+    import torch
+    host, bank = scenes if scenes is not None else build_scene_sets(cfgd, n, rank)
+    env = CarlaBEVVectorEnv({"env": env_config(cfgd), "num_envs": n}, device=device, caps=cfgd["caps"],
+                            info_mode=info_mode)
+    env.attach_bank(torch.from_numpy(bank).to(device))
     env.auto_obs = False
-    env.reset_from_bank(mask=None, bank_idx=torch.arange(n, dtype=torch.int32, device=device))
-    return env, host
+    start = torch.from_numpy(host).to(device)
+    env.load_scenes(start)
+    return env, host, start
 
 
 def cpu_baseline(cfgd, host_recs, env, seconds):
@@ -363,8 +372,9 @@ def main():
                     help="canonical-loop steps before the timed passes, which all start from the state they leave")
     ap.add_argument("--repeats", type=int, default=5,
                     help="timed passes of exactly --steps steps each (re-seeded between); value = their median")
-    ap.add_argument("--info-mode", default="none", choices=("none", "full"),
-                    help="full: device episode statistics + a StepInfos per step (not read), as step() returns")
+    ap.add_argument("--info-mode", default="full", choices=("none", "full"),
+                    help="full (default, as the reference's step() always runs Stats.step, carlabev.py:226-227): "
+                         "device episode statistics + a StepInfos per step (not read); none: statistics off")
     args = ap.parse_args()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -379,6 +389,7 @@ def main():
 
     cfgd = CONFIGS[args.config]
     n = args.envs or cfgd["envs"]
+    scenes = build_scene_sets(cfgd, n, rank, args.scene_cache)  # host workers, before the GPU is touched
     pool = None
     if args.fresh_workers > 0:  # spawned before this process touches the GPU
         pool = start_scene_pool(cfgd, args.fresh_workers, rank, world)
@@ -390,7 +401,8 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=device)
     from carlabev_env_amd._lib import check, lib
-    env, host_recs = build_env(cfgd, n, rank, device, args.info_mode, args.scene_cache)
+    env, host_recs, start_recs = build_env(cfgd, n, rank, device, args.info_mode, scenes)
+    del scenes
     P = env.params
     total_steps = args.warmup + args.steps
     burn = max(0, args.burn_in)
@@ -410,7 +422,7 @@ def main():
         env.step_infos()
         if gatherer is not None:  # config 4: frames + reward/cause/flags of every rank to rank 0, one RCCL gather
             gatherer.gather(env.frames(), env.reward, env.term, env.trunc, env.cause)
-        env.reset_from_bank(mask=env.term)  # canonical loop: reset(reset_mask=terminated)
+        env.reset_terminated()  # canonical loop: reset(reset_mask=terminated), next bank rows
         if wire:
             env._obs()
 
@@ -445,12 +457,11 @@ def main():
             ms3 = [buf[i] / max(cnt.value, 1) for i in range(3)]
         return el, ms3, host_enqueue
 
-    start_idx = torch.arange(n, dtype=torch.int32, device=device)
     snap = {}
 
     def reseed():  # back to the steady-state snapshot, so every pass replays a comparable workload
-        if not snap:  # before the burn-in: the seeded start scenes (bank rows 0..n-1)
-            env.reset_from_bank(mask=None, bank_idx=start_idx)
+        if not snap:  # before the burn-in: the seeded start scenes
+            env.load_scenes(start_recs)
             return
         env.records.copy_(snap["records"])
         env.ring.copy_(snap["ring"])
@@ -461,11 +472,11 @@ def main():
         snapshot of every env's state and frame stack: the timed passes start from
         episodes of mixed ages (the steady-state termination and reset rate of the
         loop) instead of all envs at step 0 of their first episode."""
-        env.reset_from_bank(mask=None, bank_idx=start_idx)
+        env.load_scenes(start_recs)
         term0 = env.termination_count()
         for t in range(burn):
             env.step_async_only(acts_all[t])
-            env.reset_from_bank(mask=env.term)
+            env.reset_terminated()
         torch.cuda.synchronize()
         snap["records"] = env.records.clone()
         snap["ring"] = env.ring.clone()
@@ -486,10 +497,12 @@ def main():
         burn_resets = burn_in() if burn else 0
         passes = []
         term0 = env.termination_count()
+        rows0 = env.bank_rows_used()
         for _ in range(max(1, args.repeats)):  # headline passes, no instrumentation
             reseed()
             passes.append(timed(False, False))
         pass_resets = env.termination_count() - term0
+        pass_rows = env.bank_rows_used() - rows0
         els = sorted(p[0] for p in passes)
         el = els[len(els) // 2]
         host_enq = sorted(p[2] for p in passes)[len(els) // 2]
@@ -522,13 +535,23 @@ def main():
     algo_bytes = 2 * S * S + 64
     raster_ms = burst_ms if burst_ms is not None else ms3[2]
     achieved = n * algo_bytes / (raster_ms * 1e-3) / 1e9
-    traffic = None
+    traffic = write_bytes = None
     pmc_path = os.path.join(REPO, "profiles", f"pmc_raster_config{args.config}.json")
     if os.path.exists(pmc_path):
         with open(pmc_path) as f:
             pmc = json.load(f)
         if pmc.get("envs") == n:
             traffic = pmc.get("hbm_bytes_per_launch")
+            write_bytes = pmc.get("write_kb", 0.0) * 1024
+    t_s = raster_ms * 1e-3
+    frame_bytes = n * S * S
+    counter_fields = {
+        # counter-measured DRAM rates of the same launch time (profiles/pmc_raster_config*.json)
+        "write_frac_measured": None if write_bytes is None else round(write_bytes / t_s / 1e9 / peak["write_gbs"], 4),
+        "hbm_counter_frac": None if traffic is None else round(traffic / t_s / 1e9 / HBM_PEAK_GBS, 4),
+        # kernel time over the time this box's fill_ needs for the frame bytes alone
+        "write_floor_ratio": round(t_s / (frame_bytes / (peak["write_gbs"] * 1e9)), 3),
+    }
     cpu = None
     if rank == 0 and not args.no_cpu_baseline and world == 1:
         cpu = cpu_baseline(cfgd, host_recs, env, args.cpu_seconds)
@@ -547,7 +570,8 @@ def main():
             "dtype": "f64 state / u8 frames",
             "data": "synthetic seeded scenes (host scene-gen on the Town01 class map), seeded action streams",
             "info_mode": args.info_mode,
-            "config": {"workload": cfgd["workload"], "config_id": args.config, "envs_per_gpu": n,
+            "config": {"workload": cfgd["workload"] if gather or "workload_n1" not in cfgd else cfgd["workload_n1"],
+                       "config_id": args.config, "envs_per_gpu": n,
                        "global_envs": n * world, "obs_size": S, "obs_mode": cfgd["obs_mode"],
                        "parallelism": f"env-sharded x{world}" + (" + RCCL gather" if gather else "")},
             "repeats": len(els),
@@ -559,8 +583,11 @@ def main():
                                      f"passes (warmup + timed steps), from a snapshot taken after {burn} burn-in "
                                      f"steps ({burn_resets} resets)"),
             "bank_scenes": int(env.bank.shape[0]),
-            # resets take bank rows in order (cursor), so any run of up to B consecutive resets is all distinct
-            "distinct_scenes_per_1k_resets": min(1000, int(env.bank.shape[0])),
+            "bank_scene_ids": (f"{BANK_GID0} + rank*{int(env.bank.shape[0])} + j: seeded scenes distinct from the "
+                               f"{n} start scenes (ids rank*{n} + i)"),
+            # the device cursor's advance over the headline passes: every reset took the next bank row
+            "bank_rows_handed_out": pass_rows,
+            "distinct_bank_rows_handed_out": min(pass_rows, int(env.bank.shape[0])),
             "host_enqueue_ms_per_step": round(host_enq / args.steps * 1e3, 4),
             "ms_per_step_with_kernel_events": round(el_prof / args.steps * 1e3, 4),
             # per-step HIP-event spans; with no actor slots (config 2) k_actors is not launched and
@@ -570,8 +597,7 @@ def main():
             "raster_ms_per_launch": None if burst_ms is None else round(burst_ms, 5),
             "roofline": {"bound": "hbm", "kernel": "k_raster", "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "peak_measured": peak,
-                         "frac_of_measured_write": round(achieved / peak["write_gbs"], 4),
+                         "peak_measured": peak, **counter_fields,
                          "traffic": traffic, "algorithmic_bytes_per_env": algo_bytes,
                          "timing": (f"HIP events around {args.raster_reps} back-to-back launches on the step stream"
                                     if burst_ms is not None else "HIP events around each launch in the timed steps"),

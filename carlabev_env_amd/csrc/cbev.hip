@@ -533,55 +533,15 @@ __device__ __forceinline__ void d_crop_origin(const cbev_params& P, double x, do
 // rect_from_world_center (transforms.py:46-51): centre rounded half-even, x = c - w/2
 __device__ __forceinline__ int d_rect_lo(double w, int pad, int size) { return (int)rint((double)pad + w * 1.0) - size / 2; }
 
-// LDS images of the crop. Two:
-//  * nibble image of the whole crop (every S; the only one at S = 256):
-//    nibble-packed like the map, crop row r starts at dword r * sd and holds the
-//    packed map bytes from xa = (xmin >> 1) & ~3 on, so crop pixel (c, r) is
-//    "nibble address" r * 8 sd + shift + c (shift = xmin - 2 xa, 0..7): byte >> 1
-//    of it, high nibble when odd; sd = the dwords a row needs (7 + C nibbles),
-//    rounded up to odd. 363 x 47 dwords = 68 KB at S=256, 182 x 25 = 18 KB at
-//    S=128; 7.5 VALU instructions per output pixel (address, nibble select).
-//  * byte window (S <= 128, raster8_* below): one palette id per byte, only the
-//    texels the output samples; 3.75 VALU instructions per pixel.
-// The raster is VALU-issue-bound (round 3 PMC: SQ_INSTS_VALU x 4 cycles ~ the
-// launch on every SIMD), hence the byte window wherever it fits.
-// the byte-window path (below, raster8_*) serves S <= 128
-__host__ __device__ constexpr bool raster_win8(int S) {
-#ifdef CBEV_RASTER_NIBBLE
-  return false;
-#else
-  return S <= 128;
-#endif
-}
+// The raster's crop geometry (k_raster, below): rotate90's texel-address steps
+// (RS_A00 / RS_USTEP / RS_VSTEP in the record) use this row stride; the raster
+// turns them back into 16.16 steps (raster8_affine).
 __host__ __device__ __forceinline__ int raster_stride_dwords(int S, int C) {
   return ((C + 7 + 7) / 8) | 1;
 }
-// texels per LDS row (the row stride of texel addresses)
 __host__ __device__ __forceinline__ int raster_row_texels(int S, int C) {
   return 8 * raster_stride_dwords(S, C);
 }
-// 16-byte chunks of the (byte or packed) map per staged row: 16 or 32 texels each
-__host__ __device__ __forceinline__ int raster_row_chunks(int S, int C) {
-  return ((C + 7 + 7) / 8 + 3) / 4;
-}
-// 16 bytes at 4-byte alignment (crop rows start at a dword of the map)
-typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
-__device__ __forceinline__ uint4 load16_a4(const uint8_t* p) {
-  const u32x4_a4 t = *(const u32x4_a4*)p;
-  return make_uint4(t.x, t.y, t.z, t.w);
-}
-// texel-level helpers on the LDS image (texel address ta)
-__device__ __forceinline__ uint32_t lds_texel(const uint8_t* lds, uint32_t ta) {
-  return (lds[ta >> 1] >> ((ta & 1u) << 2)) & 15u;
-}
-__device__ __forceinline__ void lds_set_texel(uint8_t* lds, uint32_t ta, uint32_t col) {
-  uint32_t* w = (uint32_t*)lds + (ta >> 3);
-  const uint32_t sh = (ta & 7u) << 2;
-  atomicAnd(w, ~(15u << sh));
-  atomicOr(w, col << sh);
-}
-// + one spare dword after the image (the nibble staging's overhang writes land there)
-__host__ __device__ __forceinline__ int raster_image_bytes(int S, int C);
 
 // Per-env rotation parameters (pygame transform.rotate, 16.16 fixed point;
 // rotate90 for exact multiples of 90 degrees) and the compose placement.
@@ -978,11 +938,8 @@ __device__ __forceinline__ void hero_env_render_setup(const KArgs& K, DRec r) {
 // More than 64 actors: d_actor_step per lane.
 // calc_target_index of every live actor of one env (nact <= 64): AW lanes per
 // actor, 64 / AW actors per round; returns lane a's result for actor a
-#ifdef CBEV_ACTOR_F64_ONLY  // A/B switch: the float64 scan alone
-constexpr bool kActorF32 = false;
-#else
+// the float32 first pass (false: the float64 scan alone, tools/micro/actor_f64_only.patch)
 constexpr bool kActorF32 = true;
-#endif
 constexpr int ACTOR_BATCH = 8;  // route points per lane loaded at once in the target search
 template <int AW>
 __device__ __forceinline__ int actor_search(const DRec& r, int nact, uint64_t livem, double fx, double fy, int nrt,
@@ -1245,279 +1202,63 @@ __global__ __launch_bounds__(256) void k_actors(KArgs K, uint8_t* __restrict__ r
 }
 
 
-// The output pass at S=256 (measured faster there: 62 vs 68 us per launch at
-// config 5; the 16-byte-store pass below wins at S=128): over one wave's chunks
-// of 1024 output pixels (16 / G rows), a chunk is four 256-pixel dword groups: in group d lane l owns the 4
-// consecutive output pixels 256 d + 4 l .. + 3 of the chunk (row r + d (4 / G)
-// + l / (16 G), columns 4 (l % (16 G)) .. + 3), gathers them one column step
-// apart and packs them into one dword, so each group is ONE 256-byte dword
-// store. Source coordinates are stepped, not recomputed (pygame's rotozoom is
-// affine in the output pixel): per gather one 64-bit add, a 24-bit
-// multiply-add for the LDS byte address, the LDS read, the nibble extract and
-// the pack.
-//   CHECK = false: the rotated surface covers the whole output and every output
-//   pixel samples inside the crop (checked once per env at the four corners;
-//   the map is affine) -> no per-pixel tests.
-//   CHECK = true: compose clipping (black outside the rotated surface) and the
-//   rotozoom background test (bg outside the source), per pixel.
-template <int G, bool R90, bool CHECK, int NW>
-__device__ __forceinline__ void raster_out4(const cbev_params& P, const RotSetup& R, const uint8_t* __restrict__ lds,
-                                           int shift, uint32_t bg, uint8_t* __restrict__ out, int nout,
-                                           int64_t out_stride, int lane, int wave,
-                                           const uint32_t* __restrict__ fov) {
-  constexpr int RPC = 16 / G;  // output rows per chunk
-  constexpr int S = 64 * G;    // == P.size
-  constexpr int LPR = S / 4;   // lanes per output row
-  constexpr int RPD = 4 / G;   // output rows per dword group
-  const int C = P.crop;
-  const uint32_t vmax = (uint32_t)((C << 16) - 1);
-  const int hero_w = P.hero_w;
-  const int hx0 = P.anchor_x - hero_w / 2, hy0 = P.anchor_y - hero_w / 2;
-  const int lrow = lane / LPR, lcol = 4 * (lane % LPR);
-  // this lane's columns: hero byte mask (Hero.draw: black w x w rect at the
-  // anchor, hero.py:26-32) and the compose-clip column test
-  uint32_t hmask = 0, xok = 0;
-#pragma unroll
-  for (int b = 0; b < 4; ++b) {
-    const int u = lcol + b;
-    if (u >= hx0 && u < hx0 + hero_w) hmask |= 0xffu << (8 * b);
-    const int xx = u - R.rx0;
-    if (xx >= 0 && xx < R.nx) xok |= 1u << b;
-  }
-  const uint32_t hblack = hmask & (CBEV_PX_BLACK * 0x01010101u);
-  const int r0 = wave * RPC;
-  const int xx0 = lcol - R.rx0, yy0 = r0 + lrow - R.ry0;
-  // lane state at (output row r0 + lrow, column lcol) of this wave's first chunk
-  int sx = R.dx00 + xx0 * R.icos - yy0 * R.isin;  // 16.16 source x (general)
-  int sy = R.dy00 + xx0 * R.isin + yy0 * R.icos;  // 16.16 source y (general)
-  int sa = R.a00 + shift + xx0 * R.ustep + yy0 * R.vstep;  // LDS texel address (rotate90)
-  // the crop's texel offset rides in the integer part of sx, so the LDS byte is
-  // (sy >> 16) * sb + (sx >> 17) with the nibble (sx >> 16) & 1
-  sx += shift << 16;
-  const uint8_t* img = lds;
-  const uint32_t sb = 4u * (uint32_t)raster_stride_dwords(S, C);  // LDS bytes per crop row
-  const int chunk_rows = NW * RPC;                // the NW output waves interleave chunks
-  const int nchunks = S / RPC;
-  // general path: (sx, sy) packed in one 64-bit value, so one 64-bit add steps
-  // both coordinates (the low word stays in [0, 2^32): no carry crosses over)
-  uint64_t pxy = ((uint64_t)(uint32_t)sy << 32) | (uint32_t)sx;
-  const uint64_t chunk_step =
-      (uint64_t)(((int64_t)(chunk_rows * R.icos) << 32) + (int64_t)(-chunk_rows * R.isin));
-  // one output row down: (dx, dy) += (-isin, icos); one column right: += (icos, isin)
-  const uint64_t group_step = (uint64_t)(((int64_t)(RPD * R.icos) << 32) + (int64_t)(-RPD * R.isin));
-  const uint64_t col_step = (uint64_t)(((int64_t)R.isin << 32) + (int64_t)R.icos);
-  for (int ch = wave, r = r0; ch < nchunks; ch += NW, r += chunk_rows) {
-    // the frame is written through the uniform base `out` plus a per-lane offset
-    const uint32_t vo = (uint32_t)(r * S + 4 * lane);
-    const bool hero_rows = (unsigned)(r + RPC - 1 - hy0) < (unsigned)(RPC - 1 + hero_w);  // chunk meets the hero rows
-    asm volatile("" : "+v"(pxy), "+v"(sa));  // keep the per-gather offsets as scalar adds
-    uint32_t w[4];
-    uint64_t qg = pxy;  // general path: source coordinates of (row r + d RPD + lrow, column lcol)
-#pragma unroll
-    for (int d = 0; d < 4; ++d) {
-      uint32_t acc = 0;
-#pragma unroll
-      for (int b = 0; b < 4; ++b) {
-        uint32_t v;
-        if (R90) {
-          const int a = sa + d * RPD * R.vstep + b * R.ustep;
-          if (CHECK) {
-            const bool ok = ((xok >> b) & 1u) && (unsigned)(r + d * RPD + lrow - R.ry0) < (unsigned)R.ny;
-            v = ok ? lds_texel(img, ok ? a : 0) : (uint32_t)CBEV_PX_BLACK;
-          } else {
-            v = lds_texel(img, a);
-          }
-        } else {
-          const uint64_t q = b == 0 ? qg : qg + (uint64_t)b * col_step;
-          const uint32_t dx = (uint32_t)q, dy = (uint32_t)(q >> 32);
-          const uint32_t byte = __umul24(dy >> 16, sb) + (dx >> 17);
-          const uint32_t nsh = (dx >> 14) & 4u;
-          if (CHECK) {  // bounds on the unshifted source coordinate
-            const int ux = (int)dx - (shift << 16);
-            const bool ok = ((xok >> b) & 1u) && (unsigned)(r + d * RPD + lrow - R.ry0) < (unsigned)R.ny;
-            const bool in = (uint32_t)ux <= vmax && dy <= vmax;
-            const uint32_t s = (img[(in && ok) ? byte : 0u] >> nsh) & 15u;
-            v = !ok ? (uint32_t)CBEV_PX_BLACK : (in ? s : bg);
-          } else {
-            v = (img[byte] >> nsh) & 15u;
-          }
-        }
-        acc |= v << (8 * b);
-      }
-      w[d] = acc;
-      if (!R90) qg += group_step;
-    }
-    if (hero_rows) {
-#pragma unroll
-      for (int d = 0; d < 4; ++d)
-        if ((unsigned)(r + d * RPD + lrow - hy0) < (unsigned)hero_w) w[d] = (w[d] & ~hmask) | hblack;
-    }
-    if (fov) {  // FovRenderer.apply_mask (fov.py:96-99): black corner triangles (uniform branch)
-#pragma unroll
-      for (int d = 0; d < 4; ++d) {
-        const uint32_t fm = fov[(vo >> 2) + 64 * d];
-        w[d] = (w[d] & ~fm) | (fm & (CBEV_PX_BLACK * 0x01010101u));
-      }
-    }
-    for (int k = 0; k < nout; ++k) {
-      uint8_t* ob = out + (int64_t)k * out_stride;
-#pragma unroll
-      for (int d = 0; d < 4; ++d)  // streamed out: keep the L2 for the map and the records
-        __builtin_nontemporal_store(w[d], (uint32_t*)(ob + (vo + (uint32_t)(256 * d))));
-    }
-    pxy += chunk_step;
-    sa += chunk_rows * R.vstep;
-  }
+// ====================================================== k_raster: the tile raster
+// The S x S observation is cut into tiles of TC = min(S, 128) columns x TR
+// rows, and one 256-thread workgroup renders one (env, tile): it stages the
+// byte window of the crop its tile samples, paints the actors / visible
+// targets / traffic lights that fall into it in the reference's draw order,
+// and writes the tile (rotate + compose + ego overlay + FOV mask). pygame's
+// rotozoom is affine in the output pixel, so the texels a tile samples lie in
+// the bounding box of its four corners' samples: the window is that box, one
+// palette id per byte. Roads are axis-aligned and a tile's box is small at
+// every heading (at most 22.7 KB for 128 x 64 tiles, 38.4 KB for 128 x 128,
+// Tiles::lds_bytes), so every heading takes the byte gathers.
+//
+// Orientation: a wave's gathers are 16 output pixels apart along an output row
+// (lane l owns 16 consecutive pixels of row l / 8). When the output rows run
+// along the crop's columns (|sin| > |cos|), lanes 16 pixels apart read crop
+// rows 16 apart, whose bytes share LDS banks (4-way conflicts on the byte
+// reads in the round-3 window). Such tiles stage the window transposed from a
+// transposed copy of the byte map (map8T, built once by cbev_set_map: a plain
+// 16-byte copy, no in-kernel transposition): window rows are then crop
+// columns, the (x, y) roles of the 16.16 sample coordinates swap, and the
+// gathers again step along window rows at every heading.
+__host__ __device__ constexpr int tile_cols(int S) { return S < 128 ? S : 128; }
+// tile rows per size (S = 64, 128, 256)
+__host__ __device__ constexpr int tile_rows(int S) { return S <= 64 ? 64 : S == 128 ? 128 : 64; }
+template <int G>
+struct Tiles {
+  static constexpr int S = 64 * G;
+  static constexpr int TC = tile_cols(S), TR = tile_rows(S);
+  static constexpr int NTX = S / TC, NTY = S / TR, T = NTX * NTY;  // tiles per env
+  static constexpr int LPR = TC / 16;                              // lanes per output row
+  static constexpr int RPC = 64 / LPR;                             // output rows per wave chunk
+  static constexpr int NCH = TR / RPC;                             // chunks per tile (dealt over 4 waves)
+  // window bound over every heading (TC - 1 and TR - 1 sample steps of the
+  // rotated unit vectors, + 2 texels of floor spread, + the 16-byte chunk
+  // rounding at a column offset of up to 3): tools/tile_window_bound.py
+  static constexpr int lds_bytes = TC == 64 ? 10560 : TR == 64 ? 22688 : 38384;
+  static constexpr int wgs_per_cu = 163840 / lds_bytes > 8 ? 8 : 163840 / lds_bytes;
+};
+
+// rotate90 (exact multiples of 90 degrees: pygame's rotate90 transposes) as the
+// affine map it is: k_ego's texel steps (+-1 column or +-rt = a row, per output
+// column / row) become 16.16 steps of +-65536 with sin / cos in {0, +-1}, and the
+// start texel's coordinates sit at +0x8000, so every sample floors to the exact
+// texel and rotate90 takes the general gather.
+__device__ __forceinline__ void raster8_affine(RotSetup& R, int rt) {
+  if (!R.r90) return;
+  const int ar = R.a00 / rt, ac = R.a00 - ar * rt;
+  // output column step = (icos, isin) in (column, row); the row step is (-isin, icos)
+  R.icos = R.ustep == 1 ? 65536 : R.ustep == -1 ? -65536 : 0;
+  R.isin = R.ustep == rt ? 65536 : R.ustep == -rt ? -65536 : 0;
+  R.dx00 = (ac << 16) + 0x8000;
+  R.dy00 = (ar << 16) + 0x8000;
+  R.r90 = 0;
 }
 
-// Output pass over one wave's chunks of 1024 output pixels (16 / G rows). In a
-// chunk lane l owns the 16 consecutive pixels of row r + l / (4 G), columns
-// 16 (l % (4 G)) .. + 15: it gathers them one column step apart, packs them into
-// four dwords and writes them with ONE 16-byte store, so a chunk is one
-// 1 KiB wave store (the stores are issue-bound per instruction, not per byte).
-// Source coordinates are stepped, not recomputed (pygame's rotozoom is affine
-// in the output pixel): per gather one 64-bit add, a 24-bit multiply-add for
-// the LDS byte address, the LDS read, the nibble extract and the pack.
-//   CHECK = false: the rotated surface covers the whole output and every output
-//   pixel samples inside the crop (checked once per env at the four corners;
-//   the map is affine) -> no per-pixel tests.
-//   CHECK = true: compose clipping (black outside the rotated surface) and the
-//   rotozoom background test (bg outside the source), per pixel.
-typedef uint32_t u32x4_nt __attribute__((ext_vector_type(4)));
-template <int G, bool R90, bool CHECK, int NW>
-__device__ __forceinline__ void raster_out(const cbev_params& P, const RotSetup& R, const uint8_t* __restrict__ lds,
-                                           int shift, uint32_t bg, uint8_t* __restrict__ out, int nout,
-                                           int64_t out_stride, int lane, int wave,
-                                           const uint32_t* __restrict__ fov) {
-  constexpr int S = 64 * G;     // == P.size
-  constexpr int LPR = S / 16;   // lanes per output row
-  constexpr int RPC = 64 / LPR; // output rows per chunk
-  const int C = P.crop;
-  const uint32_t vmax = (uint32_t)((C << 16) - 1);
-  const int hero_w = P.hero_w;
-  const int hx0 = P.anchor_x - hero_w / 2, hy0 = P.anchor_y - hero_w / 2;
-  const int lrow = lane / LPR, lcol = 16 * (lane % LPR);
-  // this lane's columns: hero byte masks (Hero.draw: black w x w rect at the
-  // anchor, hero.py:26-32) and the compose-clip column test
-  uint32_t hmask[4] = {0u, 0u, 0u, 0u}, xok = 0;
-#pragma unroll
-  for (int b = 0; b < 16; ++b) {
-    const int u = lcol + b;
-    if (u >= hx0 && u < hx0 + hero_w) hmask[b >> 2] |= 0xffu << (8 * (b & 3));
-    const int xx = u - R.rx0;
-    if (xx >= 0 && xx < R.nx) xok |= 1u << b;
-  }
-  const int r0 = wave * RPC;
-  const int xx0 = lcol - R.rx0, yy0 = r0 + lrow - R.ry0;
-  // lane state at (output row r0 + lrow, column lcol) of this wave's first chunk
-  int sx = R.dx00 + xx0 * R.icos - yy0 * R.isin;  // 16.16 source x (general)
-  int sy = R.dy00 + xx0 * R.isin + yy0 * R.icos;  // 16.16 source y (general)
-  int sa = R.a00 + shift + xx0 * R.ustep + yy0 * R.vstep;  // LDS texel address (rotate90)
-  // the crop's texel offset rides in the integer part of sx, so the LDS byte is
-  // (sy >> 16) * sb + (sx >> 17) with the nibble (sx >> 16) & 1
-  sx += shift << 16;
-  const uint8_t* img = lds;
-  const uint32_t sb = 4u * (uint32_t)raster_stride_dwords(S, C);  // LDS bytes per crop row
-  const int chunk_rows = NW * RPC;                // the NW output waves interleave chunks
-  const int nchunks = S / RPC;
-  // general path: (sx, sy) packed in one 64-bit value, so one 64-bit add steps
-  // both coordinates (the low word stays in [0, 2^32): no carry crosses over)
-  uint64_t pxy = ((uint64_t)(uint32_t)sy << 32) | (uint32_t)sx;
-  const uint64_t chunk_step =
-      (uint64_t)(((int64_t)(chunk_rows * R.icos) << 32) + (int64_t)(-chunk_rows * R.isin));
-  // one column right: (dx, dy) += (icos, isin)
-  const uint64_t col_step = (uint64_t)(((int64_t)R.isin << 32) + (int64_t)R.icos);
-  for (int ch = wave, r = r0; ch < nchunks; ch += NW, r += chunk_rows) {
-    const int row = r + lrow;
-    // the frame is written through the uniform base `out` plus a per-lane offset
-    const uint32_t vo = (uint32_t)(row * S + lcol);
-    asm volatile("" : "+v"(pxy), "+v"(sa));  // keep the per-gather offsets as scalar adds
-    const bool rok = !CHECK || (unsigned)(row - R.ry0) < (unsigned)R.ny;
-    uint32_t w[4];
-#pragma unroll
-    for (int d = 0; d < 4; ++d) {
-      uint32_t acc = 0;
-#pragma unroll
-      for (int bb = 0; bb < 4; ++bb) {
-        const int b = 4 * d + bb;
-        uint32_t v;
-        if (R90) {
-          const int a = sa + b * R.ustep;
-          if (CHECK) {
-            const bool ok = ((xok >> b) & 1u) && rok;
-            v = ok ? lds_texel(img, ok ? a : 0) : (uint32_t)CBEV_PX_BLACK;
-          } else {
-            v = lds_texel(img, a);
-          }
-        } else {
-          const uint64_t q = pxy + (uint64_t)b * col_step;
-          const uint32_t dx = (uint32_t)q, dy = (uint32_t)(q >> 32);
-          const uint32_t byte = __umul24(dy >> 16, sb) + (dx >> 17);
-          const uint32_t nsh = (dx >> 14) & 4u;
-          if (CHECK) {  // bounds on the unshifted source coordinate
-            const int ux = (int)dx - (shift << 16);
-            const bool ok = ((xok >> b) & 1u) && rok;
-            const bool in = (uint32_t)ux <= vmax && dy <= vmax;
-            const uint32_t s = (img[(in && ok) ? byte : 0u] >> nsh) & 15u;
-            v = !ok ? (uint32_t)CBEV_PX_BLACK : (in ? s : bg);
-          } else {
-            v = (img[byte] >> nsh) & 15u;
-          }
-        }
-        acc |= v << (8 * bb);
-      }
-      w[d] = acc;
-    }
-    if ((unsigned)(row - hy0) < (unsigned)hero_w) {
-#pragma unroll
-      for (int d = 0; d < 4; ++d) w[d] = (w[d] & ~hmask[d]) | (hmask[d] & (CBEV_PX_BLACK * 0x01010101u));
-    }
-    if (fov) {  // FovRenderer.apply_mask (fov.py:96-99): black corner triangles (uniform branch)
-      const uint4 fm = *(const uint4*)(fov + (vo >> 2));
-      w[0] = (w[0] & ~fm.x) | (fm.x & (CBEV_PX_BLACK * 0x01010101u));
-      w[1] = (w[1] & ~fm.y) | (fm.y & (CBEV_PX_BLACK * 0x01010101u));
-      w[2] = (w[2] & ~fm.z) | (fm.z & (CBEV_PX_BLACK * 0x01010101u));
-      w[3] = (w[3] & ~fm.w) | (fm.w & (CBEV_PX_BLACK * 0x01010101u));
-    }
-    const u32x4_nt v4 = {w[0], w[1], w[2], w[3]};
-    for (int k = 0; k < nout; ++k)  // streamed out: keep the L2 for the map and the records
-      __builtin_nontemporal_store(v4, (u32x4_nt*)(out + (int64_t)k * out_stride + vo));
-    pxy += chunk_step;
-    sa += chunk_rows * R.vstep;
-  }
-}
-
-template <int G, int NW = 4>
-__device__ __forceinline__ void raster_out_dispatch(const cbev_params& P, const RotSetup& R, bool fast,
-                                                    const uint8_t* lds, int shift, uint32_t bg, uint8_t* out, int nout,
-                                                    int64_t out_stride, int lane, int wave, const uint32_t* fov) {
-  if (G >= 4) {
-    if (R.r90) {
-      if (fast) raster_out4<G, true, false, NW>(P, R, lds, shift, bg, out, nout, out_stride, lane, wave, fov);
-      else      raster_out4<G, true, true, NW>(P, R, lds, shift, bg, out, nout, out_stride, lane, wave, fov);
-    } else {
-      if (fast) raster_out4<G, false, false, NW>(P, R, lds, shift, bg, out, nout, out_stride, lane, wave, fov);
-      else      raster_out4<G, false, true, NW>(P, R, lds, shift, bg, out, nout, out_stride, lane, wave, fov);
-    }
-    return;
-  }
-  if (R.r90) {
-    if (fast) raster_out<G, true, false, NW>(P, R, lds, shift, bg, out, nout, out_stride, lane, wave, fov);
-    else      raster_out<G, true, true, NW>(P, R, lds, shift, bg, out, nout, out_stride, lane, wave, fov);
-  } else {
-    if (fast) raster_out<G, false, false, NW>(P, R, lds, shift, bg, out, nout, out_stride, lane, wave, fov);
-    else      raster_out<G, false, true, NW>(P, R, lds, shift, bg, out, nout, out_stride, lane, wave, fov);
-  }
-}
-
-// Render one env's observation (whole 256-thread workgroup). RESET: BaseMap.reset's
-// frame (theta = 0, no actors drawn, world.py:92-100). The frame is written to
-// `nout` destinations out + k*out_stride (the frame-stack ring on reset).
-// Paint actors / visible targets / traffic lights into the LDS crop in the
-// reference's draw order (scene.py:93-95, actor_manager.py:121-132): vehicles,
-// pedestrians, visible targets, traffic lights, later wins. Four threads per
-// rect (actor or target tid >> 2); their record fields are fetched into
-// registers before the crop staging, so the loads' latency hides under it.
+// Paint inputs fetched before the staging, so their loads' latency hides under
+// it: four threads per rect (actor or target tid >> 2).
 struct PaintPre {
   int nact, nveh, nt, ntl;
   double ax, ay;  // actor tid >> 2
@@ -1549,272 +1290,59 @@ __device__ __forceinline__ PaintPre raster_paint_fetch(const DRec& r) {
   return q;
 }
 
-// one rect of side sz (rect_from_world_center, transforms.py:46-51) by the 4
-// threads of tid >> 2: thread tq covers rows tq, tq + 4, ..., each row's span
-// clipped to the crop, written a whole LDS dword (8 texels) at a time, one and-mask + or-colour pair per dword
-// it touches. Every rect of a paint pass has the same colour, so overlapping
-// rects commute; rows of an LDS image are dword-aligned.
-__device__ __forceinline__ void paint_rect4(uint8_t* lds, int rt, int shift, int C, int pad, int xmin, int ymin,
-                                            double wx, double wy, int sz, int tq, uint32_t col) {
-  const int rx = d_rect_lo(wx, pad, sz) - xmin, ry = d_rect_lo(wy, pad, sz) - ymin;
-  const int x0 = rx > 0 ? rx : 0, x1 = rx + sz < C ? rx + sz : C;
-  if (x0 >= x1) return;
-  uint32_t* l32 = (uint32_t*)lds;
-  const uint32_t colw = col * 0x11111111u;
-  for (int qy = tq; qy < sz; qy += 4) {
-    const int py = ry + qy;
-    if (py < 0 || py >= C) continue;
-    const uint32_t t0 = (uint32_t)(py * rt + shift + x0), t1 = (uint32_t)(py * rt + shift + x1);
-    for (uint32_t w = t0 >> 3; w <= (t1 - 1) >> 3; ++w) {
-      const uint32_t lo = t0 > 8 * w ? t0 - 8 * w : 0u, hi = t1 < 8 * w + 8 ? t1 - 8 * w : 8u;  // nibbles [lo, hi)
-      const uint32_t m = (hi - lo == 8u ? 0xffffffffu : ((1u << (4u * (hi - lo))) - 1u)) << (4u * lo);
-      atomicAnd(l32 + w, ~m);
-      atomicOr(l32 + w, colw & m);
-    }
-  }
-}
-
-// workgroup barrier for LDS-only hand-offs: LDS operations retired, no vmcnt
-// wait, so LDS-DMA (k_raster's next crop image) stays in flight across it
+// workgroup barrier for LDS-only hand-offs: LDS operations retired, no vmcnt wait
 __device__ __forceinline__ void lds_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
-template <int G, int NT = 256>
-__device__ __forceinline__ void raster_paint(const KArgs& K, const DRec& r, const PaintPre& q, int xmin, int ymin,
-                                             int shift, uint8_t* __restrict__ lds) {
-  const cbev_params& P = K.P;
-  const int C = P.crop;
-  const int rt = raster_row_texels(P.size, C);  // texels per LDS row
-  const int k = threadIdx.x >> 2, tq = threadIdx.x & 3;
-  {
-    for (int pass = 0; pass < 2; ++pass) {  // vehicles, then pedestrians
-      const int a0 = pass == 0 ? 0 : q.nveh, a1 = pass == 0 ? q.nveh : q.nact;
-      if (a1 <= a0) continue;
-      const uint32_t col = pass == 0 ? CBEV_PX_VEHICLE : CBEV_PX_PEDESTRIAN;
-      if (k >= a0 && k < a1) paint_rect4(lds, rt, shift, C, P.pad, xmin, ymin, q.ax, q.ay, q.asz, tq, col);
-      for (int a = NT / 4 + k; a < a1; a += NT / 4)  // more than NT / 4 actors: fetched here
-        if (a >= a0)
-          paint_rect4(lds, rt, shift, C, P.pad, xmin, ymin, RAD(r, CBEV_AD_X, a), RAD(r, CBEV_AD_Y, a),
-                             RAI(r, CBEV_AI_SIZE, a), tq, col);
-      lds_barrier();
-    }
-    const int nt = q.nt;
-    // checkpoints 2x2, goal 4x4 (scenes/utils.py:114-122)
-    if (k < nt && ((q.tvis >> (k & 31)) & 1u))
-      paint_rect4(lds, rt, shift, C, P.pad, xmin, ymin, q.tx, q.ty, k < nt - 1 ? 2 : 4, tq, CBEV_PX_ROUTE);
-    for (int i = NT / 4 + k; i < nt; i += NT / 4)
-      if ((r.vis_draw[i >> 5] >> (i & 31)) & 1u)
-        paint_rect4(lds, rt, shift, C, P.pad, xmin, ymin, r.cx[i], r.cy[i], i < nt - 1 ? 2 : 4, tq,
-                           CBEV_PX_ROUTE);
-    lds_barrier();
-    for (int t = 0; t < q.ntl; ++t) {  // traffic lights one at a time (colours may differ)
-      const int rx = r.ti[CBEV_TI_RX * r.T + t] - xmin, ry = r.ti[CBEV_TI_RY * r.T + t] - ymin;
-      const int rw = r.ti[CBEV_TI_RW * r.T + t], rh = r.ti[CBEV_TI_RH * r.T + t];
-      const uint8_t col = (uint8_t)r.ti[CBEV_TI_COLOR * r.T + t];
-      for (int qy = threadIdx.x >> 4; qy < rh; qy += NT / 16)
-        for (int qx = threadIdx.x & 15; qx < rw; qx += 16) {
-          const int px = rx + qx, py = ry + qy;
-          if (px >= 0 && py >= 0 && px < C && py < C) lds_set_texel(lds, py * rt + shift + px, col);
-        }
-      lds_barrier();
-    }
-  }
-}
-
-// One env's render set-up: crop origin, rotation, fast-path flag and the paint
-// inputs. RESET: BaseMap.reset's frame (theta = 0, no actors drawn,
-// world.py:92-100) at the record's pose; otherwise the RS_* ints k_ego wrote.
+// One env's render set-up. RESET: BaseMap.reset's frame (theta = 0, no actors
+// drawn, world.py:92-100) at the record's pose; otherwise the crop origin and
+// the RS_* rotation ints k_ego wrote for this step.
 struct RasterJob {
-  int xmin, ymin, shift, xa;  // crop origin, its texel offset in the dword-aligned LDS row, packed byte column
-  RotSetup R;
-  bool fast;
-  PaintPre pq;
+  int xmin, ymin;  // crop origin in the padded map (fov.py:70-79, d_crop_origin)
+  RotSetup R;      // affine form (raster8_affine)
+  bool fast;       // the whole output samples inside the crop, covered by the rotated surface
 };
 
 template <bool RESET, int G>
-__device__ __forceinline__ void raster_origin(const KArgs& K, const DRec& r, RasterJob& J) {
-  if (RESET) {
-    d_crop_origin(K.P, r.hd[CBEV_HD_X], r.hd[CBEV_HD_Y], &J.xmin, &J.ymin);
-  } else {
-    J.xmin = r.hi[CBEV_HI_RS_XMIN];
-    J.ymin = r.hi[CBEV_HI_RS_YMIN];
-  }
-  J.xa = (J.xmin >> 1) & ~3;    // packed byte column (dword aligned)
-  J.shift = J.xmin - 2 * J.xa;  // texel offset (0..7)
-}
-
-template <bool RESET, int G>
-__device__ __forceinline__ void raster_rot(const KArgs& K, const DRec& r, RasterJob& J) {
+__device__ __forceinline__ RasterJob raster_job(const KArgs& K, const DRec& r) {
   const cbev_params& P = K.P;
+  RasterJob J;
   const int rt = raster_row_texels(64 * G, P.crop);
   if (RESET) {  // BaseMap.reset: theta 0 -> rotate90 by one turn
+    d_crop_origin(P, r.hd[CBEV_HD_X], r.hd[CBEV_HD_Y], &J.xmin, &J.ymin);
     J.R = rot_setup(P, 90.0f, rt);
+    J.fast = raster_fast(P, J.R);
   } else {  // written by k_ego for this step
+    J.xmin = r.hi[CBEV_HI_RS_XMIN];
+    J.ymin = r.hi[CBEV_HI_RS_YMIN];
     int32_t* w = (int32_t*)&J.R;
 #pragma unroll
     for (int k = 0; k < CBEV_RS_WORDS; ++k) w[k] = r.hi[CBEV_HI_RS_R90 + k];
+    J.fast = r.hi[CBEV_HI_RS_FAST] != 0;
   }
-  J.fast = !RESET ? r.hi[CBEV_HI_RS_FAST] != 0 : raster_fast(P, J.R);
+  raster8_affine(J.R, rt);
+  return J;
 }
 
-// Crop staging: 16-byte global loads of the nibble-packed map, lane-linear over
-// the window's row chunks (STAGE_U per thread in flight), then dword LDS stores.
-// Only the rows and 32-texel chunks the output samples are staged: the
-// output -> crop map is affine, so the sampled texels lie in the bounding box of
-// the four output corners' source texels (fast path; the slow path, with
-// background / clipping tests, stages the whole crop). The image layout stays
-// the whole crop's, so the gathers are unchanged. Roads are axis-aligned, so
-// most headings sample about a 130 x 130 box of the 182 x 182 crop (S=128).
-#define STAGE_U 5
-struct StageWin {
-  int y0, ny, c0, nc;  // crop rows [y0, y0 + ny), row chunks [c0, c0 + nc)
+// A tile's window in (u, v) = (x, y), or (y, x) when transposed: crop rows
+// v in [v0, v0 + nv), the 16-byte chunks [c0, c0 + nc) of the (transposed)
+// byte map's row from umin & ~3; crop (u, v) is LDS byte (v - v0) * sb + ou + u.
+struct TileWin {
+  int tr;          // transposed (rows = crop columns, staged from map8T)
+  int umin, vmin;  // crop origin in (u, v)
+  int v0, nv, c0, nc, sb, ou;
 };
+
 template <int G>
-__device__ __forceinline__ StageWin stage_window(const cbev_params& P, const RasterJob& J) {
-  const int C = P.crop;
-  const int nch = raster_row_chunks(64 * G, C);
-  StageWin w{0, C, 0, nch};
-  if (!J.fast) return w;
+__device__ __forceinline__ TileWin tile_window(const cbev_params& P, const RasterJob& J, int ox0, int oy0) {
+  using TG = Tiles<G>;
   const RotSetup& R = J.R;
-  const int S = 64 * G;
-  int xl = 1 << 30, xh = -(1 << 30), yl = 1 << 30, yh = -(1 << 30);
-  const int rt = raster_row_texels(S, C);
-#pragma unroll
-  for (int c = 0; c < 4; ++c) {
-    const int xx = ((c & 1) ? S - 1 : 0) - R.rx0, yy = ((c & 2) ? S - 1 : 0) - R.ry0;
-    int tx, ty;
-    if (R.r90) {  // LDS texel address without the shift: row * rt + column
-      const int a = R.a00 + xx * R.ustep + yy * R.vstep;
-      ty = a / rt;
-      tx = a - ty * rt;
-    } else {
-      tx = (R.dx00 + xx * R.icos - yy * R.isin) >> 16;
-      ty = (R.dy00 + xx * R.isin + yy * R.icos) >> 16;
-    }
-    xl = min(xl, tx);
-    xh = max(xh, tx);
-    yl = min(yl, ty);
-    yh = max(yh, ty);
-  }
-  xl = max(xl, 0);
-  yl = max(yl, 0);
-  xh = min(xh, C - 1);
-  yh = min(yh, C - 1);
-  w.y0 = yl;
-  w.ny = yh - yl + 1;
-  const int cs = 5;  // 32 texels per 16-byte chunk
-  w.c0 = (J.shift + xl) >> cs;
-  w.nc = ((J.shift + xh) >> cs) - w.c0 + 1;
-  return w;
-}
-
-// All STAGE_U loads of a thread are issued back to back, then committed: no
-// branch around a load (a chunk index past the window is clamped to its last
-// chunk, which is then loaded and stored again with the same bytes) and no
-// branch around an LDS store (a row's last chunk overhanging the row stride is
-// redirected to a spare dword after the image). Branches around the loads made
-// the compiler wait for every outstanding load (vmcnt(0)) before each one, so
-// a thread's staging took STAGE_U + 1 dependent memory round trips.
-template <int G, int NT = 256>
-__device__ __forceinline__ void stage_all(const KArgs& K, const RasterJob& J, uint8_t* __restrict__ lds) {
-  const StageWin W = stage_window<G>(K.P, J);
-  const int C = K.P.crop;
-  const int sd = raster_stride_dwords(64 * G, C);
-  const int nc = W.nc, total = W.ny * nc;
-  const int rl = (total - 1) / nc, cl = (total - 1) - rl * nc;  // the window's last chunk
-  const int dr = NT / nc, dj = NT - dr * nc;
-  const uint8_t* gbase = K.map + (int64_t)(J.ymin + W.y0) * K.npitch + J.xa + 16 * W.c0;
-  uint32_t* l32 = (uint32_t*)lds + W.y0 * sd + 4 * W.c0;
-  uint32_t* spare = (uint32_t*)lds + C * sd;  // raster_image_bytes leaves one dword here
-  const int jlim = sd - 4 * W.c0;              // dwords of a row from the window's first chunk on
-  for (int q0 = 0; q0 < total; q0 += NT * STAGE_U) {
-    const int q = q0 + (int)threadIdx.x;
-    int r = q / nc, c = q - r * nc;
-    uint4 v[STAGE_U];
-    int off[STAGE_U], jj[STAGE_U];
-#pragma unroll
-    for (int u = 0; u < STAGE_U; ++u) {
-      const bool ok = q + NT * u < total;
-      const int rr = ok ? r : rl, cc = ok ? c : cl;
-      off[u] = rr * sd + 4 * cc;
-      jj[u] = 4 * cc;  // dword of the row, from the window's first chunk
-      v[u] = load16_a4(gbase + (int64_t)rr * K.npitch + 16 * cc);
-      r += dr;
-      c += dj;
-      if (c >= nc) {
-        c -= nc;
-        ++r;
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < STAGE_U; ++u) {
-      l32[off[u]] = v[u].x;
-      *(jj[u] + 1 < jlim ? l32 + off[u] + 1 : spare) = v[u].y;
-      *(jj[u] + 2 < jlim ? l32 + off[u] + 2 : spare) = v[u].z;
-      *(jj[u] + 3 < jlim ? l32 + off[u] + 3 : spare) = v[u].w;
-    }
-  }
-}
-
-// rotate (pygame transform.rotate / rotate90) + compose + ego overlay of the
-// painted crop image into `nout` frames out + k*out_stride
-template <int G, int NT = 256>
-__device__ __forceinline__ void raster_emit(const KArgs& K, const RasterJob& J, uint8_t* __restrict__ out, int nout,
-                                            int64_t out_stride, const uint8_t* __restrict__ lds) {
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t bg = lds_texel(lds, J.shift);  // crop top-left pixel after painting
-  raster_out_dispatch<G, NT / 64>(K.P, J.R, J.fast, lds, J.shift, bg, out, nout, out_stride, lane, wave, K.fov);
-}
-
-// ====================================================== byte-image raster (S <= 128)
-__host__ __device__ constexpr int r8_alloc(int S);
-// the raster's dynamic LDS: the byte image's window allocation, or the whole
-// nibble crop + one spare dword (the nibble staging's overhang writes land there)
-__host__ __device__ __forceinline__ int raster_image_bytes(int S, int C) {
-  const int nib = C * raster_stride_dwords(S, C) * 4 + 16;
-  return raster_win8(S) && r8_alloc(S) > nib ? r8_alloc(S) : nib;
-}
-// The byte window holds only the texels of the crop that the output samples
-// (the output -> crop map is affine: the bounding box of the four corners'
-// samples): crop rows [y0, y0 + ny) and the 16-byte chunks [c0, c0 + nc) of the
-// byte map's row from xa = xmin & ~3, one palette id per byte, rows
-// sb = 16 nc + 4 bytes apart (an odd number of dwords). Crop texel (x, y) is LDS
-// byte (y - y0) * sb + ox + x with ox = shift - 16 c0. The allocation is R8_LDS
-// bytes: at S=128 a heading up to about 10 degrees off an axis (roads are
-// axis-aligned) samples <= 24 KB; steeper headings take the nibble image.
-// Measured at config 2 (raster us / launch): nibble only 26.0; windows of 20 KB
-// 25.4, 22 KB 24.6, 24 KB 22.4, 28 KB 22.4, 32 KB 23.7, 36 KB (every heading)
-// 23.2; output bands for windows that do not fit: 60 (the band loop's registers
-// spilled under the 64-VGPR launch bound).
-// A gather is one byte read whose address is two SDWA instructions of the 16.16
-// coordinates; with the coordinate step and the packing, 3.75 VALU instructions
-// per pixel.
-#ifndef CBEV_R8_LDS
-#define CBEV_R8_LDS 24576
-#endif
-__host__ __device__ constexpr int r8_alloc(int S) { return S >= 128 ? CBEV_R8_LDS : 12288; }
-
-struct Win8 {
-  int y0, ny;  // crop rows [y0, y0 + ny)
-  int c0, nc;  // 16-byte chunks of the byte-map row from xa
-  int sb;      // LDS bytes per image row
-  int ox;      // LDS column of crop column 0
-};
-
-// The crop texels output rows [ra, rb) sample: the bounding box of the four
-// corners' source texels (pygame's rotozoom is affine in the output pixel),
-// clamped to the crop (samples outside it are background, no texel needed).
-template <int G>
-__device__ __forceinline__ Win8 win8(const cbev_params& P, const RasterJob& J, int ra, int rb) {
-  constexpr int S = 64 * G;
   const int C = P.crop;
-  const RotSetup& R = J.R;  // affine form (raster8_affine)
   int xl = 1 << 30, xh = -(1 << 30), yl = 1 << 30, yh = -(1 << 30);
 #pragma unroll
   for (int c = 0; c < 4; ++c) {
-    const int xx = ((c & 1) ? S - 1 : 0) - R.rx0, yy = ((c & 2) ? rb - 1 : ra) - R.ry0;
+    const int xx = ox0 + ((c & 1) ? TG::TC - 1 : 0) - R.rx0, yy = oy0 + ((c & 2) ? TG::TR - 1 : 0) - R.ry0;
     const int tx = (R.dx00 + xx * R.icos - yy * R.isin) >> 16;
     const int ty = (R.dy00 + xx * R.isin + yy * R.icos) >> 16;
     xl = min(xl, tx);
@@ -1822,30 +1350,41 @@ __device__ __forceinline__ Win8 win8(const cbev_params& P, const RasterJob& J, i
     yl = min(yl, ty);
     yh = max(yh, ty);
   }
+  // samples outside the crop are background (no texel needed)
   xl = min(max(xl, 0), C - 1);
   yl = min(max(yl, 0), C - 1);
   xh = max(min(xh, C - 1), xl);
   yh = max(min(yh, C - 1), yl);
-  Win8 W;
-  W.y0 = yl;
-  W.ny = yh - yl + 1;
-  W.c0 = (J.shift + xl) >> 4;
-  W.nc = ((J.shift + xh) >> 4) - W.c0 + 1;
-  W.sb = 16 * W.nc + 4;
-  W.ox = J.shift - 16 * W.c0;
+  TileWin W;
+  W.tr = abs(R.isin) > abs(R.icos);
+  const int ul = W.tr ? yl : xl, uh = W.tr ? yh : xh;
+  W.umin = W.tr ? J.ymin : J.xmin;
+  W.vmin = W.tr ? J.xmin : J.ymin;
+  W.v0 = W.tr ? xl : yl;
+  W.nv = (W.tr ? xh : yh) - W.v0 + 1;
+  const int ushift = W.umin & 3;
+  W.c0 = (ushift + ul) >> 4;
+  W.nc = ((ushift + uh) >> 4) - W.c0 + 1;
+  W.sb = 16 * W.nc + 4;  // an odd number of dwords: the rows of a wave's lanes fall on distinct banks
+  W.ou = ushift - 16 * W.c0;
   return W;
 }
 
 // Staging: the window's nc chunks of a row are taken by nc consecutive threads,
-// 256 / nc rows per pass; a thread's rows of all passes are loaded back to back
-// (straight-line code: no branch around a load; rows past the window are its
-// last row again, stored again with the same bytes), then stored.
+// 256 / nc rows per pass; a thread's rows of up to U passes are loaded back to
+// back (straight-line code: no branch around a load; rows past the window are
+// its last row again, stored again with the same bytes), then stored.
+typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
+__device__ __forceinline__ uint4 load16_a4(const uint8_t* p) {  // 16 bytes at 4-byte alignment
+  const u32x4_a4 t = *(const u32x4_a4*)p;
+  return make_uint4(t.x, t.y, t.z, t.w);
+}
 template <int U>
-__device__ __forceinline__ void stage8_group(const uint8_t* __restrict__ g, int p8, uint8_t* __restrict__ l, int sb,
-                                             int row, int dr, int last) {
+__device__ __forceinline__ void stage_group(const uint8_t* __restrict__ g, int pitch, uint8_t* __restrict__ l, int sb,
+                                            int row, int dr, int last) {
   uint4 v[U];
 #pragma unroll
-  for (int u = 0; u < U; ++u) v[u] = load16_a4(g + (int64_t)min(row + u * dr, last) * p8);
+  for (int u = 0; u < U; ++u) v[u] = load16_a4(g + (int64_t)min(row + u * dr, last) * pitch);
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     uint32_t* d = (uint32_t*)(l + min(row + u * dr, last) * sb);
@@ -1855,45 +1394,46 @@ __device__ __forceinline__ void stage8_group(const uint8_t* __restrict__ g, int 
     d[3] = v[u].w;
   }
 }
-__device__ __forceinline__ void stage8(const KArgs& K, const RasterJob& J, const Win8& W, uint8_t* __restrict__ lds) {
+__device__ __forceinline__ void stage_tile(const KArgs& K, const TileWin& W, uint8_t* __restrict__ lds) {
   const int nc = W.nc, dr = 256 / nc;
   const int t = (int)threadIdx.x;
   int row = t / nc;
   const int c = t - row * nc;
   row = row < dr ? row : dr - 1;  // the 256 % nc leftover threads repeat chunks of the pass's last row
-  const int passes = (W.ny + dr - 1) / dr;
-  const uint8_t* g = K.map8 + (int64_t)(J.ymin + W.y0) * K.p8 + J.xa + 16 * (W.c0 + c);
+  const int passes = (W.nv + dr - 1) / dr;
+  const uint8_t* map = W.tr ? K.map8T : K.map8;
+  const int pitch = W.tr ? K.p8T : K.p8;
+  const uint8_t* g = map + (int64_t)(W.vmin + W.v0) * pitch + (W.umin & ~3) + 16 * (W.c0 + c);
   uint8_t* l = lds + 16 * c;
-  // a window of <= R8_LDS bytes takes <= 6 passes at S = 128 (ny <= R8_LDS / (16 nc + 4), 256 / nc rows a pass)
-  if (passes <= 3) {
-    stage8_group<3>(g, K.p8, l, W.sb, row, dr, W.ny - 1);
+  if (passes <= 4) {
+    stage_group<4>(g, pitch, l, W.sb, row, dr, W.nv - 1);
   } else {
-    for (int p0 = 0; p0 < passes; p0 += 6) stage8_group<6>(g, K.p8, l, W.sb, row + p0 * dr, dr, W.ny - 1);
+    for (int p0 = 0; p0 < passes; p0 += 6) stage_group<6>(g, pitch, l, W.sb, row + p0 * dr, dr, W.nv - 1);
   }
 }
 
-// one rect (rect_from_world_center, transforms.py:46-51) by the 4 threads of
-// tid >> 2, clipped to the crop and the window: byte stores (rects of a pass
-// share their colour, so overlaps commute)
-__device__ __forceinline__ void paint8_rect(uint8_t* lds, const Win8& W, int C, int pad, int xmin, int ymin, double wx,
-                                            double wy, int sz, int tq, uint32_t col) {
-  const int rx = d_rect_lo(wx, pad, sz) - xmin, ry = d_rect_lo(wy, pad, sz) - ymin;
-  // crop columns the window holds: [-ox, -ox + 16 nc)
-  const int x0 = max(max(rx, 0), -W.ox), x1 = min(min(rx + sz, C), -W.ox + 16 * W.nc);
-  if (x0 >= x1) return;
-  for (int qy = tq; qy < sz; qy += 4) {
-    const int py = ry + qy - W.y0;
-    if (py < 0 || py >= W.ny || ry + qy >= C) continue;
-    uint8_t* rowp = lds + py * W.sb + W.ox;
-    for (int x = x0; x < x1; ++x) rowp[x] = (uint8_t)col;
+// crop rect [rx, rx + sx) x [ry, ry + sy) (rect_from_world_center,
+// transforms.py:46-51, clipped to the crop) into the window, byte stores by the
+// 4 threads of tid >> 2 (rects of a pass share their colour: overlaps commute)
+__device__ __forceinline__ void paint_win_rect(uint8_t* lds, const TileWin& W, int C, int rx, int ry, int sx, int sy,
+                                               int tq, uint32_t col) {
+  const int ru = W.tr ? ry : rx, rv = W.tr ? rx : ry, su = W.tr ? sy : sx, sv = W.tr ? sx : sy;
+  const int u0 = max(max(ru, 0), -W.ou), u1 = min(min(ru + su, C), -W.ou + 16 * W.nc);
+  if (u0 >= u1) return;
+  for (int qv = tq; qv < sv; qv += 4) {
+    const int pv = rv + qv;
+    if (pv >= C || pv < W.v0 || pv >= W.v0 + W.nv) continue;
+    uint8_t* rowp = lds + (pv - W.v0) * W.sb + W.ou;
+    for (int u = u0; u < u1; ++u) rowp[u] = (uint8_t)col;
   }
 }
 
 // Actors, the targets visible before this step's collisions and traffic lights
 // into the window in the reference's draw order (scene.py:93-95,
-// actor_manager.py:121-132): vehicles, pedestrians, targets, traffic lights.
-__device__ __forceinline__ void paint8(const KArgs& K, const DRec& r, const PaintPre& q, const RasterJob& J,
-                                       const Win8& W, uint8_t* __restrict__ lds) {
+// actor_manager.py:121-132, target.py:46-50, traffic_light.py:81-90):
+// vehicles, pedestrians, targets, traffic lights, later wins.
+__device__ __forceinline__ void paint_tile(const KArgs& K, const DRec& r, const PaintPre& q, const RasterJob& J,
+                                           const TileWin& W, uint8_t* __restrict__ lds) {
   constexpr int NT = 256;
   const cbev_params& P = K.P;
   const int C = P.crop;
@@ -1902,40 +1442,80 @@ __device__ __forceinline__ void paint8(const KArgs& K, const DRec& r, const Pain
     const int a0 = pass == 0 ? 0 : q.nveh, a1 = pass == 0 ? q.nveh : q.nact;
     if (a1 <= a0) continue;
     const uint32_t col = pass == 0 ? CBEV_PX_VEHICLE : CBEV_PX_PEDESTRIAN;
-    if (k >= a0 && k < a1) paint8_rect(lds, W, C, P.pad, J.xmin, J.ymin, q.ax, q.ay, q.asz, tq, col);
+    if (k >= a0 && k < a1)
+      paint_win_rect(lds, W, C, d_rect_lo(q.ax, P.pad, q.asz) - J.xmin, d_rect_lo(q.ay, P.pad, q.asz) - J.ymin, q.asz,
+                     q.asz, tq, col);
     for (int a = NT / 4 + k; a < a1; a += NT / 4)  // more than NT / 4 actors: fetched here
-      if (a >= a0)
-        paint8_rect(lds, W, C, P.pad, J.xmin, J.ymin, RAD(r, CBEV_AD_X, a), RAD(r, CBEV_AD_Y, a),
-                    RAI(r, CBEV_AI_SIZE, a), tq, col);
+      if (a >= a0) {
+        const int sz = RAI(r, CBEV_AI_SIZE, a);
+        paint_win_rect(lds, W, C, d_rect_lo(RAD(r, CBEV_AD_X, a), P.pad, sz) - J.xmin,
+                       d_rect_lo(RAD(r, CBEV_AD_Y, a), P.pad, sz) - J.ymin, sz, sz, tq, col);
+      }
     lds_barrier();
   }
   const int nt = q.nt;
   // checkpoints 2x2, goal 4x4 (scenes/utils.py:114-122)
-  if (k < nt && ((q.tvis >> (k & 31)) & 1u))
-    paint8_rect(lds, W, C, P.pad, J.xmin, J.ymin, q.tx, q.ty, k < nt - 1 ? 2 : 4, tq, CBEV_PX_ROUTE);
+  if (k < nt && ((q.tvis >> (k & 31)) & 1u)) {
+    const int sz = k < nt - 1 ? 2 : 4;
+    paint_win_rect(lds, W, C, d_rect_lo(q.tx, P.pad, sz) - J.xmin, d_rect_lo(q.ty, P.pad, sz) - J.ymin, sz, sz, tq,
+                   CBEV_PX_ROUTE);
+  }
   for (int i = NT / 4 + k; i < nt; i += NT / 4)
-    if ((r.vis_draw[i >> 5] >> (i & 31)) & 1u)
-      paint8_rect(lds, W, C, P.pad, J.xmin, J.ymin, r.cx[i], r.cy[i], i < nt - 1 ? 2 : 4, tq, CBEV_PX_ROUTE);
+    if ((r.vis_draw[i >> 5] >> (i & 31)) & 1u) {
+      const int sz = i < nt - 1 ? 2 : 4;
+      paint_win_rect(lds, W, C, d_rect_lo(r.cx[i], P.pad, sz) - J.xmin, d_rect_lo(r.cy[i], P.pad, sz) - J.ymin, sz, sz,
+                     tq, CBEV_PX_ROUTE);
+    }
   lds_barrier();
-  const int wx0 = -W.ox, wx1 = -W.ox + 16 * W.nc;  // crop columns the window holds
   for (int t = 0; t < q.ntl; ++t) {  // traffic lights one at a time (colours may differ)
     const int rx = r.ti[CBEV_TI_RX * r.T + t] - J.xmin, ry = r.ti[CBEV_TI_RY * r.T + t] - J.ymin;
     const int rw = r.ti[CBEV_TI_RW * r.T + t], rh = r.ti[CBEV_TI_RH * r.T + t];
     const uint8_t col = (uint8_t)r.ti[CBEV_TI_COLOR * r.T + t];
-    for (int qy = threadIdx.x >> 4; qy < rh; qy += NT / 16)
-      for (int qx = threadIdx.x & 15; qx < rw; qx += 16) {
-        const int px = rx + qx, py = ry + qy;
-        if (px >= 0 && py >= 0 && px < C && py < C && px >= wx0 && px < wx1 && py >= W.y0 && py < W.y0 + W.ny)
-          lds[(py - W.y0) * W.sb + W.ox + px] = col;
+    const int ru = W.tr ? ry : rx, rv = W.tr ? rx : ry, su = W.tr ? rh : rw, sv = W.tr ? rw : rh;
+    for (int qv = threadIdx.x >> 4; qv < sv; qv += NT / 16)
+      for (int qu = threadIdx.x & 15; qu < su; qu += 16) {
+        const int pu = ru + qu, pv = rv + qv;
+        if (pu >= 0 && pv >= 0 && pu < C && pv < C && pu >= -W.ou && pu < -W.ou + 16 * W.nc && pv >= W.v0 &&
+            pv < W.v0 + W.nv)
+          lds[(pv - W.v0) * W.sb + W.ou + pu] = col;
       }
     lds_barrier();
   }
 }
 
-// pygame rotate's background: the crop's top-left pixel after painting
-// (fov.py:84-88), which a window need not hold: the map texel there, then the
-// last pass in draw order with a rect over it.
-// (dy >> 16) * sb + (dx >> 16): v_mul_u32_u24 and v_add_u32 with SDWA word selects
+// pygame rotate's background, the crop's top-left pixel after painting
+// (fov.py:84-88): the map texel there, then the last rect over it in draw order
+// (only the tiles that sample outside the crop need it). Uniform: every thread
+// computes it from the record.
+__device__ __forceinline__ uint32_t crop_background(const KArgs& K, const DRec& r, const RasterJob& J, bool paint) {
+  const cbev_params& P = K.P;
+  uint32_t col = K.map8[(int64_t)J.ymin * K.p8 + J.xmin];
+  if (!paint) return col;
+  auto covers = [](int rx, int ry, int sx, int sy) { return rx <= 0 && 0 < rx + sx && ry <= 0 && 0 < ry + sy; };
+  const int nact = r.hi[CBEV_HI_NACT], nveh = r.hi[CBEV_HI_NVEH], nt = r.hi[CBEV_HI_NROUTE], ntl = r.hi[CBEV_HI_NTL];
+  for (int a = 0; a < nact; ++a) {  // vehicles [0, nveh), then pedestrians
+    const int sz = RAI(r, CBEV_AI_SIZE, a);
+    if (covers(d_rect_lo(RAD(r, CBEV_AD_X, a), P.pad, sz) - J.xmin, d_rect_lo(RAD(r, CBEV_AD_Y, a), P.pad, sz) - J.ymin,
+               sz, sz))
+      col = a < nveh ? CBEV_PX_VEHICLE : CBEV_PX_PEDESTRIAN;
+  }
+  for (int i = 0; i < nt; ++i) {
+    const int sz = i < nt - 1 ? 2 : 4;
+    if (((r.vis_draw[i >> 5] >> (i & 31)) & 1u) &&
+        covers(d_rect_lo(r.cx[i], P.pad, sz) - J.xmin, d_rect_lo(r.cy[i], P.pad, sz) - J.ymin, sz, sz))
+      col = CBEV_PX_ROUTE;
+  }
+  for (int t = 0; t < ntl; ++t)
+    if (covers(r.ti[CBEV_TI_RX * r.T + t] - J.xmin, r.ti[CBEV_TI_RY * r.T + t] - J.ymin, r.ti[CBEV_TI_RW * r.T + t],
+               r.ti[CBEV_TI_RH * r.T + t]))
+      col = (uint32_t)r.ti[CBEV_TI_COLOR * r.T + t];
+  return col;
+}
+
+typedef uint32_t u32x4_nt __attribute__((ext_vector_type(4)));  // one 16-byte (non-temporal) store
+
+// (v >> 16) * sb + (u >> 16) of the packed window coordinates (v << 32 | u):
+// v_mul_u32_u24 and v_add_u32 with SDWA word selects
 __device__ __forceinline__ uint32_t crop_byte_addr(uint64_t q, uint32_t sb) {
   uint32_t a;
   asm("v_mul_u32_u24_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1\n\t"
@@ -1944,56 +1524,75 @@ __device__ __forceinline__ uint32_t crop_byte_addr(uint64_t q, uint32_t sb) {
       : "s"(sb), "v"((uint32_t)(q >> 32)), "v"((uint32_t)q));
   return a;
 }
-// a byte of the LDS image at an absolute LDS address (the dynamic LDS starts at
-// 0: k_raster declares no static LDS). A C-level read adds the array's base, one
-// more VALU instruction per pixel; the compiler's wait-count insertion does not
-// see this read, so its users wait for it explicitly (s_waitcnt lgkmcnt(0)
-// naming the registers).
+// a byte of the LDS window at an absolute LDS address (the dynamic LDS starts at
+// 0: the raster kernels declare no static LDS). A C-level read adds the array's
+// base, one more VALU instruction per pixel; the compiler's wait-count insertion
+// does not see this read, so its users wait for it explicitly.
 __device__ __forceinline__ void lds_u8(uint32_t& d, uint32_t a) { asm volatile("ds_read_u8 %0, %1" : "=v"(d) : "v"(a)); }
 
-// Output rows of chunks [0, nch) (RPC rows each, dealt over the NW waves): lane
-// l of a chunk owns the 16 consecutive pixels of row r + l / LPR, columns
-// 16 (l % LPR) .. + 15, gathered one column step apart and written with one
-// 16-byte store. The rotated surface covers the whole output and every output
-// pixel samples inside the window (raster8_env's conditions): no per-pixel tests.
-template <int G, int NW>
-__device__ __forceinline__ void raster_out8(const cbev_params& P, const RotSetup& R, const Win8& W,
-                                            const uint8_t* __restrict__ lds, uint8_t* __restrict__ out, int nout,
-                                            int64_t out_stride, int lane, int wave,
-                                            const uint32_t* __restrict__ fov, int nch) {
-  constexpr int S = 64 * G;     // == P.size
-  constexpr int LPR = S / 16;   // lanes per output row
-  constexpr int RPC = 64 / LPR; // output rows per chunk
+// Hero.draw (hero.py:26-32, the black w x w rect at the anchor) and
+// FovRenderer.apply_mask (fov.py:96-99, black corner triangles) on a lane's
+// 16 output pixels at frame offset vo (row Y, columns X .. X + 15)
+__device__ __forceinline__ void overlay16(const cbev_params& P, const uint32_t* __restrict__ fov, uint32_t vo, int X,
+                                          int Y, bool hero_chunk, uint32_t* w) {
+  if (fov) {  // uniform branch
+    const uint4 fm = *(const uint4*)(fov + (vo >> 2));
+    w[0] = (w[0] & ~fm.x) | (fm.x & (CBEV_PX_BLACK * 0x01010101u));
+    w[1] = (w[1] & ~fm.y) | (fm.y & (CBEV_PX_BLACK * 0x01010101u));
+    w[2] = (w[2] & ~fm.z) | (fm.z & (CBEV_PX_BLACK * 0x01010101u));
+    w[3] = (w[3] & ~fm.w) | (fm.w & (CBEV_PX_BLACK * 0x01010101u));
+  }
   const int hero_w = P.hero_w;
   const int hx0 = P.anchor_x - hero_w / 2, hy0 = P.anchor_y - hero_w / 2;
-  // lane l owns row l / LPR, columns 16 (l % LPR) .. + 15 of the chunk; when the
-  // output rows run across the image rows (|sin| > |cos|: the column groups' 16
-  // pixels apart land 16 image rows apart, on banks of one parity) each 32-lane
-  // half takes half the column groups of all the chunk's rows instead (2-way
-  // conflicts, not 4: 21.7 vs 23.9 us with every ego at yaw 0; at yaw 90 the
-  // row-major mapping is the faster, 18.9 vs 19.3)
-  const bool across = (LPR == 8) && abs(R.isin) > abs(R.icos);
-  const int lrow = across ? ((lane & 31) >> 2) : lane / LPR;
-  const int lcol = across ? 16 * ((lane & 3) + 4 * (lane >> 5)) : 16 * (lane % LPR);
-  const int r0 = wave * RPC;
-  const int xx0 = lcol - R.rx0, yy0 = r0 + lrow - R.ry0;
-  // window coordinates (crop coordinates moved by (ox, -y0)) in 16.16, packed in
-  // one 64-bit value so one 64-bit add steps both (the low word stays in
-  // [0, 2^32): no carry crosses over)
-  const int sx = R.dx00 + xx0 * R.icos - yy0 * R.isin + (W.ox << 16);
-  const int sy = R.dy00 + xx0 * R.isin + yy0 * R.icos - (W.y0 << 16);
+  // the byte mask is built only in the chunks that meet the hero rows (no registers held)
+  if (hero_chunk && (unsigned)(Y - hy0) < (unsigned)hero_w) {
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      uint32_t m = 0;
+#pragma unroll
+      for (int bb = 0; bb < 4; ++bb) {
+        const int u = X + 4 * d + bb;
+        if (u >= hx0 && u < hx0 + hero_w) m |= 0xffu << (8 * bb);
+      }
+      w[d] = (w[d] & ~m) | (m & (CBEV_PX_BLACK * 0x01010101u));
+    }
+  }
+}
+
+// Output of one tile whose every pixel samples inside the window (J.fast: the
+// rotated surface covers the whole output and every sample lies inside the
+// crop; checked once per env at the four corners): chunks of RPC rows dealt
+// over the 4 waves; lane l owns the 16 consecutive pixels of row l / LPR,
+// columns 16 (l % LPR) .. + 15 of the tile, gathered one column step apart
+// (one 64-bit add steps both packed window coordinates: the low word stays in
+// [0, 2^32), so no carry crosses over), packed into 4 dwords by v_lshl_or +
+// v_perm and written with ONE 16-byte non-temporal store.
+template <int G>
+__device__ __forceinline__ void tile_out(const cbev_params& P, const RotSetup& R, const TileWin& W, int ox0, int oy0,
+                                         const uint8_t* __restrict__ lds, uint8_t* __restrict__ out, int nout,
+                                         int64_t out_stride, const uint32_t* __restrict__ fov) {
+  using TG = Tiles<G>;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lrow = lane / TG::LPR, X = ox0 + 16 * (lane % TG::LPR);
+  const int Y0 = oy0 + wave * TG::RPC + lrow;
+  const int xx = X - R.rx0, yy = Y0 - R.ry0;
+  const int sx = R.dx00 + xx * R.icos - yy * R.isin, sy = R.dy00 + xx * R.isin + yy * R.icos;
+  // window coordinates: (u, v) moved by (ou, -v0)
+  const int u = (W.tr ? sy : sx) + (W.ou << 16), v = (W.tr ? sx : sy) - (W.v0 << 16);
+  const int du_c = W.tr ? R.isin : R.icos, dv_c = W.tr ? R.icos : R.isin;    // one output column right
+  const int du_r = W.tr ? R.icos : -R.isin, dv_r = W.tr ? -R.isin : R.icos;  // one output row down
+  constexpr int chunk_rows = 4 * TG::RPC;
   const uint32_t sb = (uint32_t)W.sb;
-  const int chunk_rows = NW * RPC;
-  uint64_t pxy = ((uint64_t)(uint32_t)sy << 32) | (uint32_t)sx;
-  // one output row down: (dx, dy) += (-isin, icos); one column right: += (icos, isin)
-  const uint64_t chunk_step =
-      (uint64_t)(((int64_t)(chunk_rows * R.icos) << 32) + (int64_t)(-chunk_rows * R.isin));
-  const uint64_t col_step = (uint64_t)(((int64_t)R.isin << 32) + (int64_t)R.icos);
-  for (int ch = wave, r = r0; ch < nch; ch += NW, r += chunk_rows) {
-    const int row = r + lrow;
-    const uint32_t vo = (uint32_t)(row * S + lcol);
+  uint64_t pxy = ((uint64_t)(uint32_t)v << 32) | (uint32_t)u;
+  const uint64_t col_step = (uint64_t)(((int64_t)dv_c << 32) + (int64_t)du_c);
+  const uint64_t chunk_step = (uint64_t)(((int64_t)(chunk_rows * dv_r) << 32) + (int64_t)(chunk_rows * du_r));
+  const int hy0 = P.anchor_y - P.hero_w / 2;
+  for (int ch = wave; ch < TG::NCH; ch += 4) {
+    const int Yc = oy0 + ch * TG::RPC;  // the chunk's first row (uniform)
+    const int Y = Yc + lrow;
+    const uint32_t vo = (uint32_t)(Y * TG::S + X);
     asm volatile("" : "+v"(pxy));
-    uint32_t w[4];
     uint64_t q = pxy;
     uint32_t px[16];
 #pragma unroll
@@ -2007,32 +1606,13 @@ __device__ __forceinline__ void raster_out8(const cbev_params& P, const RotSetup
                    "+v"(px[14]), "+v"(px[15])
                  :
                  : "memory");
+    uint32_t w[4];
 #pragma unroll
     for (int d = 0; d < 4; ++d) {  // three v_lshl_or_b32 / v_perm_b32 per dword (ids < 16: no masking)
       const uint32_t x = px[4 * d] | (px[4 * d + 1] << 8), y = px[4 * d + 2] | (px[4 * d + 3] << 8);
       w[d] = __builtin_amdgcn_perm(y, x, 0x05040100u);
     }
-    if (fov) {  // FovRenderer.apply_mask (fov.py:96-99): black corner triangles (uniform branch)
-      const uint4 fm = *(const uint4*)(fov + (vo >> 2));
-      w[0] = (w[0] & ~fm.x) | (fm.x & (CBEV_PX_BLACK * 0x01010101u));
-      w[1] = (w[1] & ~fm.y) | (fm.y & (CBEV_PX_BLACK * 0x01010101u));
-      w[2] = (w[2] & ~fm.z) | (fm.z & (CBEV_PX_BLACK * 0x01010101u));
-      w[3] = (w[3] & ~fm.w) | (fm.w & (CBEV_PX_BLACK * 0x01010101u));
-    }
-    // Hero.draw (hero.py:26-32): the black w x w rect at the anchor; its byte
-    // mask is built only in the chunks that meet the hero rows (no registers held)
-    if ((unsigned)(r + RPC - 1 - hy0) < (unsigned)(RPC - 1 + hero_w) && (unsigned)(row - hy0) < (unsigned)hero_w) {
-#pragma unroll
-      for (int d = 0; d < 4; ++d) {
-        uint32_t m = 0;
-#pragma unroll
-        for (int bb = 0; bb < 4; ++bb) {
-          const int u = lcol + 4 * d + bb;
-          if (u >= hx0 && u < hx0 + hero_w) m |= 0xffu << (8 * bb);
-        }
-        w[d] = (w[d] & ~m) | (m & (CBEV_PX_BLACK * 0x01010101u));
-      }
-    }
+    overlay16(P, fov, vo, X, Y, (unsigned)(Yc + TG::RPC - 1 - hy0) < (unsigned)(TG::RPC - 1 + P.hero_w), w);
     const u32x4_nt v4 = {w[0], w[1], w[2], w[3]};
     for (int k = 0; k < nout; ++k)  // streamed out: keep the L2 for the map and the records
       __builtin_nontemporal_store(v4, (u32x4_nt*)(out + (int64_t)k * out_stride + vo));
@@ -2040,125 +1620,134 @@ __device__ __forceinline__ void raster_out8(const cbev_params& P, const RotSetup
   }
 }
 
-
-// rotate90 (exact multiples of 90 degrees: pygame's rotate90 transposes) as the
-// affine map it is: k_ego's texel steps (+-1 column or +-rt = a row, per output
-// column / row) become 16.16 steps of +-65536 with sin / cos in {0, +-1}, and the
-// start texel's coordinates sit at +0x8000, so every sample floors to the exact
-// texel and rotate90 takes the general gather (one output pass fewer to compile).
-__device__ __forceinline__ void raster8_affine(RotSetup& R, int rt) {
-  if (!R.r90) return;
-  const int ar = R.a00 / rt, ac = R.a00 - ar * rt;
-  // output column step = (icos, isin) in (column, row); the row step is (-isin, icos)
-  R.icos = R.ustep == 1 ? 65536 : R.ustep == -1 ? -65536 : 0;
-  R.isin = R.ustep == rt ? 65536 : R.ustep == -rt ? -65536 : 0;
-  R.dx00 = (ac << 16) + 0x8000;
-  R.dy00 = (ar << 16) + 0x8000;
-  R.r90 = 0;
+// The same tile with the per-pixel tests of pygame's rotozoom and blit for the
+// envs whose output samples outside the crop or past the rotated surface
+// (!J.fast): compose clipping (black outside the rotated surface) and the
+// rotozoom background (bg for samples outside the source crop). The window
+// coordinates are kept as two ints (they may leave the window here).
+template <int G>
+__device__ __forceinline__ void tile_out_check(const cbev_params& P, const RotSetup& R, const TileWin& W, int ox0,
+                                               int oy0, const uint8_t* __restrict__ lds, uint32_t bg,
+                                               uint8_t* __restrict__ out, int nout, int64_t out_stride,
+                                               const uint32_t* __restrict__ fov) {
+  using TG = Tiles<G>;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lrow = lane / TG::LPR, X = ox0 + 16 * (lane % TG::LPR);
+  const uint32_t vmax = (uint32_t)((P.crop << 16) - 1);
+  uint32_t xok = 0;  // compose clip per column: inside the rotated surface
+#pragma unroll
+  for (int b = 0; b < 16; ++b) {
+    const int xx = X + b - R.rx0;
+    if (xx >= 0 && xx < R.nx) xok |= 1u << b;
+  }
+  const int du_c = W.tr ? R.isin : R.icos, dv_c = W.tr ? R.icos : R.isin;
+  const int hy0 = P.anchor_y - P.hero_w / 2;
+  for (int ch = wave; ch < TG::NCH; ch += 4) {
+    const int Yc = oy0 + ch * TG::RPC;
+    const int Y = Yc + lrow;
+    const uint32_t vo = (uint32_t)(Y * TG::S + X);
+    const int xx = X - R.rx0, yy = Y - R.ry0;
+    const int sx = R.dx00 + xx * R.icos - yy * R.isin, sy = R.dy00 + xx * R.isin + yy * R.icos;
+    int u = W.tr ? sy : sx, v = W.tr ? sx : sy;  // crop coordinates (16.16)
+    const bool rok = (unsigned)yy < (unsigned)R.ny;
+    uint32_t w[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int b = 0; b < 16; ++b) {
+      const bool ok = rok && ((xok >> b) & 1u);
+      const bool in = (uint32_t)u <= vmax && (uint32_t)v <= vmax;
+      const int a = ((v >> 16) - W.v0) * W.sb + W.ou + (u >> 16);
+      const uint32_t s = lds[(ok && in) ? a : 0];
+      const uint32_t px = !ok ? (uint32_t)CBEV_PX_BLACK : (in ? s : bg);
+      w[b >> 2] |= px << (8 * (b & 3));
+      u += du_c;
+      v += dv_c;
+    }
+    overlay16(P, fov, vo, X, Y, (unsigned)(Yc + TG::RPC - 1 - hy0) < (unsigned)(TG::RPC - 1 + P.hero_w), w);
+    const u32x4_nt v4 = {w[0], w[1], w[2], w[3]};
+    for (int k = 0; k < nout; ++k)
+      __builtin_nontemporal_store(v4, (u32x4_nt*)(out + (int64_t)k * out_stride + vo));
+  }
 }
 
-// One env's observation by the byte window (whole 256-thread workgroup), when
-// the output samples only inside the crop (J.fast) and the window fits R8_LDS:
-// staged, painted (PAINT: the step's frame; the reset frame draws no actors)
-// and written. Otherwise (headings past about 10 degrees off the axes at S=128,
-// or output beyond the crop) returns false and the caller renders the nibble
-// image of the whole crop.
+// Tile t of one env's observation by the whole 256-thread workgroup: window,
+// staging, paint (PAINT: the step's frame; the reset frame draws no actors),
+// output, into `nout` frames out + k * out_stride.
 template <int G, bool PAINT>
-__device__ __forceinline__ bool raster8_env(const KArgs& K, uint8_t* rec, const RasterJob& J0,
+__device__ __forceinline__ void raster_tile(const KArgs& K, const DRec& r, const RasterJob& J, int t,
                                             uint8_t* __restrict__ out, int nout, int64_t out_stride,
                                             uint8_t* __restrict__ lds) {
-  constexpr int S = 64 * G, LPR = S / 16, RPC = 64 / LPR, NCH = S / RPC;
-  if (!J0.fast) return false;
-  RasterJob J = J0;
-  J.xa = J.xmin & ~3;  // byte-map column (dword aligned)
-  J.shift = J.xmin & 3;
-  raster8_affine(J.R, raster_row_texels(S, K.P.crop));
-  const Win8 W = win8<G>(K.P, J, 0, S);
-  if (W.ny * W.sb > r8_alloc(S)) return false;
-  const DRec r = bind_rec(rec, K.L, K.C);
+  using TG = Tiles<G>;
+  const int ox0 = (t % TG::NTX) * TG::TC, oy0 = (t / TG::NTX) * TG::TR;
+  TileWin W = tile_window<G>(K.P, J, ox0, oy0);
+  if (W.nv * W.sb > TG::lds_bytes) {  // cannot happen (Tiles::lds_bytes bounds every heading): flag, stay in bounds
+    if (threadIdx.x == 0) atomicOr(K.err, CBEV_ERR_RASTER_WINDOW);
+    W.nv = TG::lds_bytes / W.sb;
+  }
   PaintPre pq{};
   if (PAINT) pq = raster_paint_fetch(r);  // in flight under the staging
-  stage8(K, J, W, lds);
+  stage_tile(K, W, lds);
   __syncthreads();
   if (PAINT) {
     CBEV_STAMP(2, 1);
-    paint8(K, r, pq, J, W, lds);
+    paint_tile(K, r, pq, J, W, lds);
     CBEV_STAMP(2, 2);
   }
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  raster_out8<G, 4>(K.P, J.R, W, lds, out, nout, out_stride, lane, wave, K.fov, NCH);
-  return true;
-}
-
-// BaseMap.reset's observation (theta = 0, nothing painted, world.py:92-100) of
-// one record by a 256-thread workgroup, into `nout` frames out + k*out_stride
-// (every slot of the frame-stack ring on reset).
-template <int G>
-__device__ __forceinline__ void raster_reset_env(const KArgs& K, const DRec& r, uint8_t* __restrict__ out, int nout,
-                                                 int64_t out_stride, uint8_t* __restrict__ lds) {
-  RasterJob J;
-  raster_origin<true, G>(K, r, J);
-  raster_rot<true, G>(K, r, J);
-  if constexpr (raster_win8(64 * G)) {
-    if (raster8_env<G, false>(K, (uint8_t*)r.hd - K.L.hd, J, out, nout, out_stride, lds)) return;
+  if (J.fast) {
+    tile_out<G>(K.P, J.R, W, ox0, oy0, lds, out, nout, out_stride, K.fov);
+  } else {
+    tile_out_check<G>(K.P, J.R, W, ox0, oy0, lds, crop_background(K, r, J, PAINT), out, nout, out_stride, K.fov);
   }
-  stage_all<G>(K, J, lds);
-  __syncthreads();
-  raster_emit<G>(K, J, out, nout, out_stride, lds);
 }
 
-// One env per workgroup (G = size / 64 gathers per output row): crop staging,
-// paint in draw order, output. 8 waves at S=256, where the 68 KB crop image
-// leaves 2 workgroups per CU (4 waves each would leave the SIMDs half empty);
-// 4 waves below, where 8 workgroups share a CU. Measured alternatives (two envs
-// per workgroup with the next env's loads in flight, two crop images per
-// workgroup filled by LDS-DMA while the other is written out, a persistent
-// grid, a column-block lane mapping, a byte image of the whole crop, output
-// bands for the byte window) are in DESIGN.md §3. The raster kernels declare no
-// static LDS: the byte window's gathers address the LDS absolutely (from 0).
-__host__ __device__ constexpr int raster_threads(int S) { return S >= 256 ? 512 : 256; }
+// XCD-aware (env, tile) of workgroup w: the dispatcher deals workgroups
+// round-robin over the 8 XCDs (w -> XCD w % 8); env block e / 64 lives in the
+// L2 of XCD (e / 64) % 8 since k_ego (xcd_env_of_wg), so an env's T tiles are
+// dealt to that XCD. Exact for n % 512 == 0, the identity on the tail.
+__device__ __forceinline__ void xcd_tile_of_wg(int w, int n, int T, int* e, int* t) {
+  const int n512 = n & ~511;
+  if (w >= n512 * T) {
+    *e = w / T;
+    *t = w - *e * T;
+    return;
+  }
+  const int x = w & 7, j = w >> 3;
+  const int per = 64 * T;  // tiles of one env block
+  const int blk = j / per, rem = j - blk * per;
+  const int i = rem / T;
+  *t = rem - i * T;
+  *e = 64 * (8 * blk + x) + i;
+}
 
+// One (env, tile) per workgroup; register target from the LDS-limited residency
+// (Tiles::wgs_per_cu workgroups of 4 waves per CU = waves per SIMD). The raster
+// kernels declare no static LDS: the gathers address the LDS absolutely.
 template <int G>
-// waves per EU the register allocation targets: the LDS image already caps a CU
-// at 6 workgroups of 4 waves at S <= 128 (2 of 8 at S = 256), so asking for 6
-// instead of 8 costs no residency and leaves the compiler 80 VGPRs: SGPR spills
-// to VGPR lanes 96 -> 59, config 2 24.68 -> 23.99 us, config 3 25.66 -> 24.94
-#ifndef CBEV_RASTER_WPE
-#define CBEV_RASTER_WPE 6
-#endif
-__global__ __launch_bounds__(raster_threads(64 * G)) __attribute__((amdgpu_waves_per_eu(CBEV_RASTER_WPE)))
-void k_raster(
-    KArgs K, uint8_t* __restrict__ recs, int n, uint8_t* __restrict__ frames) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(Tiles<G>::wgs_per_cu)))
+void k_raster(KArgs K, uint8_t* __restrict__ recs, int n, uint8_t* __restrict__ frames) {
   extern __shared__ __align__(16) uint8_t lds[];
-  constexpr int NT = raster_threads(64 * G);
   CBEV_STAMP(2, 0);
-  const int e = xcd_env_of_wg(blockIdx.x, n);
+  int e, t;
+  xcd_tile_of_wg(blockIdx.x, n, Tiles<G>::T, &e, &t);
   if (e >= n) return;
   const int64_t SS = (int64_t)K.P.size * K.P.size;
   const DRec r = bind_rec(recs + (int64_t)e * K.L.record_bytes, K.L, K.C);
-  RasterJob J;
-  raster_origin<false, G>(K, r, J);
-  raster_rot<false, G>(K, r, J);
-  if constexpr (raster_win8(64 * G)) {
-    if (raster8_env<G, true>(K, recs + (int64_t)e * K.L.record_bytes, J, frames + (int64_t)e * SS, 1, 0, lds)) {
-      CBEV_STAMP(2, 3);
-      return;
-    }
-  }
-  // staging at raised wave priority: the CU's other workgroups are mostly
-  // painting or writing out, and issuing this one's map loads first keeps the
-  // memory pipe busier (raster 25.5 -> 24.9 us at config 2)
-  __builtin_amdgcn_s_setprio(2);
-  J.pq = raster_paint_fetch(r);  // in flight under the staging
-  stage_all<G, NT>(K, J, lds);
-  __builtin_amdgcn_s_setprio(0);
-  __syncthreads();
-  CBEV_STAMP(2, 1);
-  raster_paint<G, NT>(K, r, J.pq, J.xmin, J.ymin, J.shift, lds);
-  CBEV_STAMP(2, 2);
-  raster_emit<G, NT>(K, J, frames + (int64_t)e * SS, 1, 0, lds);
+  const RasterJob J = raster_job<false, G>(K, r);
+  raster_tile<G, true>(K, r, J, t, frames + e * SS, 1, 0, lds);
   CBEV_STAMP(2, 3);
+}
+
+// BaseMap.reset's observation (theta = 0, nothing painted, world.py:92-100) of
+// one record by a 256-thread workgroup, tile by tile, into `nout` frames
+// out + k * out_stride (every slot of the frame-stack ring on reset).
+template <int G>
+__device__ __forceinline__ void raster_reset_env(const KArgs& K, const DRec& r, uint8_t* __restrict__ out, int nout,
+                                                 int64_t out_stride, uint8_t* __restrict__ lds) {
+  const RasterJob J = raster_job<true, G>(K, r);
+  for (int t = 0; t < Tiles<G>::T; ++t) {
+    raster_tile<G, false>(K, r, J, t, out, nout, out_stride, lds);
+    __syncthreads();  // the window is restaged for the next tile
+  }
 }
 
 // Partial reset (SyncVectorEnv.reset with reset_mask -> CarlaBEV.reset):
@@ -2202,7 +1791,6 @@ __global__ __launch_bounds__(256) void k_reset(KArgs K, uint8_t* __restrict__ re
       if (K.stats != nullptr && threadIdx.x == 0) K.stats[e].t0 = (double)wall_clock64();  // episode start
       DRec r = bind_rec((uint8_t*)src, K.L, K.C);  // read-only use below
       raster_reset_env<G>(K, r, ring + (int64_t)e * SS, n_frames, (int64_t)n * SS, lds);
-      __syncthreads();  // the LDS image is reused by the next env
     }
   }
 }
@@ -2218,7 +1806,6 @@ __global__ __launch_bounds__(256) void k_bank_frames(KArgs K, const uint8_t* __r
   for (int b = blockIdx.x; b < n_bank; b += gridDim.x) {
     DRec r = bind_rec((uint8_t*)bank + (int64_t)b * K.L.record_bytes, K.L, K.C);
     raster_reset_env<G>(K, r, frames + b * SS, 1, 0, lds);
-    __syncthreads();
   }
 }
 
@@ -2234,7 +1821,8 @@ __global__ __launch_bounds__(256) void k_bank_frames(KArgs K, const uint8_t* __r
 // XCD's env blocks and counts the selected envs' pieces in env order, taking
 // every WPX-th.
 #define RESET_PU 4                      // 16-byte loads per thread in flight
-#define RESET_LIST_WGS 512              // k_reset_list's grid cap
+#define RESET_MASK_WGS 512              // k_reset_mask's grid cap
+#define CBEV_RESET_MASK_MAX_N (1 << 20)  // k_reset_mask's unit masks: 2 B per 16 envs of LDS
 #define RESET_PIECE (4096 * RESET_PU)   // bytes per piece
 __host__ __device__ __forceinline__ int reset_pieces(int64_t bytes) {
   return (int)((bytes + RESET_PIECE - 1) / RESET_PIECE);
@@ -2306,40 +1894,99 @@ __global__ __launch_bounds__(256) void k_reset_copy(KArgs K, uint8_t* __restrict
 }
 
 // Canonical-loop reset (reset(reset_mask=terminated), tools/debug_env.py:56-132)
-// from the termination list the last k_ego wrote: records[e] <- bank[b] and
-// bank_frames[b] into every frame-stack slot of env e, for the `count` listed
-// envs only (no scan of an n-entry mask). The list is in atomic order, so each
-// env's bank row comes from its rank among the listed env ids: the k-th
-// terminated env in id order takes bank[(cursor + k) % n_bank], which walks the
-// whole bank in order (every reset a distinct scene until it wraps) and does not
-// depend on the order the terminations were appended in. Pieces as in
-// k_reset_copy (16 KB, RESET_PU loads per thread in flight), dealt over the grid.
-// The leading scalar arguments are preloaded into SGPRs by the launch (kernarg
-// preloading): the count load is issued at wave start.
-__global__ __launch_bounds__(256) void k_reset_list(const uint32_t* __restrict__ count,
-                                                    const int32_t* __restrict__ list,
-                                                    const unsigned long long* __restrict__ cursor, int n, int n_bank,
-                                                    int rb, int SS, int n_frames, uint8_t* __restrict__ recs,
-                                                    const uint8_t* __restrict__ bank,
-                                                    const uint8_t* __restrict__ bank_frames, uint8_t* __restrict__ ring,
-                                                    KArgs K) {
-  const unsigned long long cur = *cursor;
-  const int cnt = min((int)__builtin_amdgcn_readfirstlane(*count), n);
-  asm volatile("" ::"s"(cur), "s"(cnt));  // the cursor loaded beside the count (one wait)
-  if (cnt == 0) return;
-  const int pf = reset_pieces(SS), ppe = pf + reset_pieces(rb);
-  const int total = cnt * ppe;
-  if ((int)blockIdx.x >= total) return;
-  for (int p = blockIdx.x; p < total; p += gridDim.x) {
-    const int slot = p / ppe, c = p - slot * ppe;
-    const int e = list[slot];
-    // rank of e among the listed ids (ids are distinct: one append per terminated env)
-    int rank = 0;
-    for (int j0 = 0; j0 < cnt; j0 += 256) {
-      const int j = j0 + (int)threadIdx.x;
-      rank += __syncthreads_count(j < cnt && list[j] < e);
+// from a bank with cached reset frames: every env with mask[e] != 0 takes the
+// next bank row in env-id order, bank[(cursor + k) % n_bank] for the k-th
+// selected env, so consecutive resets walk the whole bank (every reset a
+// distinct scene until it wraps) whatever order the kernels ran in. The mask is
+// read when the reset runs (cbev_reset_terminated passes the last step's term
+// buffer, so in-place edits of it between the step and the reset count).
+// Ranking, once per workgroup and independent of how many envs are selected:
+// the mask is cut into 16-byte units, each thread takes `upt` consecutive
+// units (16-byte loads, all in flight), keeps each unit's nonzero bits in LDS
+// and its count; one workgroup exclusive scan gives every thread's first slot.
+// Piece p of slot s = p / ppe then finds its env by a binary search over the
+// 256 thread prefixes, the unit within the thread and the set bit within the
+// unit: O(n / 4096 + log) per workgroup, no pass over the selected envs per
+// piece. Pieces as in k_reset_copy (16 KB, RESET_PU loads per thread in
+// flight), dealt over the grid. The cursor is double-buffered by call parity:
+// every workgroup reads cursor_in, workgroup 0 writes cursor_out = cursor_in +
+// the selected count (the next call reads it), so rows advance only when a
+// reset actually ran. The leading scalar arguments are preloaded into SGPRs.
+__device__ __forceinline__ uint32_t nonzero_bytes16(const uint4 v) {  // bit b: byte b of the 16 is nonzero
+  uint32_t m = 0;
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint32_t y = (((w[k] & 0x7f7f7f7fu) + 0x7f7f7f7fu) | w[k]) & 0x80808080u;  // bit 7 of each nonzero byte
+    m |= (((y >> 7) & 1u) | ((y >> 14) & 2u) | ((y >> 21) & 4u) | ((y >> 28) & 8u)) << (4 * k);
+  }
+  return m;
+}
+
+__global__ __launch_bounds__(256) void k_reset_mask(int n, int n_bank, int rb, int SS, int n_frames, int upt,
+                                                    const uint8_t* __restrict__ mask,
+                                                    const unsigned long long* __restrict__ cursor_in,
+                                                    unsigned long long* __restrict__ cursor_out,
+                                                    uint8_t* __restrict__ recs, const uint8_t* __restrict__ bank,
+                                                    const uint8_t* __restrict__ bank_frames,
+                                                    uint8_t* __restrict__ ring, KArgs K) {
+  extern __shared__ __align__(16) uint8_t lds[];
+  int* pre = (int*)lds;                      // [256] exclusive prefix of the threads' counts, [256] = total
+  int* wsum = pre + 257;                     // [4] wave totals
+  uint16_t* um = (uint16_t*)(lds + 1056);    // [256 * upt] unit masks
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const unsigned long long cur = *cursor_in;  // loaded beside the mask
+  const int nu = (n + 15) >> 4;               // 16-byte units
+  const bool vec = ((uintptr_t)mask & 15u) == 0;
+  int cnt = 0;
+  for (int k = 0; k < upt; ++k) {
+    const int u = tid * upt + k;
+    uint32_t m = 0;
+    if (u < nu) {
+      if (vec && 16 * u + 16 <= n) {
+        m = nonzero_bytes16(*(const uint4*)(mask + 16 * (int64_t)u));
+      } else {
+        for (int b = 0; b < 16; ++b)
+          if (16 * u + b < n && mask[16 * (int64_t)u + b] != 0) m |= 1u << b;
+      }
     }
-    const int b = (int)((cur + (unsigned long long)rank) % (unsigned long long)n_bank);
+    um[u] = (uint16_t)m;
+    cnt += __popc(m);
+  }
+  // workgroup exclusive scan of cnt (wave inclusive scan by shuffles, then the wave totals)
+  int inc = cnt;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int o = __shfl_up(inc, d, 64);
+    if (lane >= d) inc += o;
+  }
+  if (lane == 63) wsum[wave] = inc;
+  __syncthreads();
+  int wpre = 0;
+  for (int w = 0; w < wave; ++w) wpre += wsum[w];
+  pre[tid] = wpre + inc - cnt;
+  const int total = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+  if (blockIdx.x == 0 && tid == 0) *cursor_out = cur + (unsigned long long)total;
+  __syncthreads();
+  const int pf = reset_pieces(SS), ppe = pf + reset_pieces(rb);
+  const int pieces = total * ppe;
+  for (int p = blockIdx.x; p < pieces; p += gridDim.x) {
+    const int slot = p / ppe, c = p - slot * ppe;
+    // the thread whose slots hold `slot`: the last t with pre[t] <= slot
+    int lo = 0, hi = 255;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (pre[mid] <= slot) lo = mid;
+      else hi = mid - 1;
+    }
+    int j = slot - pre[lo], u = lo * upt;
+    uint32_t m = um[u];
+    for (int pc = __popc(m); j >= pc; pc = __popc(m)) {
+      j -= pc;
+      m = um[++u];
+    }
+    const int e = 16 * u + nth_set_bit(m, j);
+    const int b = (int)((cur + (unsigned long long)slot) % (unsigned long long)n_bank);
     const bool fr = c < pf;  // uniform
     const uint8_t* src = fr ? bank_frames + (int64_t)b * SS : bank + (int64_t)b * rb;
     uint8_t* dst = fr ? ring + (int64_t)e * SS : recs + (int64_t)e * rb;
@@ -2347,25 +1994,28 @@ __global__ __launch_bounds__(256) void k_reset_list(const uint32_t* __restrict__
     const int64_t o0 = (int64_t)(fr ? c : c - pf) * RESET_PIECE + 16 * (int64_t)threadIdx.x;
     uint4 v[RESET_PU];
 #pragma unroll
-    for (int j = 0; j < RESET_PU; ++j) {
-      const int64_t o = o0 + 4096 * j;
-      v[j] = *(const uint4*)(src + (o < lim ? o : 0));
+    for (int q = 0; q < RESET_PU; ++q) {
+      const int64_t o = o0 + 4096 * q;
+      v[q] = *(const uint4*)(src + (o < lim ? o : 0));
     }
 #pragma unroll
-    for (int j = 0; j < RESET_PU; ++j) asm volatile("" ::"v"(v[j].x), "v"(v[j].y), "v"(v[j].z), "v"(v[j].w));
+    for (int q = 0; q < RESET_PU; ++q) asm volatile("" ::"v"(v[q].x), "v"(v[q].y), "v"(v[q].z), "v"(v[q].w));
 #pragma unroll
-    for (int j = 0; j < RESET_PU; ++j) {
-      const int64_t o = o0 + 4096 * j;
+    for (int q = 0; q < RESET_PU; ++q) {
+      const int64_t o = o0 + 4096 * q;
       if (o >= lim) continue;
       if (fr) {
-        for (int f = 0; f < n_frames; ++f) *(uint4*)(dst + (int64_t)f * n * SS + o) = v[j];
+        for (int f = 0; f < n_frames; ++f) *(uint4*)(dst + (int64_t)f * n * SS + o) = v[q];
       } else {
-        *(uint4*)(dst + o) = v[j];
+        *(uint4*)(dst + o) = v[q];
       }
     }
     if (c == pf && threadIdx.x == 0 && K.stats != nullptr) K.stats[e].t0 = (double)wall_clock64();
   }
 }
+// k_reset_mask's dynamic LDS: prefixes + wave totals (1056 B) + the unit masks
+__host__ __forceinline__ int reset_mask_upt(int n) { return ((n + 15) / 16 + 255) / 256; }
+__host__ __forceinline__ size_t reset_mask_lds(int n) { return 1056 + 2 * 256 * (size_t)reset_mask_upt(n); }
 
 // ============================================================== collision / reward (k_ego S5-S6)
 // squared distance from (x, y) to raw-route segment i (carl_reward_fn.py:36-48)
@@ -2763,7 +2413,6 @@ __device__ __forceinline__ void collide_env(const KArgs& K, DRec r, int e, const
   if (terminal) {
     atomicAdd(K.nterm, 1ull);
     if (K.stats != nullptr) d_episode_summary(K, r, e);
-    if (K.tl_list != nullptr) K.tl_list[atomicAdd(K.tl_count, 1u)] = e;  // cbev_reset_terminated's list
   }
   reward_out[e] = reward;
   term_out[e] = (uint8_t)terminal;
@@ -2862,16 +2511,35 @@ __global__ __launch_bounds__(256) void k_ego(uint8_t* __restrict__ recs, int n, 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   auto rec = [&](int k) { return bind_ego(lds + k * pk.bytes, recs + (int64_t)(e0 + k) * rb, K, pk); };
-  if (blockIdx.x == 0 && tid == 0) {
-    if (K.ep_count_next != nullptr) *K.ep_count_next = 0;
-    if (K.tl_count_next != nullptr) {  // the previous step's resets took bank rows [cursor, cursor + count)
-      *K.tl_cursor += *K.tl_count_next;
-      *K.tl_count_next = 0;
+  if (blockIdx.x == 0 && tid == 0 && K.ep_count_next != nullptr) *K.ep_count_next = 0;
+  // S2 + S1 under the staging (waves 0 and 1 issue none of it, so their loads
+  // are waited for precisely while the LDS-DMA of waves 2 and 3 stays in
+  // flight). S2's inputs come from HBM into registers, issued first: the pose,
+  // the route length and S2_PF route points per thread (128 / ne threads per
+  // env: the first 64 points at 16 envs per workgroup, 128 at 8; points beyond
+  // are loaded in the loop); each of an env's threads computes the yaw's cos /
+  // sin itself (the same d_sincos as S1), so S2 needs no barrier before it and
+  // runs under the staging instead of after it.
+  constexpr int S2_PF = 8;
+  const int tpe2 = 128 / ne, s2k = tid / tpe2, s2sub = tid - s2k * tpe2;
+  const bool s2 = wave <= 1 && s2k < ne_eff;
+  double s2x[S2_PF], s2y[S2_PF], s2hx = 0.0, s2hy = 0.0, s2yaw = 0.0;
+  int s2nr = 0;
+  const DRec s2g = bind_rec(recs + (int64_t)(e0 + (s2 ? s2k : 0)) * rb, K.L, K.C);
+  if (s2) {
+    s2hx = s2g.hd[CBEV_HD_X];
+    s2hy = s2g.hd[CBEV_HD_Y];
+    s2yaw = s2g.hd[CBEV_HD_YAW];
+    s2nr = s2g.hi[CBEV_HI_NROUTE];
+#pragma unroll
+    for (int j = 0; j < S2_PF; ++j) {  // index clamped to the route capacity: no branch around a load
+      const int i = min(s2sub + j * tpe2, K.C.route_cap - 1);
+      s2x[j] = s2g.cx[i];
+      s2y[j] = s2g.cy[i];
     }
   }
-  // S1 under the staging (waves 0 and 1 issue none of it): the actions, and
-  // from the record's yaw and speed cos / sin of the yaw (wave 0, which runs the
-  // chain) beside tan(clip(delta)) (wave 1)
+  // S1: the actions, and from the record's yaw and speed cos / sin of the yaw
+  // (wave 0, which runs the chain) beside tan(clip(delta)) (wave 1)
   float ag = 0.f, asa = 0.f, ab = 0.f;
   if (wave <= 1 && lane < ne_eff) {
     d_decode_action(K, actions, e0 + lane, &ag, &asa, &ab);
@@ -2897,46 +2565,49 @@ __global__ __launch_bounds__(256) void k_ego(uint8_t* __restrict__ recs, int n, 
     pav = RAD(g, CBEV_AD_V, a);
     pasz = RAI(g, CBEV_AI_SIZE, a);
   }
-  __syncthreads();
-  CBEV_STAMP(0, 1);
   CBEV_STAMP(3, 1);
-  // S2
-  {
-    const int tpe = 256 / ne, k = tid / tpe, sub = tid - k * tpe;
-    if (k < ne_eff) {
-      const uint8_t* base = lds + k * pk.bytes;
-      const double* hd = (const double*)(base + K.L.hd);
-      const double* cx = (const double*)(base + K.L.cx);
-      const double* cy = (const double*)(base + K.L.cy);
-      const int nr = ((const int32_t*)(base + K.L.hi))[CBEV_HI_NROUTE];
-      const double fx = hd[CBEV_HD_X] + CB_WHEELBASE * pre[k].cyaw;
-      const double fy = hd[CBEV_HD_Y] + CB_WHEELBASE * pre[k].syaw;
-      // np.argmin(np.hypot(dx, dy)): the first smallest hypot, in one pass
-      double bd = INFINITY;
-      int bi = 0x7fffffff;
-#pragma unroll 4
-      for (int i = sub; i < nr; i += tpe) {
-        const double h = hypot(fx - cx[i], fy - cy[i]);
+  // S2: Controller.calc_target_index (stanley_controller.py:51-62),
+  // np.argmin(np.hypot(dx, dy)): the first smallest hypot, in one pass
+  if (s2) {
+    double syaw, cyaw;
+    d_sincos(s2yaw, &syaw, &cyaw);
+    const double fx = s2hx + CB_WHEELBASE * cyaw;
+    const double fy = s2hy + CB_WHEELBASE * syaw;
+    double bd = INFINITY;
+    int bi = 0x7fffffff;
+#pragma unroll
+    for (int j = 0; j < S2_PF; ++j) {
+      const int i = s2sub + j * tpe2;
+      if (i < s2nr) {
+        const double h = hypot(fx - s2x[j], fy - s2y[j]);
         if (h < bd) {  // first minimum within this thread's (increasing) indices; NaN never wins
           bd = h;
           bi = i;
         }
       }
-      CBEV_STAMP(3, 2);
-      butterfly(tpe, [&](auto off) {  // smallest hypot, lowest index on ties
-        constexpr int O = decltype(off)::value;
-        const double qd = peer_f64<O>(bd);
-        const int qi = peer_i32<O>(bi);
-        if (qd < bd || (qd == bd && qi < bi)) {
-          bd = qd;
-          bi = qi;
-        }
-      });
-      if (sub == 0) best[k] = bi == 0x7fffffff ? 0 : bi;
     }
+    for (int i = s2sub + S2_PF * tpe2; i < s2nr; i += tpe2) {  // routes past the prefetched points
+      const double h = hypot(fx - s2g.cx[i], fy - s2g.cy[i]);
+      if (h < bd) {
+        bd = h;
+        bi = i;
+      }
+    }
+    CBEV_STAMP(3, 2);
+    butterfly(tpe2, [&](auto off) {  // smallest hypot, lowest index on ties
+      constexpr int O = decltype(off)::value;
+      const double qd = peer_f64<O>(bd);
+      const int qi = peer_i32<O>(bi);
+      if (qd < bd || (qd == bd && qi < bi)) {
+        bd = qd;
+        bi = qi;
+      }
+    });
+    if (s2sub == 0) best[s2k] = bi == 0x7fffffff ? 0 : bi;
   }
   CBEV_STAMP(3, 3);
-  __syncthreads();
+  __syncthreads();  // the staging has landed; S1 / S2 results in LDS
+  CBEV_STAMP(0, 1);
   CBEV_STAMP(0, 2);
   // S3
   if (tid < ne_eff) {
@@ -3437,8 +3108,10 @@ struct cbev_ctx {
   int device;
   uint8_t* map_dev;
   int64_t map_bytes;
-  uint8_t* map8_dev;  // byte map (byte-image raster staging)
+  uint8_t* map8_dev;  // byte map (the raster's window staging)
   int p8;
+  uint8_t* map8T_dev;  // the byte map transposed (windows of tiles whose output rows run along crop columns)
+  int p8T;
   uint32_t* lut_dev;  // 16 entries
   int prof_on;
   int64_t prof_n;
@@ -3458,19 +3131,18 @@ struct cbev_ctx {
   int ep_ring, ep_n;
   int64_t step_count;         // cbev_step calls since cbev_set_episode_stats
   double tick_s;
-  // termination list of the last cbev_step (cbev_reset_terminated)
-  int32_t* tl_list_dev;       // [tl_cap]
-  int tl_cap;
-  uint32_t* tl_count_dev;     // [2]: step parity
-  unsigned long long* tl_cursor_dev;
-  int tl_parity;              // counter the next cbev_step appends to
-  int tl_last_n;              // n of the last cbev_step (0: none yet)
+  // bank cursor of cbev_reset_masked, double-buffered by call parity: [cur_parity]
+  // holds the rows taken so far, the next call writes the other one
+  unsigned long long* cur_dev;  // [2]
+  int cur_parity;
+  const uint8_t* last_term;   // term buffer of the last cbev_step (cbev_reset_terminated's mask)
+  int last_n;                 // n of the last cbev_step (0: none yet)
 };
 
 // Envs per k_ego workgroup: small groups spread the record staging (LDS-DMA
 // throughput is per CU) and the chains over more CUs; the largest divisor of 64
 // not above CBEV_EGO_NE (default below) whose LDS fits the budget. Never fewer
-// than 4: the element loops of S2 / S5 give each env 256 / ne threads and reduce
+// than 4: the element loops of S5 (S2) give each env 256 / ne (128 / ne) threads and reduce
 // them with wave shuffles, which do not cross a 64-lane wave (ne >= 4 keeps an
 // env's threads inside one wave). Returns 0 when 4 envs do not fit.
 static int ego_ne_for(int per_env, int actor_cap) {
@@ -3565,6 +3237,8 @@ static KArgs kargs(const cbev_ctx* c) {
   K.npitch = c->npitch;
   K.map8 = c->map8_dev;
   K.p8 = c->p8;
+  K.map8T = c->map8T_dev;
+  K.p8T = c->p8T;
   K.fov = (const uint32_t*)c->fov_dev;
   K.err = c->err_dev;
   K.nterm = c->nterm_dev;
@@ -3572,9 +3246,6 @@ static KArgs kargs(const cbev_ctx* c) {
   K.ep_rows = nullptr;
   K.ep_count = K.ep_count_next = nullptr;
   K.tick_s = c->tick_s;
-  K.tl_list = nullptr;
-  K.tl_count = K.tl_count_next = nullptr;
-  K.tl_cursor = c->tl_cursor_dev;
   return K;
 }
 
@@ -3592,14 +3263,17 @@ static const void* bank_frames_kernel(int size) {
 static const void* reset_kernel(int size) {
   return size == 64 ? (const void*)k_reset<1> : size == 128 ? (const void*)k_reset<2> : (const void*)k_reset<4>;
 }
-static size_t raster_lds_bytes(const cbev_params& P) { return (size_t)raster_image_bytes(P.size, P.crop); }
+static size_t raster_lds_bytes(const cbev_params& P) {
+  return P.size == 64 ? Tiles<1>::lds_bytes : P.size == 128 ? Tiles<2>::lds_bytes : Tiles<4>::lds_bytes;
+}
+static int raster_tiles(int size) { return size == 64 ? Tiles<1>::T : size == 128 ? Tiles<2>::T : Tiles<4>::T; }
 // One step's observation for n records: one workgroup per env.
 static void launch_raster(const cbev_ctx* c, const KArgs& K, void* records, int n, uint8_t* frames, hipStream_t s) {
   const size_t lb = raster_lds_bytes(c->P);
   switch (c->P.size) {
-    case 64: hipLaunchKernelGGL(k_raster<1>, dim3(n), dim3(raster_threads(64)), lb, s, K, (uint8_t*)records, n, frames); break;
-    case 128: hipLaunchKernelGGL(k_raster<2>, dim3(n), dim3(raster_threads(128)), lb, s, K, (uint8_t*)records, n, frames); break;
-    default: hipLaunchKernelGGL(k_raster<4>, dim3(n), dim3(raster_threads(256)), lb, s, K, (uint8_t*)records, n, frames); break;
+    case 64: hipLaunchKernelGGL(k_raster<1>, dim3(n * Tiles<1>::T), dim3(256), lb, s, K, (uint8_t*)records, n, frames); break;
+    case 128: hipLaunchKernelGGL(k_raster<2>, dim3(n * Tiles<2>::T), dim3(256), lb, s, K, (uint8_t*)records, n, frames); break;
+    default: hipLaunchKernelGGL(k_raster<4>, dim3(n * Tiles<4>::T), dim3(256), lb, s, K, (uint8_t*)records, n, frames); break;
   }
 }
 
@@ -3674,10 +3348,8 @@ int cbev_create(const cbev_params* params, const cbev_caps* caps, int device, cb
   if (e == hipSuccess) e = hipMemset(c->err_dev, 0, sizeof(int32_t));
   if (e == hipSuccess) e = hipMalloc(&c->nterm_dev, sizeof(unsigned long long));
   if (e == hipSuccess) e = hipMemset(c->nterm_dev, 0, sizeof(unsigned long long));
-  if (e == hipSuccess) e = hipMalloc(&c->tl_count_dev, 2 * sizeof(uint32_t));
-  if (e == hipSuccess) e = hipMemset(c->tl_count_dev, 0, 2 * sizeof(uint32_t));
-  if (e == hipSuccess) e = hipMalloc(&c->tl_cursor_dev, sizeof(unsigned long long));
-  if (e == hipSuccess) e = hipMemset(c->tl_cursor_dev, 0, sizeof(unsigned long long));
+  if (e == hipSuccess) e = hipMalloc(&c->cur_dev, 2 * sizeof(unsigned long long));
+  if (e == hipSuccess) e = hipMemset(c->cur_dev, 0, 2 * sizeof(unsigned long long));
   if (e == hipSuccess) {
     int khz = 0;  // wall_clock64() rate
     e = hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device);
@@ -3694,6 +3366,9 @@ int cbev_create(const cbev_params* params, const cbev_caps* caps, int device, cb
     e = hipFuncSetAttribute(raster_kernel(P.size), hipFuncAttributeMaxDynamicSharedMemorySize, (int)raster_lds_bytes(P));
   if (e == hipSuccess)
     e = hipFuncSetAttribute(reset_kernel(P.size), hipFuncAttributeMaxDynamicSharedMemorySize, (int)raster_lds_bytes(P));
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute((const void*)k_reset_mask, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)reset_mask_lds(CBEV_RESET_MASK_MAX_N));
   if (e == hipSuccess)
     e = hipFuncSetAttribute(bank_frames_kernel(P.size), hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)raster_lds_bytes(P));
@@ -3743,6 +3418,7 @@ int cbev_wall_clock_hz(const cbev_ctx* c, double* hz) {
 int cbev_termination_count(cbev_ctx* c, int64_t* count) {
   if (!c || !count) return set_err(CBEV_EINVAL, "null argument");
   HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipDeviceSynchronize());  // k_ego's counts are queued on the caller's (non-blocking) stream
   unsigned long long v = 0;
   HIP_TRY(hipMemcpy(&v, c->nterm_dev, sizeof v, hipMemcpyDeviceToHost));
   *count = (int64_t)v;
@@ -3752,6 +3428,7 @@ int cbev_termination_count(cbev_ctx* c, int64_t* count) {
 int cbev_error_flags(cbev_ctx* c, int32_t* flags, int clear) {
   if (!c || !flags) return set_err(CBEV_EINVAL, "null argument");
   HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipDeviceSynchronize());
   HIP_TRY(hipMemcpy(flags, c->err_dev, sizeof(int32_t), hipMemcpyDeviceToHost));
   if (clear && *flags) HIP_TRY(hipMemset(c->err_dev, 0, sizeof(int32_t)));
   return CBEV_OK;
@@ -3818,12 +3495,11 @@ void cbev_destroy(cbev_ctx* c) {
   }
   if (c->map_dev) (void)hipFree(c->map_dev);
   if (c->map8_dev) (void)hipFree(c->map8_dev);
+  if (c->map8T_dev) (void)hipFree(c->map8T_dev);
   if (c->lut_dev) (void)hipFree(c->lut_dev);
   if (c->err_dev) (void)hipFree(c->err_dev);
   if (c->nterm_dev) (void)hipFree(c->nterm_dev);
-  if (c->tl_list_dev) (void)hipFree(c->tl_list_dev);
-  if (c->tl_count_dev) (void)hipFree(c->tl_count_dev);
-  if (c->tl_cursor_dev) (void)hipFree(c->tl_cursor_dev);
+  if (c->cur_dev) (void)hipFree(c->cur_dev);
   if (c->area_dev) (void)hipFree(c->area_dev);
   if (c->fov_dev) (void)hipFree(c->fov_dev);
   free(c);
@@ -3863,6 +3539,17 @@ int cbev_set_map(cbev_ctx* c, const uint8_t* map_host, int64_t bytes) {
   HIP_TRY(hipMemset(c->map8_dev, 0, (size_t)p8 * H + 4096));
   HIP_TRY(hipMemcpy(c->map8_dev, map8.data(), (size_t)p8 * H, hipMemcpyHostToDevice));
   c->p8 = p8;
+  // and transposed (row x = map column x), with the same slack
+  const int p8T = (H + 64 + 63) & ~63;
+  std::vector<uint8_t> map8T((size_t)p8T * W, 0);
+  for (int y = 0; y < H; ++y)
+    for (int x = 0; x < W; ++x) map8T[(size_t)x * p8T + y] = map_host[(size_t)y * pitch + x];
+  if (c->map8T_dev) HIP_TRY(hipFree(c->map8T_dev));
+  c->map8T_dev = nullptr;
+  HIP_TRY(hipMalloc(&c->map8T_dev, (size_t)p8T * W + 4096));
+  HIP_TRY(hipMemset(c->map8T_dev, 0, (size_t)p8T * W + 4096));
+  HIP_TRY(hipMemcpy(c->map8T_dev, map8T.data(), (size_t)p8T * W, hipMemcpyHostToDevice));
+  c->p8T = p8T;
   return CBEV_OK;
 }
 
@@ -3874,21 +3561,10 @@ int cbev_step(cbev_ctx* c, void* records, int n, const void* actions, uint8_t* f
   if (n <= 0) return CBEV_OK;
   // every argument check before the first launch, so an error leaves the records untouched
   if (c->stats && n > c->ep_n) return set_err(CBEV_EINVAL, "n %d exceeds the %d envs of the episode stats", n, c->ep_n);
-  if (n > c->tl_cap) {  // the termination list holds one entry per env (grows once; synchronises)
-    HIP_TRY(hipSetDevice(c->device));
-    if (c->tl_list_dev) HIP_TRY(hipFree(c->tl_list_dev));
-    c->tl_list_dev = nullptr;
-    c->tl_cap = 0;
-    HIP_TRY(hipMalloc(&c->tl_list_dev, (size_t)n * sizeof(int32_t)));
-    c->tl_cap = n;
-  }
   hipStream_t s = (hipStream_t)stream;
   KArgs K = kargs(c);
-  K.tl_list = c->tl_list_dev;
-  K.tl_count = c->tl_count_dev + c->tl_parity;
-  K.tl_count_next = c->tl_count_dev + (c->tl_parity ^ 1);
-  c->tl_parity ^= 1;
-  c->tl_last_n = n;
+  c->last_term = term;
+  c->last_n = n;
   const int wg4 = (n + 3) / 4;
   hipEvent_t* ev = nullptr;
   if (c->prof_on && c->prof_n < CBEV_PROF_MAX) ev = c->prof_ev + 4 * c->prof_n++;
@@ -3973,35 +3649,44 @@ int cbev_reset_frames(cbev_ctx* c, void* records, int n, const void* bank, int n
   return CBEV_OK;
 }
 
-int cbev_reset_terminated(cbev_ctx* c, void* records, int n, const void* bank, int n_bank, const uint8_t* bank_frames,
-                          uint8_t* frames, int n_frames, void* stream) {
-  if (!c || !records || !bank || !bank_frames || !frames) return set_err(CBEV_EINVAL, "null argument");
+int cbev_reset_masked(cbev_ctx* c, void* records, int n, const uint8_t* mask, const void* bank, int n_bank,
+                      const uint8_t* bank_frames, uint8_t* frames, int n_frames, void* stream) {
+  if (!c || !records || !mask || !bank || !bank_frames || !frames) return set_err(CBEV_EINVAL, "null argument");
   if (n_bank <= 0) return set_err(CBEV_EINVAL, "empty bank");
   if (n_frames < 1) return set_err(CBEV_EINVAL, "n_frames < 1");
-  if (c->tl_last_n == 0) return set_err(CBEV_ESTATE, "cbev_reset_terminated before any cbev_step");
-  if (n != c->tl_last_n) return set_err(CBEV_EINVAL, "n %d != the %d envs of the last cbev_step", n, c->tl_last_n);
+  if (n > CBEV_RESET_MASK_MAX_N) return set_err(CBEV_EINVAL, "n %d exceeds %d", n, CBEV_RESET_MASK_MAX_N);
+  if (n <= 0) return CBEV_OK;
   KArgs K = kargs(c);
-  const int64_t ppe = reset_pieces((int64_t)c->P.size * c->P.size) + reset_pieces(c->L.record_bytes);
+  const int SS = c->P.size * c->P.size;
+  const int64_t ppe = reset_pieces((int64_t)SS) + reset_pieces(c->L.record_bytes);
   const int64_t pieces = (int64_t)n * ppe;
-  const int grid = pieces >= RESET_LIST_WGS ? RESET_LIST_WGS : (int)pieces;
-  // the counter the last cbev_step appended to (parity flipped after it)
-  const uint32_t* cnt = c->tl_count_dev + (c->tl_parity ^ 1);
-  hipLaunchKernelGGL(k_reset_list, dim3(grid), dim3(256), 0, (hipStream_t)stream, cnt, (const int32_t*)c->tl_list_dev,
-                     (const unsigned long long*)c->tl_cursor_dev, n, n_bank, (int)c->L.record_bytes,
-                     c->P.size * c->P.size, n_frames, (uint8_t*)records, (const uint8_t*)bank, bank_frames, frames, K);
+  const int grid = pieces >= RESET_MASK_WGS ? RESET_MASK_WGS : (int)pieces;
+  const int upt = reset_mask_upt(n);
+  const unsigned long long* cin = c->cur_dev + c->cur_parity;
+  unsigned long long* cout = c->cur_dev + (c->cur_parity ^ 1);
+  hipLaunchKernelGGL(k_reset_mask, dim3(grid), dim3(256), reset_mask_lds(n), (hipStream_t)stream, n, n_bank,
+                     (int)c->L.record_bytes, SS, n_frames, upt, mask, cin, cout, (uint8_t*)records,
+                     (const uint8_t*)bank, bank_frames, frames, K);
   HIP_TRY(hipGetLastError());
+  c->cur_parity ^= 1;
   return CBEV_OK;
+}
+
+int cbev_reset_terminated(cbev_ctx* c, void* records, int n, const void* bank, int n_bank, const uint8_t* bank_frames,
+                          uint8_t* frames, int n_frames, void* stream) {
+  if (!c) return set_err(CBEV_EINVAL, "null argument");
+  if (c->last_n == 0) return set_err(CBEV_ESTATE, "cbev_reset_terminated before any cbev_step");
+  if (n != c->last_n) return set_err(CBEV_EINVAL, "n %d != the %d envs of the last cbev_step", n, c->last_n);
+  return cbev_reset_masked(c, records, n, c->last_term, bank, n_bank, bank_frames, frames, n_frames, stream);
 }
 
 int cbev_bank_cursor(cbev_ctx* c, int64_t* cursor) {
   if (!c || !cursor) return set_err(CBEV_EINVAL, "null argument");
   HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipDeviceSynchronize());  // the resets are queued on the caller's (non-blocking) stream
   unsigned long long v = 0;
-  HIP_TRY(hipMemcpy(&v, c->tl_cursor_dev, sizeof v, hipMemcpyDeviceToHost));
-  uint32_t cnt[2] = {0, 0};
-  HIP_TRY(hipMemcpy(cnt, c->tl_count_dev, sizeof cnt, hipMemcpyDeviceToHost));
-  // rows taken so far: the folded cursor + the last step's list (taken if it was reset)
-  *cursor = (int64_t)(v + cnt[c->tl_parity ^ 1]);
+  HIP_TRY(hipMemcpy(&v, c->cur_dev + c->cur_parity, sizeof v, hipMemcpyDeviceToHost));
+  *cursor = (int64_t)v;
   return CBEV_OK;
 }
 
@@ -4101,6 +3786,8 @@ static void area_tab(int ssize, int dsize, double scale, std::vector<int32_t>& o
 
 int cbev_pack_frames(cbev_ctx* c, const uint8_t* frames, int n, uint8_t* packed, void* stream) {
   if (!c || !frames || !packed) return set_err(CBEV_EINVAL, "null argument");
+  // 16-byte loads of the ids, 8-byte stores of the packed bytes
+  if (((uintptr_t)frames & 15) || ((uintptr_t)packed & 7)) return set_err(CBEV_EINVAL, "misaligned frames / packed");
   if (n <= 0) return CBEV_OK;
   const int64_t n16 = (int64_t)n * c->P.size * c->P.size / 16;  // S is a multiple of 64
   const int grid = (int)std::min<int64_t>((n16 + 255) / 256, 8192);
@@ -4111,6 +3798,7 @@ int cbev_pack_frames(cbev_ctx* c, const uint8_t* frames, int n, uint8_t* packed,
 
 int cbev_unpack_frames(cbev_ctx* c, const uint8_t* packed, int n, uint8_t* frames, void* stream) {
   if (!c || !frames || !packed) return set_err(CBEV_EINVAL, "null argument");
+  if (((uintptr_t)frames & 15) || ((uintptr_t)packed & 7)) return set_err(CBEV_EINVAL, "misaligned frames / packed");
   if (n <= 0) return CBEV_OK;
   const int64_t n16 = (int64_t)n * c->P.size * c->P.size / 16;
   const int grid = (int)std::min<int64_t>((n16 + 255) / 256, 8192);

@@ -25,8 +25,10 @@ struct KArgs {
   const uint8_t* map;  // padded class map, nibble-packed: render_h rows x npitch bytes,
                        // texel x of a row in byte x >> 1, high nibble when x is odd
   int npitch;
-  const uint8_t* map8;  // the same map, one palette id per byte (p8 bytes per row): the byte-image raster stages it
+  const uint8_t* map8;  // the same map, one palette id per byte (p8 bytes per row): the raster stages it
   int p8;
+  const uint8_t* map8T;  // map8 transposed (p8T bytes per map column): windows of transposed tiles
+  int p8T;
   const uint32_t* fov;  // FOV corner mask, S*S bytes (0xff = black), or null (fov_masked off)
   int32_t* err;         // device error word (CBEV_ERR_* bits, read by cbev_error_flags)
   unsigned long long* nterm;  // terminations since cbev_create (cbev_termination_count)
@@ -36,14 +38,6 @@ struct KArgs {
   int32_t* ep_count;          // this step's row count (zeroed by the step before)
   int32_t* ep_count_next;     // the next step's row count, zeroed by this step
   double tick_s;              // seconds per wall_clock64() tick
-  // termination list (cbev_reset_terminated): k_ego appends each env that
-  // terminates to tl_list (tl_count entries); block 0 first folds the previous
-  // step's count into the bank cursor and zeroes it (tl_count_next, the counter
-  // the next step appends to). Null: off.
-  int32_t* tl_list;
-  uint32_t* tl_count;
-  uint32_t* tl_count_next;
-  unsigned long long* tl_cursor;
 };
 
 // class id of padded-map texel (x, y)

@@ -87,6 +87,13 @@ class ScenePool:
         for p in self._procs:
             p.start()
 
+    def request_gids(self, gids):
+        """Queue scenes for explicit global ids (in batches)."""
+        gids = [int(g) for g in gids]
+        for i in range(0, len(gids), self.batch):
+            self._tasks.put(gids[i:i + self.batch])
+            self.requested += len(gids[i:i + self.batch])
+
     def request(self, n: int):
         """Queue n more scenes (in batches)."""
         while n > 0:
@@ -126,3 +133,31 @@ class ScenePool:
             p.join(timeout=10)
             if p.is_alive():
                 p.terminate()
+
+
+def build_scenes(cfg_dict: dict, caps: dict, difficulty: str, seed0: int, record_bytes: int, gids,
+                 workers: int = 8, timeout: float = 1800.0) -> np.ndarray:
+    """Packed records of the scenes of `gids` (uint8[len(gids)][record_bytes], in
+    gid order), built by `workers` spawned processes: the same bytes the
+    in-process HostResetBuilder writes (tests/test_scene_pool.py)."""
+    gids = [int(g) for g in gids]
+    out = np.zeros((len(gids), record_bytes), np.uint8)
+    if not gids:
+        return out
+    where = {g: i for i, g in enumerate(gids)}
+    pool = ScenePool(cfg_dict, caps, difficulty, seed0, record_bytes, workers=max(1, workers),
+                     batch=max(1, min(64, len(gids) // (4 * max(1, workers)) or 1)))
+    try:
+        pool.request_gids(gids)
+        done = 0
+        deadline = time.perf_counter() + timeout
+        while done < len(gids):
+            if time.perf_counter() > deadline:
+                raise TimeoutError(f"built {done} of {len(gids)} scenes in {timeout:.0f} s")
+            got, recs = pool.poll(timeout=5.0)
+            for k, g in enumerate(got):
+                out[where[g]] = recs[k]
+            done += len(got)
+    finally:
+        pool.close()
+    return out

@@ -43,10 +43,22 @@ def payload_bytes(n: int, s: int, packed: bool = True) -> int:
     return (raw + 15) // 16 * 16
 
 
+def _raw_stream(t, stream):
+    """`stream` (a raw hipStream_t) or, when None, the caller's current torch stream
+    on t's device: the pack / unpack kernels are then ordered with the step kernels
+    that wrote the frames and with the collective that reads them."""
+    import ctypes
+    import torch
+    if stream is not None:
+        return stream
+    return ctypes.c_void_p(torch._C._cuda_getCurrentRawStream(t.device.index))
+
+
 def pack_frames(frames, out=None, ctx=None, stream=None):
     """Palette-id frames (n, S, S) uint8 -> nibble-packed (n, S*S/2): byte j =
     pixel 2j | pixel 2j+1 << 4. Device tensors go through the HIP kernel
-    (cbev_pack_frames, needs the env's C-ABI context); CPU tensors (gloo) through torch."""
+    (cbev_pack_frames, needs the env's C-ABI context; on `stream`, default the
+    current torch stream); CPU tensors (gloo) through torch."""
     import torch
     n = frames.shape[0]
     flat = frames.reshape(n, -1)
@@ -56,7 +68,7 @@ def pack_frames(frames, out=None, ctx=None, stream=None):
         import ctypes
         from ._lib import check, lib
         check(lib().cbev_pack_frames(ctx, ctypes.c_void_p(flat.data_ptr()), n, ctypes.c_void_p(out.data_ptr()),
-                                     stream), "cbev_pack_frames")
+                                     _raw_stream(flat, stream)), "cbev_pack_frames")
     else:
         torch.bitwise_or(flat[:, 0::2], flat[:, 1::2] << 4, out=out)
     return out
@@ -71,7 +83,7 @@ def unpack_frames(packed, s: int, ctx=None, stream=None):
         import ctypes
         from ._lib import check, lib
         check(lib().cbev_unpack_frames(ctx, ctypes.c_void_p(packed.data_ptr()), n, ctypes.c_void_p(out.data_ptr()),
-                                       stream), "cbev_unpack_frames")
+                                       _raw_stream(packed, stream)), "cbev_unpack_frames")
     else:
         flat = out.view(n, -1)
         flat[:, 0::2] = packed & 15

@@ -89,15 +89,15 @@ class StepInfos(Mapping):
     "episode": ..., "_episode": mask}), built from the device's episode rows the
     first time it is read. Not reading it costs no host work and no sync."""
 
-    __slots__ = ("_env", "_step", "_event", "_d", "__weakref__")
+    __slots__ = ("_env", "_step", "_d", "__weakref__")
 
-    def __init__(self, env, step: int, event):
-        self._env, self._step, self._event, self._d = env, step, event, None
+    def __init__(self, env, step: int):
+        self._env, self._step, self._d = env, step, None
 
     def _get(self) -> dict:
         if self._d is None:
-            self._d = self._env._materialize_infos(self._step, self._event)
-            self._env = self._event = None
+            self._d = self._env._materialize_infos(self._step)
+            self._env = None
         return self._d
 
     def __getitem__(self, key):
@@ -244,7 +244,7 @@ class CarlaBEVVectorEnv:
             check(L.cbev_set_episode_stats(ctx, _ptr(self._ep_stats), N, _ptr(self._ep_rows), _ptr(self._ep_counts),
                                            EP_RING), "cbev_set_episode_stats")
         self.bank = None
-        self._bank_cursor = 0
+        self._all_mask = None  # uint8 ones: reset_from_bank(mask=None) without bank_idx
         self._bank_ctx_ids = None  # scenario-context id per bank row set by refresh_bank
         self._retired_ctx: deque = deque()  # ids of overwritten bank rows, released oldest first
         self._stepped = False
@@ -287,7 +287,7 @@ class CarlaBEVVectorEnv:
         check(lib().cbev_bank_frames(self._ctx, _ptr(self.bank), B, _ptr(self.bank_frames), self._stream()),
               "cbev_bank_frames")
 
-    RETIRED_CTX_KEEP = 1 << 16  # contexts of overwritten bank rows kept for envs still running them
+    RETIRED_CTX_KEEP = 1 << 16  # contexts of overwritten bank rows checked for release past this many
 
     def refresh_bank(self, slot0: int, records: np.ndarray, contexts=None) -> int:
         """Write k fresh scene records (uint8[k][record_bytes], e.g. from a ScenePool)
@@ -298,8 +298,9 @@ class CarlaBEVVectorEnv:
         each gets an id written into its record's CTX_ID, so episodes reset from the
         row report it in episode_info as the reference merges _scenario_context
         (carlabev.py:182). The id of an overwritten row is retired: envs may still run
-        that scene, so retired contexts are released only after RETIRED_CTX_KEEP newer
-        ones."""
+        that scene, so once more than RETIRED_CTX_KEEP (or 2 N) ids are retired, the
+        pending infos are read and the retired ids no env's record carries any more are
+        released (one device read of the records' CTX_ID words)."""
         if self.bank is None:
             raise RuntimeError("no scene bank attached")
         B, k = self.bank.shape[0], int(records.shape[0])
@@ -322,8 +323,8 @@ class CarlaBEVVectorEnv:
                 cid = self._new_ctx_id(contexts[j])
                 self._bank_ctx_ids[row] = cid
                 LY.RecordView(records[j], self.layout).hi[ci] = cid
-            while len(self._retired_ctx) > self.RETIRED_CTX_KEEP:
-                self._ctx_table.pop(self._retired_ctx.popleft(), None)
+            if len(self._retired_ctx) > max(self.RETIRED_CTX_KEEP, 2 * self.num_envs):
+                self._release_retired_contexts()
         src = torch.from_numpy(np.ascontiguousarray(records)).pin_memory()
         done = 0
         s = slot0 % B
@@ -336,6 +337,25 @@ class CarlaBEVVectorEnv:
             s = (s + m) % B
         self._refresh_keep = src  # the pinned staging must outlive the async copy
         return s
+
+    def record_ctx_ids(self) -> np.ndarray:
+        """CTX_ID of every env's record as it is now (synchronises)."""
+        o = self.layout.off["hi"] + 4 * LY.HI["CTX_ID"]
+        return self.records[:, o:o + 4].contiguous().view(torch.int32).reshape(-1).cpu().numpy()
+
+    def _release_retired_contexts(self):
+        """Forget the retired scenario contexts that no env runs and no unread
+        StepInfos refers to (the pending ones are read first)."""
+        self._flush_pending(all_=True)
+        live = set(self.record_ctx_ids().tolist())
+        keep = deque()
+        while self._retired_ctx:
+            cid = self._retired_ctx.popleft()
+            if cid in live:
+                keep.append(cid)
+            else:
+                self._ctx_table.pop(cid, None)
+        self._retired_ctx = keep
 
     def termination_count(self) -> int:
         """Episodes terminated so far on this env's device context (synchronises)."""
@@ -360,71 +380,93 @@ class CarlaBEVVectorEnv:
         return torch.from_numpy(host).to(self.device)
 
     def reset_terminated(self):
-        """The canonical loop's reset(reset_mask=terminated) on the device: the envs the
-        last step terminated (listed by the step kernel, no mask scan) <- the next bank
-        rows in order (bank[(cursor + k) % B] for the k-th of them by env id; the cursor
-        walks the whole bank), reset frame into every frame-stack slot. One launch, no
-        host sync."""
+        """The canonical loop's reset(reset_mask=terminated) on the device: every env
+        whose `term` flag is set when the launch runs (the last step's, including any
+        in-place edit of env.term since) <- the next bank rows in env-id order
+        (bank[(cursor + k) % B] for the k-th of them; the cursor walks the whole bank,
+        so every reset is a distinct scene until it wraps), reset frame into every
+        frame-stack slot. One launch, no host sync."""
         if self.bank is None:
             raise RuntimeError("no scene bank attached")
+        if not self._stepped:
+            raise RuntimeError("reset_terminated before any step()")
+        return self._reset_masked(self.term)
+
+    def _reset_masked(self, mask: torch.Tensor):
         N, B = self.num_envs, self.bank.shape[0]
         rec = self._p_step[0]
         if self.resize:
-            check(lib().cbev_reset_terminated(self._ctx, rec, N, self._p_bank, B, self._p_bank_frames, self._p_full, 1,
-                                              self._stream()), "cbev_reset_terminated")
-            self._resize_into_ring(self.term, all_slots=True)
+            check(lib().cbev_reset_masked(self._ctx, rec, N, mask.data_ptr(), self._p_bank, B, self._p_bank_frames,
+                                          self._p_full, 1, self._stream()), "cbev_reset_masked")
+            self._resize_into_ring(mask, all_slots=True)
         else:
-            check(lib().cbev_reset_terminated(self._ctx, rec, N, self._p_bank, B, self._p_bank_frames, self._p_ring,
-                                              self.F, self._stream()), "cbev_reset_terminated")
+            check(lib().cbev_reset_masked(self._ctx, rec, N, mask.data_ptr(), self._p_bank, B, self._p_bank_frames,
+                                          self._p_ring, self.F, self._stream()), "cbev_reset_masked")
         if not self.auto_obs:
             return None
         obs = self._obs()
         return obs.clone() if self.copy_obs else obs
 
     def bank_rows_used(self) -> int:
-        """Bank rows reset_terminated() has handed out since the env was created
-        (synchronises); with B rows, resets k .. k + B - 1 all got distinct scenes."""
+        """Bank rows the cursor resets (reset_terminated, reset_from_bank without
+        bank_idx) have handed out since the env was created (synchronises); with B
+        rows, resets k .. k + B - 1 all got distinct scenes."""
         n = ctypes.c_int64()
         check(lib().cbev_bank_cursor(self._ctx, ctypes.byref(n)), "cbev_bank_cursor")
         return int(n.value)
 
     def reset_from_bank(self, mask: torch.Tensor | None = None, bank_idx: torch.Tensor | None = None):
-        """Device-only partial reset: env i (mask[i]) <- bank[bank_idx[i]] (default: a rotating
-        offset into the bank), reset frame into every frame-stack slot. One launch, no host sync.
-        mask = this env's own `term` tensor with no bank_idx is the canonical loop's
-        reset(reset_mask=terminated): served by reset_terminated()."""
+        """Device-only partial reset from the scene bank, reset frame into every
+        frame-stack slot. One launch, no host sync.
+        Without bank_idx: the envs selected by mask (all when None; its contents as
+        the launch reads them) take the next bank rows of the device cursor in env-id
+        order (reset_terminated is this with mask = env.term).
+        With bank_idx: env i (mask[i]) <- bank[bank_idx[i]]; the cursor is untouched."""
         if self.bank is None:
             raise RuntimeError("no scene bank attached")
-        if mask is self.term and bank_idx is None and self._stepped:
-            return self.reset_terminated()
         N, B = self.num_envs, self.bank.shape[0]
-        offset = 0
-        if bank_idx is None:
-            offset = self._bank_cursor
-            self._bank_cursor = (self._bank_cursor + N) % B
-        else:  # the kernels read N int32 bank rows on this device
-            bank_idx = torch.as_tensor(bank_idx)
-            if bank_idx.numel() != N:
-                raise ValueError(f"bank_idx has {bank_idx.numel()} entries, expected {N}")
-            bank_idx = bank_idx.reshape(N).to(device=self.device, dtype=torch.int32).contiguous()
         if mask is not None:
             mask = torch.as_tensor(mask)
             if mask.numel() != N:
                 raise ValueError(f"reset mask has {mask.numel()} entries, expected {N}")
             mask = mask.reshape(N).to(device=self.device, dtype=torch.uint8).contiguous()
+        if bank_idx is None:
+            if mask is None:
+                if self._all_mask is None:
+                    self._all_mask = torch.ones(N, dtype=torch.uint8, device=self.device)
+                mask = self._all_mask
+            return self._reset_masked(mask)
+        bank_idx = torch.as_tensor(bank_idx)  # the kernels read N int32 bank rows on this device
+        if bank_idx.numel() != N:
+            raise ValueError(f"bank_idx has {bank_idx.numel()} entries, expected {N}")
+        bank_idx = bank_idx.reshape(N).to(device=self.device, dtype=torch.int32).contiguous()
         if self.resize:
             check(lib().cbev_reset_frames(self._ctx, _ptr(self.records), N, _ptr(self.bank), B, _ptr(mask),
-                                          _ptr(bank_idx), offset, _ptr(self.bank_frames), _ptr(self.full), 1,
+                                          _ptr(bank_idx), 0, _ptr(self.bank_frames), _ptr(self.full), 1,
                                           self._stream()), "cbev_reset_frames")
             self._resize_into_ring(mask, all_slots=True)
         else:
             check(lib().cbev_reset_frames(self._ctx, _ptr(self.records), N, _ptr(self.bank), B, _ptr(mask),
-                                          _ptr(bank_idx), offset, _ptr(self.bank_frames), _ptr(self.ring), self.F,
+                                          _ptr(bank_idx), 0, _ptr(self.bank_frames), _ptr(self.ring), self.F,
                                           self._stream()), "cbev_reset_frames")
         if not self.auto_obs:
             return None
         obs = self._obs()
         return obs.clone() if self.copy_obs else obs
+
+    def load_scenes(self, records: torch.Tensor):
+        """Every env <- records[i] (N packed records on this device, e.g. the seeded
+        start scenes), reset observation rendered into every frame-stack slot; the
+        bank and its cursor are untouched. One launch."""
+        N = self.num_envs
+        if records.device != self.device or records.dtype != torch.uint8 or tuple(records.shape) != (N, self.rb):
+            raise ValueError(f"expected a ({N}, {self.rb}) uint8 tensor on {self.device}")
+        records = records.contiguous()
+        dst = self.full if self.resize else self.ring
+        check(lib().cbev_reset(self._ctx, _ptr(self.records), N, _ptr(records), N, None, None, 0, _ptr(dst),
+                               1 if self.resize else self.F, self._stream()), "cbev_reset")
+        if self.resize:
+            self._resize_into_ring(None, all_slots=True)
 
     def _resize_into_ring(self, mask: torch.Tensor | None, all_slots: bool):
         """ResizeObservation + the mask/grayscale colour test of self.full into the ring:
@@ -562,9 +604,7 @@ class CarlaBEVVectorEnv:
         from the device only when accessed; {} otherwise."""
         if self.info_mode != "full":
             return {}
-        ev = torch.cuda.Event()
-        ev.record(torch.cuda.current_stream(self.device))
-        infos = StepInfos(self, self._ep_step - 1, ev)
+        infos = StepInfos(self, self._ep_step - 1)
         self._pending.append((self._ep_step - 1, weakref.ref(infos)))
         return infos
 
@@ -578,12 +618,15 @@ class CarlaBEVVectorEnv:
             if obj is not None:
                 obj._get()
 
-    def _materialize_infos(self, step: int, event) -> dict:
+    def _materialize_infos(self, step: int) -> dict:
         """Vector-env infos of `step` from its device rows (SyncVectorEnv._add_info
         layout: {"episode_info": {key: array, "_key": mask}, "_episode_info": mask,
         "episode": {"r", "l", "t"} + masks, "_episode": mask}; {} when no env
-        terminated). The scenario context is merged as carlabev.py:181-182 does."""
-        event.synchronize()
+        terminated). The scenario context is merged as carlabev.py:181-182 does.
+        Waits for the device (a step's rows stay valid until EP_RING - 1 newer
+        steps are queued, and _flush_pending reads them before that), so a step
+        enqueues no event or other marker for its infos."""
+        torch.cuda.synchronize(self.device)
         slot = step % EP_RING
         cnt = int(self._ep_counts[slot].item())
         if cnt == 0:

@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define CBEV_ABI_VERSION 4
+#define CBEV_ABI_VERSION 5
 
 typedef struct cbev_ctx cbev_ctx;
 
@@ -93,6 +93,9 @@ int cbev_termination_count(cbev_ctx* ctx, int64_t* count);
  *                          envs/spaces.py:46); that env stepped action 0.
  *                          Negative indices in [-n, 0) count from the end. */
 #define CBEV_ERR_ACTION_INDEX 1
+/*   CBEV_ERR_RASTER_WINDOW a raster tile's crop window exceeded its LDS bound
+ *                          (an internal invariant; the frame is not valid). */
+#define CBEV_ERR_RASTER_WINDOW 2
 int cbev_error_flags(cbev_ctx* ctx, int32_t* flags_host, int clear);
 
 /* Reset the envs selected by mask (uint8[n], NULL = all):
@@ -119,18 +122,22 @@ int cbev_reset_frames(cbev_ctx* ctx, void* records, int n, const void* bank, int
                       const int32_t* bank_idx, int bank_offset, const uint8_t* bank_frames, uint8_t* frames,
                       int n_frames, void* stream);
 
+/* `reset(options={"reset_mask": mask})` (SyncVectorEnv.reset -> CarlaBEV.reset,
+ * carlabev.py:96-148) from a bank with cached reset frames, each reset a fresh
+ * bank row: the envs with mask[e] != 0 (uint8[n], read when the launch runs)
+ * take the next rows of a device cursor in env-id order, the k-th selected env
+ * bank[(cursor + k) % n_bank], and the cursor moves past them, so consecutive
+ * resets walk the whole bank. Records and ring contents as cbev_reset_frames
+ * with those bank rows. One launch, no host sync; n <= 2^20. */
+int cbev_reset_masked(cbev_ctx* ctx, void* records, int n, const uint8_t* mask, const void* bank, int n_bank,
+                      const uint8_t* bank_frames, uint8_t* frames, int n_frames, void* stream);
 /* The canonical loop's reset, `reset(options={"reset_mask": terminated})`
- * (tools/debug_env.py:56-132 -> SyncVectorEnv.reset -> CarlaBEV.reset,
- * carlabev.py:96-148), from a bank with cached reset frames: the same records and
- * ring contents as cbev_reset_frames with mask = the terminations of the last
- * cbev_step on this context (n must be that step's n), without scanning a mask:
- * k_ego lists the envs that terminate. Bank rows are taken in order from a
- * device cursor: the k-th terminated env in env-id order gets
- * bank[(cursor + k) % n_bank], and the cursor moves past them when the next
- * cbev_step starts, so consecutive resets walk the whole bank. One launch. */
+ * (tools/debug_env.py:56-132): cbev_reset_masked with mask = the `term` buffer
+ * of the last cbev_step on this context (n must be that step's n). */
 int cbev_reset_terminated(cbev_ctx* ctx, void* records, int n, const void* bank, int n_bank,
                           const uint8_t* bank_frames, uint8_t* frames, int n_frames, void* stream);
-/* Bank rows the terminated-env resets have taken since cbev_create (synchronises). */
+/* Bank rows cbev_reset_masked / cbev_reset_terminated have handed out since
+ * cbev_create (synchronises the device). */
 int cbev_bank_cursor(cbev_ctx* ctx, int64_t* cursor);
 
 /* Wrapper stack on the device (wrap_env, envs/__init__.py:62-83). `ring` holds
@@ -163,7 +170,8 @@ int cbev_vector_obs(cbev_ctx* ctx, const void* records, int n, float* out, void*
  * <= 15): packed = uint8[n][S*S/2], byte j of env e = frames[e][2j] |
  * frames[e][2j + 1] << 4. cbev_unpack_frames is the inverse. The reference has
  * no multi-process path (SyncVectorEnv, envs/__init__.py:116-119): this halves
- * the bytes the gather of the compact observation moves over xGMI. */
+ * the bytes the gather of the compact observation moves over xGMI. frames must be
+ * 16-byte and packed 8-byte aligned (CBEV_EINVAL otherwise). */
 int cbev_pack_frames(cbev_ctx* ctx, const uint8_t* frames, int n, uint8_t* packed, void* stream);
 int cbev_unpack_frames(cbev_ctx* ctx, const uint8_t* packed, int n, uint8_t* frames, void* stream);
 

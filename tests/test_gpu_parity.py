@@ -515,16 +515,11 @@ def test_parity_bench_caps_small(config):
         run_parity(["mix3"], 19, 80, size=256, seed0=30_000, caps=caps)
 
 
-def test_reset_terminated_matches_masked_reset():
-    """cbev_reset_terminated (the canonical loop's reset from k_ego's termination
-    list) = cbev_reset_frames with mask = that step's terminations and bank rows
-    handed out in env-id order from the cursor: the k-th terminated env gets
-    bank[(cursor + k) % B], and the cursor moves past them at the next step."""
-    cfg, P, padded, layout, builder = world(caps=bench_caps(3))
-    n, B, F = 45, 11, 4
-    recs, _ = build_records(builder, n, ["rt_hard_v1"], seed0=2100)
-    bank, _ = build_records(builder, B, ["rt_hard_v1", "rt_medium_v1"], seed0=2900)
-    dw = DevWorld(P, padded, bench_caps(3))
+def _bank_world(n, B, F, caps, kinds, seed0, bank_seed0):
+    cfg, P, padded, layout, builder = world(caps=caps)
+    recs, _ = build_records(builder, n, kinds, seed0=seed0)
+    bank, _ = build_records(builder, B, kinds, seed0=bank_seed0)
+    dw = DevWorld(P, padded, caps)
     L = lib()
     S = P.size
     d_bank = torch.from_numpy(bank.copy()).cuda()
@@ -533,6 +528,38 @@ def test_reset_terminated_matches_masked_reset():
     d_recs = torch.from_numpy(recs.copy()).cuda()
     ring = torch.zeros((F, n, S, S), dtype=torch.uint8, device="cuda")
     check(L.cbev_reset(dw.ctx, ptr(d_recs), n, None, 0, None, None, 0, ptr(ring), F, None), "reset")
+    return P, layout, dw, d_bank, bf, d_recs, ring
+
+
+def _want_reset(L, dw, d_recs, ring, d_bank, bf, mask_np, cursor, F):
+    """cbev_reset_frames with the bank rows the cursor reset hands out: the k-th
+    selected env in id order gets bank[(cursor + k) % B]."""
+    n, B = d_recs.shape[0], d_bank.shape[0]
+    ids = np.flatnonzero(mask_np)
+    bidx = np.zeros(n, np.int32)
+    bidx[ids] = (cursor + np.arange(len(ids))) % B
+    want_r, want_f = d_recs.clone(), ring.clone()
+    m = torch.from_numpy(mask_np.astype(np.uint8)).cuda()
+    check(L.cbev_reset_frames(dw.ctx, ptr(want_r), n, ptr(d_bank), B, ptr(m), ptr(torch.from_numpy(bidx).cuda()),
+                              0, ptr(bf), ptr(want_f), F, None), "reset_frames")
+    return want_r, want_f, len(ids)
+
+
+def _cursor(L, dw):
+    c = ctypes.c_int64()
+    check(L.cbev_bank_cursor(dw.ctx, ctypes.byref(c)), "cursor")
+    return c.value
+
+
+def test_reset_terminated_matches_masked_reset():
+    """cbev_reset_terminated (the canonical loop's reset from the last step's term
+    buffer) = cbev_reset_frames with mask = that step's terminations and bank rows
+    handed out in env-id order from the cursor: the k-th terminated env gets
+    bank[(cursor + k) % B], and the cursor moves past them."""
+    n, B, F = 45, 11, 4
+    P, layout, dw, d_bank, bf, d_recs, ring = _bank_world(n, B, F, bench_caps(3), ["rt_hard_v1", "rt_medium_v1"],
+                                                           2100, 2900)
+    L = lib()
     rew = torch.zeros(n, dtype=torch.float64, device="cuda")
     term = torch.zeros(n, dtype=torch.uint8, device="cuda")
     trunc = torch.zeros_like(term)
@@ -551,22 +578,80 @@ def test_reset_terminated_matches_masked_reset():
         check(L.cbev_step(dw.ctx, ptr(d_recs), n, ptr(a), ptr(ring[t % F]), ptr(rew), ptr(term), ptr(trunc),
                           ptr(cause), None, None), "step")
         torch.cuda.synchronize()
-        m = term.cpu().numpy().astype(bool)
-        ids = np.flatnonzero(m)
-        total += len(ids)
-        bidx = np.zeros(n, np.int32)
-        bidx[ids] = (cursor + np.arange(len(ids))) % B
-        want_r, want_f = d_recs.clone(), ring.clone()
-        check(L.cbev_reset_frames(dw.ctx, ptr(want_r), n, ptr(d_bank), B, ptr(term), ptr(torch.from_numpy(bidx).cuda()),
-                                  0, ptr(bf), ptr(want_f), F, None), "reset_frames")
+        want_r, want_f, k = _want_reset(L, dw, d_recs, ring, d_bank, bf, term.cpu().numpy().astype(bool), cursor, F)
+        total += k
         check(L.cbev_reset_terminated(dw.ctx, ptr(d_recs), n, ptr(d_bank), B, ptr(bf), ptr(ring), F, None), "reset_term")
         torch.cuda.synchronize()
         assert torch.equal(d_recs, want_r), t
         assert torch.equal(ring, want_f), t
-        cursor += len(ids)
-        c = ctypes.c_int64()
-        check(L.cbev_bank_cursor(dw.ctx, ctypes.byref(c)), "cursor")
-        assert c.value == cursor, (t, c.value, cursor)
+        cursor += k
+        assert _cursor(L, dw) == cursor, t
     assert total > 20
     # n must match the last step's
     assert L.cbev_reset_terminated(dw.ctx, ptr(d_recs), n - 1, ptr(d_bank), B, ptr(bf), ptr(ring), F, None) != 0
+
+
+def test_reset_masked_mass_termination_and_edits():
+    """The cursor reset when most of a large batch terminates at once (every env
+    pushed off the road: the ranking must not depend on the count), with the mask
+    edited in place between the step and the reset (term |= extra, term[i] = 0:
+    the reset reads the buffer when it runs), an unaligned mask view, and a step
+    with no reset (the cursor moves only when a reset runs)."""
+    n, B, F = 4099, 5003, 1
+    P, layout, dw, d_bank, bf, d_recs, ring = _bank_world(n, B, F, bench_caps(2), ["rt_no_traffic_v1"], 6000, 16000)
+    L = lib()
+    rew = torch.zeros(n, dtype=torch.float64, device="cuda")
+    term = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    trunc = torch.zeros_like(term)
+    cause = torch.zeros(n, dtype=torch.int32, device="cuda")
+    acts = action_stream(P, n, 6, seed=3)
+    rng = np.random.default_rng(11)
+    cursor = 0
+
+    def step(t, push):
+        h = d_recs.cpu().numpy()
+        for e in push:
+            LY.RecordView(h[e], layout).hd[LY.HD["X"]] += 60.0
+        d_recs.copy_(torch.from_numpy(h))
+        a = torch.from_numpy(np.ascontiguousarray(acts[t])).cuda()
+        check(L.cbev_step(dw.ctx, ptr(d_recs), n, ptr(a), ptr(ring[0]), ptr(rew), ptr(term), ptr(trunc), ptr(cause),
+                          None, None), "step")
+        torch.cuda.synchronize()
+
+    # 1: (almost) every env terminates
+    step(0, range(n))
+    m = term.cpu().numpy().astype(bool)
+    assert m.sum() > n // 2
+    want_r, want_f, k = _want_reset(L, dw, d_recs, ring, d_bank, bf, m, cursor, F)
+    check(L.cbev_reset_terminated(dw.ctx, ptr(d_recs), n, ptr(d_bank), B, ptr(bf), ptr(ring), F, None), "reset_term")
+    torch.cuda.synchronize()
+    assert torch.equal(d_recs, want_r) and torch.equal(ring, want_f)
+    cursor += k
+    assert _cursor(L, dw) == cursor
+    # 2: a step whose terminations are not reset: the cursor stays
+    step(1, rng.choice(n, size=300, replace=False))
+    assert term.cpu().numpy().sum() > 0 and _cursor(L, dw) == cursor
+    # 3: in-place edits of the term buffer before the reset
+    step(2, rng.choice(n, size=700, replace=False))
+    extra = torch.from_numpy((rng.random(n) < 0.05).astype(np.uint8)).cuda()
+    term |= extra
+    term[:17] = 0
+    m = term.cpu().numpy().astype(bool)
+    want_r, want_f, k = _want_reset(L, dw, d_recs, ring, d_bank, bf, m, cursor, F)
+    check(L.cbev_reset_terminated(dw.ctx, ptr(d_recs), n, ptr(d_bank), B, ptr(bf), ptr(ring), F, None), "reset_term")
+    torch.cuda.synchronize()
+    assert torch.equal(d_recs, want_r) and torch.equal(ring, want_f)
+    cursor += k
+    assert _cursor(L, dw) == cursor
+    # 4: cbev_reset_masked with an arbitrary mask at an odd byte offset (byte-wise mask loads)
+    buf = torch.zeros(n + 3, dtype=torch.uint8, device="cuda")
+    mview = buf[3:]
+    mh = rng.random(n) < 0.4
+    mview.copy_(torch.from_numpy(mh.astype(np.uint8) * 7))  # any nonzero byte selects
+    want_r, want_f, k = _want_reset(L, dw, d_recs, ring, d_bank, bf, mh, cursor, F)
+    check(L.cbev_reset_masked(dw.ctx, ptr(d_recs), n, ptr(mview), ptr(d_bank), B, ptr(bf), ptr(ring), F, None),
+          "reset_masked")
+    torch.cuda.synchronize()
+    assert torch.equal(d_recs, want_r) and torch.equal(ring, want_f)
+    cursor += k
+    assert _cursor(L, dw) == cursor and cursor > B  # wrapped around the bank

@@ -145,6 +145,7 @@ def test_resize_rejects_upscale():
     ("bev_semantic", "vehicle_weighted", (128, 128)),
     ("bev_semantic", "stack", (96, 96)),
     ("bev_rgb", "stack", (84, 84)),
+    ("bev_rgb", "stack", (128, 128)),  # config 3's wire format: gray 4-stack at the render size, no resize
 ])
 def test_vector_env_wrapped_obs_match_oracle(obs_mode, fusion, obs_size):
     """make_env with resize / fusion: every step's observation equals the wrapper
