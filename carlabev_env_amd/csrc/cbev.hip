@@ -663,9 +663,12 @@ __device__ unsigned g_hwid[CBEV_NSTAMP][4096];                   // HW_ID (SE / 
 // so a 64-env block stays on one XCD) and copies the record ranges its float64
 // chains and element loops read into LDS with LDS-DMA (16-byte lane-linear
 // pieces, all in flight at once), packed per env as two ranges of the layout:
-//   [HD, HI, cx, cy] [raw_x, raw_y, raw_cum, vis, vis_draw]
-// (EgoPack). cyaw (read at one index, by the shaping reward only) and the
-// actor groups (read by a few lanes) stay in HBM. raw_cum is staged: its reads
+//   [HD, HI] [raw_x, raw_y, raw_cum, vis, vis_draw]
+// (EgoPack). The route (cx, cy, cyaw) stays in HBM: S2 and S5's target loop
+// read it from registers loaded at launch, the rest at one or a few indices
+// (round 4: staging it was half of the staged bytes, and the staging's per-CU
+// throughput sets the length of S0); the actor groups (read by a few lanes)
+// stay in HBM too. raw_cum is staged: its reads
 // at the arg-min segment (S5) and the route end (S6) sat inside the chains, a
 // dependent HBM latency each. The fields the kernel changes (HD, HI, the vis
 // group) are copied back at the end.
@@ -684,7 +687,7 @@ struct EgoPack {
 };
 __host__ __device__ __forceinline__ EgoPack ego_pack(const cbev_layout& L) {
   EgoPack p;
-  p.n0 = (int)(L.cyaw / 16);                              // HD, HI, cx, cy (the record's prefix)
+  p.n0 = (int)(L.cx / 16);                                // HD, HI (the record's prefix)
   const int64_t end = L.vis + 8 * (int64_t)L.vis_words;  // raw_x .. vis_draw
   p.n = p.n0 + (int)((end - L.raw_x + 15) / 16);
   p.raw_x = (int)L.raw_x;
@@ -694,14 +697,14 @@ __host__ __device__ __forceinline__ EgoPack ego_pack(const cbev_layout& L) {
   return p;
 }
 
-// DRec of a staged env: the two ranges in LDS, cyaw and the actor groups in HBM
+// DRec of a staged env: the two ranges in LDS; the route (cx, cy, cyaw: read
+// from registers prefetched at launch, or at one or a few indices) and the actor
+// groups in HBM
 __device__ __forceinline__ DRec bind_ego(uint8_t* l, uint8_t* g, const KArgs& K, const EgoPack& p) {
   DRec r = bind_rec(g, K.L, K.C);
   const DRec s = bind_rec(l, K.L, K.C);  // the first range at the record's offsets
   r.hd = s.hd;
   r.hi = s.hi;
-  r.cx = s.cx;
-  r.cy = s.cy;
   uint8_t* l1 = l + 16 * p.n0 - K.L.raw_x;  // the second range: record offset o at l1 + o
   r.raw_x = (int32_t*)(l1 + K.L.raw_x);
   r.raw_y = (int32_t*)(l1 + K.L.raw_y);
@@ -1362,7 +1365,7 @@ __device__ __forceinline__ TileWin tile_window(const cbev_params& P, const Raste
   W.vmin = W.tr ? J.xmin : J.ymin;
   W.v0 = W.tr ? xl : yl;
   W.nv = (W.tr ? xh : yh) - W.v0 + 1;
-  const int ushift = W.umin & 3;
+  const int ushift = W.umin & 3;  // the staging reads from 4-byte boundaries
   W.c0 = (ushift + ul) >> 4;
   W.nc = ((ushift + uh) >> 4) - W.c0 + 1;
   W.sb = 16 * W.nc + 4;  // an odd number of dwords: the rows of a wave's lanes fall on distinct banks
@@ -1379,27 +1382,32 @@ __device__ __forceinline__ uint4 load16_a4(const uint8_t* p) {  // 16 bytes at 4
   const u32x4_a4 t = *(const u32x4_a4*)p;
   return make_uint4(t.x, t.y, t.z, t.w);
 }
+typedef __attribute__((address_space(3))) uint32_t lds_u32;  // a dword of LDS
 template <int U>
 __device__ __forceinline__ void stage_group(const uint8_t* __restrict__ g, int pitch, uint8_t* __restrict__ l, int sb,
                                             int row, int dr, int last) {
   uint4 v[U];
 #pragma unroll
   for (int u = 0; u < U; ++u) v[u] = load16_a4(g + (int64_t)min(row + u * dr, last) * pitch);
+  // four dword stores (volatile LDS pointer: not merged into one ds_write_b128,
+  // which the window rows' odd-dword pitch leaves 4-byte aligned, and an
+  // off-alignment wide DS access is replayed at 64 cycles per wave-instruction)
 #pragma unroll
   for (int u = 0; u < U; ++u) {
-    uint32_t* d = (uint32_t*)(l + min(row + u * dr, last) * sb);
+    volatile lds_u32* d = (volatile lds_u32*)(l + min(row + u * dr, last) * sb);
     d[0] = v[u].x;
     d[1] = v[u].y;
     d[2] = v[u].z;
     d[3] = v[u].w;
   }
 }
+template <int NT>
 __device__ __forceinline__ void stage_tile(const KArgs& K, const TileWin& W, uint8_t* __restrict__ lds) {
-  const int nc = W.nc, dr = 256 / nc;
+  const int nc = W.nc, dr = NT / nc;
   const int t = (int)threadIdx.x;
   int row = t / nc;
   const int c = t - row * nc;
-  row = row < dr ? row : dr - 1;  // the 256 % nc leftover threads repeat chunks of the pass's last row
+  row = row < dr ? row : dr - 1;  // the NT % nc leftover threads repeat chunks of the pass's last row
   const int passes = (W.nv + dr - 1) / dr;
   const uint8_t* map = W.tr ? K.map8T : K.map8;
   const int pitch = W.tr ? K.p8T : K.p8;
@@ -1424,6 +1432,7 @@ __device__ __forceinline__ void paint_win_rect(uint8_t* lds, const TileWin& W, i
     const int pv = rv + qv;
     if (pv >= C || pv < W.v0 || pv >= W.v0 + W.nv) continue;
     uint8_t* rowp = lds + (pv - W.v0) * W.sb + W.ou;
+#pragma clang loop vectorize(disable) interleave(disable)  // no wide DS stores off their alignment
     for (int u = u0; u < u1; ++u) rowp[u] = (uint8_t)col;
   }
 }
@@ -1432,9 +1441,9 @@ __device__ __forceinline__ void paint_win_rect(uint8_t* lds, const TileWin& W, i
 // into the window in the reference's draw order (scene.py:93-95,
 // actor_manager.py:121-132, target.py:46-50, traffic_light.py:81-90):
 // vehicles, pedestrians, targets, traffic lights, later wins.
+template <int NT>
 __device__ __forceinline__ void paint_tile(const KArgs& K, const DRec& r, const PaintPre& q, const RasterJob& J,
                                            const TileWin& W, uint8_t* __restrict__ lds) {
-  constexpr int NT = 256;
   const cbev_params& P = K.P;
   const int C = P.crop;
   const int k = threadIdx.x >> 2, tq = threadIdx.x & 3;
@@ -1489,7 +1498,7 @@ __device__ __forceinline__ void paint_tile(const KArgs& K, const DRec& r, const 
 // computes it from the record.
 __device__ __forceinline__ uint32_t crop_background(const KArgs& K, const DRec& r, const RasterJob& J, bool paint) {
   const cbev_params& P = K.P;
-  uint32_t col = K.map8[(int64_t)J.ymin * K.p8 + J.xmin];
+  uint32_t col = (uint32_t)d_map_texel(K, J.xmin, J.ymin);
   if (!paint) return col;
   auto covers = [](int rx, int ry, int sx, int sy) { return rx <= 0 && 0 < rx + sx && ry <= 0 && 0 < ry + sy; };
   const int nact = r.hi[CBEV_HI_NACT], nveh = r.hi[CBEV_HI_NVEH], nt = r.hi[CBEV_HI_NROUTE], ntl = r.hi[CBEV_HI_NTL];
@@ -1513,6 +1522,10 @@ __device__ __forceinline__ uint32_t crop_background(const KArgs& K, const DRec& 
 }
 
 typedef uint32_t u32x4_nt __attribute__((ext_vector_type(4)));  // one 16-byte (non-temporal) store
+// one 16-byte store of frame bytes (streamed out: the caller reads them later)
+__device__ __forceinline__ void store16_frame(uint8_t* p, u32x4_nt v) {
+  __builtin_nontemporal_store(v, (u32x4_nt*)p);
+}
 
 // (v >> 16) * sb + (u >> 16) of the packed window coordinates (v << 32 | u):
 // v_mul_u32_u24 and v_add_u32 with SDWA word selects
@@ -1567,7 +1580,7 @@ __device__ __forceinline__ void overlay16(const cbev_params& P, const uint32_t* 
 // (one 64-bit add steps both packed window coordinates: the low word stays in
 // [0, 2^32), so no carry crosses over), packed into 4 dwords by v_lshl_or +
 // v_perm and written with ONE 16-byte non-temporal store.
-template <int G>
+template <int G, int NT>
 __device__ __forceinline__ void tile_out(const cbev_params& P, const RotSetup& R, const TileWin& W, int ox0, int oy0,
                                          const uint8_t* __restrict__ lds, uint8_t* __restrict__ out, int nout,
                                          int64_t out_stride, const uint32_t* __restrict__ fov) {
@@ -1582,13 +1595,14 @@ __device__ __forceinline__ void tile_out(const cbev_params& P, const RotSetup& R
   const int u = (W.tr ? sy : sx) + (W.ou << 16), v = (W.tr ? sx : sy) - (W.v0 << 16);
   const int du_c = W.tr ? R.isin : R.icos, dv_c = W.tr ? R.icos : R.isin;    // one output column right
   const int du_r = W.tr ? R.icos : -R.isin, dv_r = W.tr ? -R.isin : R.icos;  // one output row down
-  constexpr int chunk_rows = 4 * TG::RPC;
+  constexpr int NW = NT / 64;  // waves: the chunks are dealt over them
+  constexpr int chunk_rows = NW * TG::RPC;
   const uint32_t sb = (uint32_t)W.sb;
   uint64_t pxy = ((uint64_t)(uint32_t)v << 32) | (uint32_t)u;
   const uint64_t col_step = (uint64_t)(((int64_t)dv_c << 32) + (int64_t)du_c);
   const uint64_t chunk_step = (uint64_t)(((int64_t)(chunk_rows * dv_r) << 32) + (int64_t)(chunk_rows * du_r));
   const int hy0 = P.anchor_y - P.hero_w / 2;
-  for (int ch = wave; ch < TG::NCH; ch += 4) {
+  for (int ch = wave; ch < TG::NCH; ch += NW) {
     const int Yc = oy0 + ch * TG::RPC;  // the chunk's first row (uniform)
     const int Y = Yc + lrow;
     const uint32_t vo = (uint32_t)(Y * TG::S + X);
@@ -1615,7 +1629,7 @@ __device__ __forceinline__ void tile_out(const cbev_params& P, const RotSetup& R
     overlay16(P, fov, vo, X, Y, (unsigned)(Yc + TG::RPC - 1 - hy0) < (unsigned)(TG::RPC - 1 + P.hero_w), w);
     const u32x4_nt v4 = {w[0], w[1], w[2], w[3]};
     for (int k = 0; k < nout; ++k)  // streamed out: keep the L2 for the map and the records
-      __builtin_nontemporal_store(v4, (u32x4_nt*)(out + (int64_t)k * out_stride + vo));
+      store16_frame(out + (int64_t)k * out_stride + vo, v4);
     pxy += chunk_step;
   }
 }
@@ -1625,7 +1639,7 @@ __device__ __forceinline__ void tile_out(const cbev_params& P, const RotSetup& R
 // (!J.fast): compose clipping (black outside the rotated surface) and the
 // rotozoom background (bg for samples outside the source crop). The window
 // coordinates are kept as two ints (they may leave the window here).
-template <int G>
+template <int G, int NT>
 __device__ __forceinline__ void tile_out_check(const cbev_params& P, const RotSetup& R, const TileWin& W, int ox0,
                                                int oy0, const uint8_t* __restrict__ lds, uint32_t bg,
                                                uint8_t* __restrict__ out, int nout, int64_t out_stride,
@@ -1643,7 +1657,7 @@ __device__ __forceinline__ void tile_out_check(const cbev_params& P, const RotSe
   }
   const int du_c = W.tr ? R.isin : R.icos, dv_c = W.tr ? R.icos : R.isin;
   const int hy0 = P.anchor_y - P.hero_w / 2;
-  for (int ch = wave; ch < TG::NCH; ch += 4) {
+  for (int ch = wave; ch < TG::NCH; ch += NT / 64) {
     const int Yc = oy0 + ch * TG::RPC;
     const int Y = Yc + lrow;
     const uint32_t vo = (uint32_t)(Y * TG::S + X);
@@ -1666,14 +1680,14 @@ __device__ __forceinline__ void tile_out_check(const cbev_params& P, const RotSe
     overlay16(P, fov, vo, X, Y, (unsigned)(Yc + TG::RPC - 1 - hy0) < (unsigned)(TG::RPC - 1 + P.hero_w), w);
     const u32x4_nt v4 = {w[0], w[1], w[2], w[3]};
     for (int k = 0; k < nout; ++k)
-      __builtin_nontemporal_store(v4, (u32x4_nt*)(out + (int64_t)k * out_stride + vo));
+      store16_frame(out + (int64_t)k * out_stride + vo, v4);
   }
 }
 
 // Tile t of one env's observation by the whole 256-thread workgroup: window,
 // staging, paint (PAINT: the step's frame; the reset frame draws no actors),
 // output, into `nout` frames out + k * out_stride.
-template <int G, bool PAINT>
+template <int G, bool PAINT, int NT = 256>
 __device__ __forceinline__ void raster_tile(const KArgs& K, const DRec& r, const RasterJob& J, int t,
                                             uint8_t* __restrict__ out, int nout, int64_t out_stride,
                                             uint8_t* __restrict__ lds) {
@@ -1686,17 +1700,18 @@ __device__ __forceinline__ void raster_tile(const KArgs& K, const DRec& r, const
   }
   PaintPre pq{};
   if (PAINT) pq = raster_paint_fetch(r);  // in flight under the staging
-  stage_tile(K, W, lds);
+  stage_tile<NT>(K, W, lds);
   __syncthreads();
   if (PAINT) {
     CBEV_STAMP(2, 1);
-    paint_tile(K, r, pq, J, W, lds);
+    paint_tile<NT>(K, r, pq, J, W, lds);
     CBEV_STAMP(2, 2);
   }
   if (J.fast) {
-    tile_out<G>(K.P, J.R, W, ox0, oy0, lds, out, nout, out_stride, K.fov);
+    tile_out<G, NT>(K.P, J.R, W, ox0, oy0, lds, out, nout, out_stride, K.fov);
   } else {
-    tile_out_check<G>(K.P, J.R, W, ox0, oy0, lds, crop_background(K, r, J, PAINT), out, nout, out_stride, K.fov);
+    tile_out_check<G, NT>(K.P, J.R, W, ox0, oy0, lds, crop_background(K, r, J, PAINT), out, nout, out_stride,
+                          K.fov);
   }
 }
 
@@ -1722,8 +1737,10 @@ __device__ __forceinline__ void xcd_tile_of_wg(int w, int n, int T, int* e, int*
 // One (env, tile) per workgroup; register target from the LDS-limited residency
 // (Tiles::wgs_per_cu workgroups of 4 waves per CU = waves per SIMD). The raster
 // kernels declare no static LDS: the gathers address the LDS absolutely.
+constexpr int kRasterNT = 256;  // k_raster's workgroup size
 template <int G>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(Tiles<G>::wgs_per_cu)))
+__global__ __launch_bounds__(kRasterNT)
+__attribute__((amdgpu_waves_per_eu(Tiles<G>::wgs_per_cu * kRasterNT / 256 > 8 ? 8 : Tiles<G>::wgs_per_cu * kRasterNT / 256)))
 void k_raster(KArgs K, uint8_t* __restrict__ recs, int n, uint8_t* __restrict__ frames) {
   extern __shared__ __align__(16) uint8_t lds[];
   CBEV_STAMP(2, 0);
@@ -1733,7 +1750,7 @@ void k_raster(KArgs K, uint8_t* __restrict__ recs, int n, uint8_t* __restrict__ 
   const int64_t SS = (int64_t)K.P.size * K.P.size;
   const DRec r = bind_rec(recs + (int64_t)e * K.L.record_bytes, K.L, K.C);
   const RasterJob J = raster_job<false, G>(K, r);
-  raster_tile<G, true>(K, r, J, t, frames + e * SS, 1, 0, lds);
+  raster_tile<G, true, kRasterNT>(K, r, J, t, frames + e * SS, 1, 0, lds);
   CBEV_STAMP(2, 3);
 }
 
@@ -2083,6 +2100,7 @@ __host__ __device__ __forceinline__ CollScratchLayout coll_scratch_layout(const 
 }
 enum { CS_TGT_LAST = 0, CS_ACT_LAST = 1, CS_NAS = 2, CS_BSEG = 5, CS_TILE = 6 };
 struct CollPre {  // one env's reduced pre-pass results, as seen by collide_env
+  double spx, spy;              // the Stanley set point cx / cy[target index] (loaded in S4)
   int tgt_last, act_last, nas;  // last visible target / actor hit (-1: none), actors_state entries
   const uint32_t* hitw;         // visible targets hit (cleared from the visibility bits)
   double ttc_carl, ttc_sh;      // min compute_ttc_raw / compute_ttc over the actors (INF if none)
@@ -2248,7 +2266,7 @@ __device__ __forceinline__ void collide_env(const KArgs& K, DRec r, int e, const
 
   // scene_info / controller_info (scene.py:206-225, stanley_controller.py:125-163)
   const int tidx = hi[CBEV_HI_TIDX];
-  const double spx = r.cx[tidx], spy = r.cy[tidx];
+  const double spx = pre.spx, spy = pre.spy;
   double dist2wp;
   {
     double dx = x - spx, dy = y - spy;
@@ -2538,6 +2556,21 @@ __global__ __launch_bounds__(256) void k_ego(uint8_t* __restrict__ recs, int n, 
       s2y[j] = s2g.cy[i];
     }
   }
+  // S5's targets (env tid / tpe, points sub, sub + tpe, ...): the first S5_PF of
+  // a thread's route points, loaded now; the Stanley set point of S6's thread
+  // (tid < ne) is loaded in S4 once S3 has moved the target index
+  constexpr int S5_PF = 4;
+  const int tpe5 = 256 / ne, k5 = tid / tpe5, sub5 = tid - k5 * tpe5;
+  double t5x[S5_PF], t5y[S5_PF];
+  if (k5 < ne_eff) {
+    const DRec g = bind_rec(recs + (int64_t)(e0 + k5) * rb, K.L, K.C);
+#pragma unroll
+    for (int j = 0; j < S5_PF; ++j) {
+      const int i = min(sub5 + j * tpe5, K.C.route_cap - 1);
+      t5x[j] = g.cx[i];
+      t5y[j] = g.cy[i];
+    }
+  }
   // S1: the actions, and from the record's yaw and speed cos / sin of the yaw
   // (wave 0, which runs the chain) beside tan(clip(delta)) (wave 1)
   float ag = 0.f, asa = 0.f, ab = 0.f;
@@ -2616,6 +2649,7 @@ __global__ __launch_bounds__(256) void k_ego(uint8_t* __restrict__ recs, int n, 
   }
   __syncthreads();
   // S4
+  double s6spx = 0.0, s6spy = 0.0;  // S6's set point (wave 0 lane k = S6's thread of env k)
   if (lane < ne_eff) {
     if (wave == 1) {
       hero_env_comfort(rec(lane));
@@ -2626,6 +2660,9 @@ __global__ __launch_bounds__(256) void k_ego(uint8_t* __restrict__ recs, int n, 
       d_sincos(yaw, &pre[lane].syaw, &pre[lane].cyaw);
     } else if (wave == 0) {
       const DRec r = rec(lane);
+      const int tidx = r.hi[CBEV_HI_TIDX];  // after S3 (scene_info, scene.py:206-225)
+      s6spx = r.cx[tidx];
+      s6spy = r.cy[tidx];
       const double x = r.hd[CBEV_HD_X], y = r.hd[CBEV_HD_Y];
       const int tx = (int)d_clip(rint(x), 0, P.map_w - 1), ty = (int)d_clip(rint(y), 0, P.map_h - 1);
       const int tile = d_map_texel(K, tx + P.pad, ty + P.pad);  // world.py:159-165
@@ -2712,8 +2749,18 @@ __global__ __launch_bounds__(256) void k_ego(uint8_t* __restrict__ recs, int n, 
       int* I = (int*)(sk + SL.ints);
       const int hrx = I[3], hry = I[4];
       const int nt = r.hi[CBEV_HI_NROUTE];
-#pragma unroll 4
-      for (int i = sub; i < nt; i += tpe) {
+#pragma unroll
+      for (int j = 0; j < S5_PF; ++j) {  // the prefetched points (k == k5, sub == sub5)
+        const int i = sub + j * tpe;
+        if (i >= nt || !((r.vis[i >> 5] >> (i & 31)) & 1u)) continue;
+        const int sz = (i < nt - 1) ? 2 : 4;
+        const int trx = d_rect_lo(t5x[j], P.pad, sz), try_ = d_rect_lo(t5y[j], P.pad, sz);
+        if (hrx < trx + sz && hry < try_ + sz && hrx + hw > trx && hry + hw > try_) {
+          atomicOr((uint32_t*)(sk + SL.hitw) + (i >> 5), 1u << (i & 31));
+          atomicMax(&I[CS_TGT_LAST], i);
+        }
+      }
+      for (int i = sub + S5_PF * tpe; i < nt; i += tpe) {  // routes past the prefetched points
         if (!((r.vis[i >> 5] >> (i & 31)) & 1u)) continue;
         const int sz = (i < nt - 1) ? 2 : 4;
         const int trx = d_rect_lo(r.cx[i], P.pad, sz), try_ = d_rect_lo(r.cy[i], P.pad, sz);
@@ -2777,7 +2824,9 @@ __global__ __launch_bounds__(256) void k_ego(uint8_t* __restrict__ recs, int n, 
   // S6
   if (tid < ne_eff) {
     const DRec r = rec(tid);
-    const CollPre cp = coll_reduce_serial(scr + tid * SL.bytes, SL, r.hi[CBEV_HI_NACT], r.hi[CBEV_HI_NRAW]);
+    CollPre cp = coll_reduce_serial(scr + tid * SL.bytes, SL, r.hi[CBEV_HI_NACT], r.hi[CBEV_HI_NRAW]);
+    cp.spx = s6spx;  // tid < ne: wave 0, the lane that loaded them in S4
+    cp.spy = s6spy;
     collide_env(K, r, e0 + tid, cp, reward_out, term_out, trunc_out, cause_out, info_out);
   }
   __syncthreads();
@@ -3271,9 +3320,9 @@ static int raster_tiles(int size) { return size == 64 ? Tiles<1>::T : size == 12
 static void launch_raster(const cbev_ctx* c, const KArgs& K, void* records, int n, uint8_t* frames, hipStream_t s) {
   const size_t lb = raster_lds_bytes(c->P);
   switch (c->P.size) {
-    case 64: hipLaunchKernelGGL(k_raster<1>, dim3(n * Tiles<1>::T), dim3(256), lb, s, K, (uint8_t*)records, n, frames); break;
-    case 128: hipLaunchKernelGGL(k_raster<2>, dim3(n * Tiles<2>::T), dim3(256), lb, s, K, (uint8_t*)records, n, frames); break;
-    default: hipLaunchKernelGGL(k_raster<4>, dim3(n * Tiles<4>::T), dim3(256), lb, s, K, (uint8_t*)records, n, frames); break;
+    case 64: hipLaunchKernelGGL(k_raster<1>, dim3(n * Tiles<1>::T), dim3(kRasterNT), lb, s, K, (uint8_t*)records, n, frames); break;
+    case 128: hipLaunchKernelGGL(k_raster<2>, dim3(n * Tiles<2>::T), dim3(kRasterNT), lb, s, K, (uint8_t*)records, n, frames); break;
+    default: hipLaunchKernelGGL(k_raster<4>, dim3(n * Tiles<4>::T), dim3(kRasterNT), lb, s, K, (uint8_t*)records, n, frames); break;
   }
 }
 

@@ -155,6 +155,9 @@ def build_scenes(cfg_dict: dict, caps: dict, difficulty: str, seed0: int, record
             if time.perf_counter() > deadline:
                 raise TimeoutError(f"built {done} of {len(gids)} scenes in {timeout:.0f} s")
             got, recs = pool.poll(timeout=5.0)
+            if not got and not any(pr.is_alive() for pr in pool._procs):
+                raise RuntimeError("every scene worker exited (a spawned worker re-imports the caller's __main__: "
+                                   "guard the caller's top-level code with `if __name__ == '__main__'`)")
             for k, g in enumerate(got):
                 out[where[g]] = recs[k]
             done += len(got)

@@ -150,6 +150,51 @@ def test_episode_info_after_bank_resets_and_held_infos():
     env.close()
 
 
+def test_refresh_bank_releases_only_dead_contexts():
+    """A fast bank refresh (every step, far more retired scenario contexts than
+    the keep window) never releases the context of a scene an env still runs,
+    and terminations report the context of the bank scene they were reset from
+    (carlabev.py:182); the context table stays bounded."""
+    n, B = 6, 4
+    env = _env(n)
+    env.reset(seed=7, options=_opts("rt_easy_v1"))
+    env.attach_bank(env.build_bank([900 + k for k in range(B)], _opts("rt_easy_v1")))
+    env.RETIRED_CTX_KEEP = 2  # release as soon as 2 N ids are retired
+    host = env._new_record_buffer(B)
+    rng = np.random.default_rng(1)
+    slot, tag = 0, 0
+    env_tag = {}  # env -> tag of the bank scene it was last reset from (None: untagged)
+    bank_tag = [None] * B  # build_bank's scenes carry the builder's contexts, no tag
+    seen = 0
+    for t in range(400):
+        obs, r, term, trunc, infos = env.step(rng.integers(0, 9, n))
+        done = term.cpu().numpy().astype(bool)
+        for i in np.flatnonzero(done):
+            if env_tag.get(i) is not None:
+                assert infos["episode_info"]["tag"][i] == env_tag[i], (t, i)
+                seen += 1
+        if done.any():
+            rows0 = env.bank_rows_used()
+            env.reset_terminated()
+            for k, i in enumerate(np.flatnonzero(done)):
+                env_tag[i] = bank_tag[(rows0 + k) % B]
+        # refresh the whole bank with fresh tagged scenes every step
+        ctxs = []
+        for k in range(B):
+            env.build_reset_record(host[k], 2000 + tag, _opts("rt_easy_v1"))
+            ctxs.append({"tag": tag})
+            tag += 1
+        slot = env.refresh_bank(slot, host, ctxs)
+        bank_tag = [c["tag"] for c in ctxs]
+        live = set(env.record_ctx_ids().tolist())
+        assert live <= set(env._ctx_table), (t, live - set(env._ctx_table))
+        assert len(env._ctx_table) <= 4 * n + 2 * B + 16, len(env._ctx_table)
+        if seen >= 4 and t > 50:
+            break
+    assert tag > 2 * n + env.RETIRED_CTX_KEEP and seen >= 1
+    env.close()
+
+
 def test_obs_copies_and_input_validation():
     env = _env(6, info_mode="none")
     env2 = _env(6, info_mode="none")

@@ -13,42 +13,49 @@ import sys
 
 import numpy as np
 
-REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-sys.path.insert(0, REPO)
 
-ap = argparse.ArgumentParser()
-ap.add_argument("--config", type=int, default=2)
-ap.add_argument("--reps", type=int, default=50)
-ap.add_argument("--angles", default="0,3,10,30,45,60,80,87,90")
-a = ap.parse_args()
+def main():
+    REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    sys.path.insert(0, REPO)
 
-import torch  # noqa: E402
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", type=int, default=2)
+    ap.add_argument("--reps", type=int, default=50)
+    ap.add_argument("--angles", default="0,3,10,30,45,60,80,87,90")
+    a = ap.parse_args()
 
-import bench  # noqa: E402
-from carlabev_env_amd import layout as LY  # noqa: E402
-from carlabev_env_amd._lib import check, lib  # noqa: E402
+    import torch  # noqa: E402
 
-cfgd = bench.CONFIGS[a.config]
-n = cfgd["envs"]
-dev = torch.device("cuda", 0)
-env, host = bench.build_env(cfgd, n, 0, dev)
-acts = torch.zeros((n,), dtype=torch.int32, device=dev) if env.params.action_kind == 0 else \
-    torch.zeros((n, 3), dtype=torch.float32, device=dev)
-env.auto_obs = False
-base = env.records.clone()
-L = lib()
-yaw_off = env.layout.off["hd"] + 8 * LY.HD["YAW"]
-ms = ctypes.c_double()
-for deg in [float(x) for x in a.angles.split(",")]:
-    env.records.copy_(base)
-    r = env.records.view(n, -1)
-    yaw = torch.full((n,), np.radians(deg), dtype=torch.float64, device=dev)
-    r[:, yaw_off:yaw_off + 8] = yaw.view(torch.uint8).view(n, 8)
-    env.step_async_only(acts)
-    torch.cuda.synchronize()
-    times = []
-    for _ in range(3):
-        check(L.cbev_profile_raster(env._ctx, env.records.data_ptr(), n, env.frames().data_ptr(), a.reps, None,
-                                    ctypes.byref(ms)), "profile_raster")
-        times.append(ms.value * 1e3)  # ms per launch
-    print(f"heading {deg:5.1f} deg: raster {np.median(times):6.2f} us/launch", flush=True)
+    import bench  # noqa: E402
+    from carlabev_env_amd import layout as LY  # noqa: E402
+    from carlabev_env_amd._lib import check, lib  # noqa: E402
+
+    cfgd = bench.CONFIGS[a.config]
+    n = cfgd["envs"]
+    dev = torch.device("cuda", 0)
+    env, host, _start = bench.build_env(cfgd, n, 0, dev)
+    acts = torch.zeros((n,), dtype=torch.int32, device=dev) if env.params.action_kind == 0 else \
+        torch.zeros((n, 3), dtype=torch.float32, device=dev)
+    env.auto_obs = False
+    base = env.records.clone()
+    L = lib()
+    yaw_off = env.layout.off["hd"] + 8 * LY.HD["YAW"]
+    ms = ctypes.c_double()
+    for deg in [float(x) for x in a.angles.split(",")]:
+        env.records.copy_(base)
+        r = env.records.view(n, -1)
+        yaw = torch.full((n,), np.radians(deg), dtype=torch.float64, device=dev)
+        r[:, yaw_off:yaw_off + 8] = yaw.view(torch.uint8).view(n, 8)
+        env.step_async_only(acts)
+        torch.cuda.synchronize()
+        times = []
+        for _ in range(3):
+            check(L.cbev_profile_raster(env._ctx, env.records.data_ptr(), n, env.frames().data_ptr(), a.reps, None,
+                                        ctypes.byref(ms)), "profile_raster")
+            times.append(ms.value * 1e3)  # ms per launch
+        print(f"heading {deg:5.1f} deg: raster {np.median(times):6.2f} us/launch", flush=True)
+
+
+
+if __name__ == "__main__":
+    main()

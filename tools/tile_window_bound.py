@@ -5,9 +5,9 @@ A tile of TC x TR output pixels samples the crop at an affine map of its
 pixels: the corners' samples are (TC - 1, TR - 1) steps of the rotated unit
 vectors apart, so the window (in the orientation k_raster picks: rows along
 the axis the output rows run closer to) spans at most floor(extent) + 2 texels
-each way. A row of the window is the 16-byte chunks of the byte map covering
-its texels from a column offset of up to 3 (umin & 3), plus 4 bytes (an odd
-dword count per row).
+each way. A row of the window is the 16-texel chunks covering its texels at
+any start offset (the staging reads the nibble map from 8-texel boundaries),
+16 bytes each in LDS, plus 4 bytes (an odd dword count per row).
 """
 import math
 
@@ -21,7 +21,7 @@ def bound(tc: int, tr: int, step_deg: float = 0.01):
             c, s = s, c
         eu, ev = (tc - 1) * c + (tr - 1) * s, (tc - 1) * s + (tr - 1) * c
         nu, nv = math.floor(eu) + 2, math.floor(ev) + 2
-        nc = (3 + nu - 1) // 16 + 2
+        nc = (nu + 14) // 16 + 1  # 16-texel chunks over nu texels, at any start offset within a chunk
         b = nv * (16 * nc + 4)
         if b > best:
             best, arg = b, (i * step_deg, nu, nv, nc)
