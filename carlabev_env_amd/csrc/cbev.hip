@@ -1227,8 +1227,12 @@ __global__ __launch_bounds__(256) void k_actors(KArgs K, uint8_t* __restrict__ r
 // columns, the (x, y) roles of the 16.16 sample coordinates swap, and the
 // gathers again step along window rows at every heading.
 __host__ __device__ constexpr int tile_cols(int S) { return S < 128 ? S : 128; }
-// tile rows per size (S = 64, 128, 256)
-__host__ __device__ constexpr int tile_rows(int S) { return S <= 64 ? 64 : S == 128 ? 128 : 64; }
+// tile rows per size (S = 64, 128, 256): 128 x 128 tiles at S = 256 too (config
+// 5: 57.6 us per launch against 67.7 with 128 x 64 tiles at 7 workgroups per CU
+// and 97.6 with 64 x 64 at 8: fewer, larger items pay the per-item record ->
+// window -> map-load chain, which at S = 256 reads a 9.2 MB byte map from
+// beyond the L2, fewer times)
+__host__ __device__ constexpr int tile_rows(int S) { return S <= 64 ? 64 : 128; }
 template <int G>
 struct Tiles {
   static constexpr int S = 64 * G;
