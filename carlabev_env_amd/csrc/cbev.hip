@@ -726,7 +726,7 @@ __device__ __forceinline__ void ego_stage_in(uint8_t* lds, const uint8_t* __rest
   const int total = ne * n;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  if (wave < 2) return;  // waves 0 and 1 run S1 meanwhile (k_ego)
+  if (wave < 2) return;  // waves 0 and 1 run S2 meanwhile (k_ego)
   for (int b = (wave - 2) * 64; b < total; b += 128) {
     const int q = b + lane;
     if (q < total) {
@@ -823,6 +823,7 @@ __device__ __forceinline__ double d_hero_delta(double v, float sa) {
 // tan(clip(delta)) of State.update.
 struct HeroPre {
   double cyaw, syaw, tdelta;
+  float g, sa, b;  // the decoded action (S1, for S3's thread)
 };
 
 // Ego update, part A (one thread per env): target index update, throttle /
@@ -2492,8 +2493,8 @@ __device__ __forceinline__ void butterfly(int tpe, F&& f) {
 // k_raster:
 //   S0  the ne records' prefixes (HD .. vis_draw) staged into LDS
 //       (ego_stage_in), then the actions decoded
-//   S1  cos / sin of the yaw (wave 0) beside tan(clip(delta)) (wave 1), from
-//       the record in HBM while waves 2 and 3 stage it
+//   S1  cos / sin of the yaw (wave 2) beside tan(clip(delta)) (wave 3), from
+//       the record in HBM, on the staging waves after they issued the LDS-DMA
 //   S2  Controller.calc_target_index over (env, route point) pairs: hypot, the
 //       first minimum (stanley_controller.py:51-62)
 //   S3  the ego chain, one thread per env (BaseAgent.physics_step, hero.py:88-138)
@@ -2575,13 +2576,18 @@ __global__ __launch_bounds__(256) void k_ego(uint8_t* __restrict__ recs, int n, 
       t5y[j] = g.cy[i];
     }
   }
-  // S1: the actions, and from the record's yaw and speed cos / sin of the yaw
-  // (wave 0, which runs the chain) beside tan(clip(delta)) (wave 1)
-  float ag = 0.f, asa = 0.f, ab = 0.f;
-  if (wave <= 1 && lane < ne_eff) {
+  // S1 on the staging waves once their LDS-DMA is issued (they would otherwise
+  // idle until the barrier; S2 on waves 0 and 1 then starts as soon as its own
+  // loads land): the actions, and from the record's yaw and speed cos / sin of
+  // the yaw (wave 2) beside tan(clip(delta)) (wave 3), into LDS for S3
+  if (wave >= 2 && lane < ne_eff) {
+    float ag, asa, ab;
     d_decode_action(K, actions, e0 + lane, &ag, &asa, &ab);
     const double* ghd = (const double*)(recs + (int64_t)(e0 + lane) * rb + K.L.hd);
-    if (wave == 0) {
+    if (wave == 2) {
+      pre[lane].g = ag;
+      pre[lane].sa = asa;
+      pre[lane].b = ab;
       d_sincos(ghd[CBEV_HD_YAW], &pre[lane].syaw, &pre[lane].cyaw);
     } else {
       const double max_steer = 30.0 * (CB_PI / 180.0);
@@ -2648,7 +2654,7 @@ __global__ __launch_bounds__(256) void k_ego(uint8_t* __restrict__ recs, int n, 
   CBEV_STAMP(0, 2);
   // S3
   if (tid < ne_eff) {
-    const float gsb[3] = {ag, asa, ab};
+    const float gsb[3] = {pre[tid].g, pre[tid].sa, pre[tid].b};
     hero_env_a(K, rec(tid), e0 + tid, actions, best[tid], pre[tid], gsb);
   }
   __syncthreads();
