@@ -106,3 +106,4 @@ EXPORTED_SYMBOLS = ("cbev_abi_version", "cbev_params_size", "cbev_layout_of", "c
                     "cbev_wall_clock_hz", "cbev_termination_count", "cbev_pack_frames", "cbev_unpack_frames")
 
 ERR_ACTION_INDEX = 1  # CBEV_ERR_ACTION_INDEX (include/cbev.h)
+ERR_RASTER_WINDOW = 2  # CBEV_ERR_RASTER_WINDOW (include/cbev.h)

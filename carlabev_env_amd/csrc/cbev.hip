@@ -1244,8 +1244,12 @@ struct Tiles {
   static constexpr int NCH = TR / RPC;                             // chunks per tile (dealt over 4 waves)
   // window bound over every heading (TC - 1 and TR - 1 sample steps of the
   // rotated unit vectors, + 2 texels of floor spread, + the 16-byte chunk
-  // rounding at a column offset of up to 3): tools/tile_window_bound.py
-  static constexpr int lds_bytes = TC == 64 ? 10560 : TR == 64 ? 22688 : 38384;
+  // rounding at a column offset of up to 3: tools/tile_window_bound.py), plus
+  // one spare row of the widest pitch (the bound is sampled over
+  // float headings; the kernel's 16.16 isin / icos never exceed them, the spare
+  // row covers the sampling). A larger window is clamped and flagged
+  // (CBEV_ERR_RASTER_WINDOW), which the GPU parity tests assert never happens.
+  static constexpr int lds_bytes = TC == 64 ? 10672 : TR == 64 ? 22688 : 38584;
   static constexpr int wgs_per_cu = 163840 / lds_bytes > 8 ? 8 : 163840 / lds_bytes;
 };
 
@@ -1930,10 +1934,13 @@ __global__ __launch_bounds__(256) void k_reset_copy(KArgs K, uint8_t* __restrict
 // 256 thread prefixes, the unit within the thread and the set bit within the
 // unit: O(n / 4096 + log) per workgroup, no pass over the selected envs per
 // piece. Pieces as in k_reset_copy (16 KB, RESET_PU loads per thread in
-// flight), dealt over the grid. The cursor is double-buffered by call parity:
-// every workgroup reads cursor_in, workgroup 0 writes cursor_out = cursor_in +
-// the selected count (the next call reads it), so rows advance only when a
-// reset actually ran. The leading scalar arguments are preloaded into SGPRs.
+// flight), dealt over the grid. One device cursor: every workgroup reads it at
+// its start, and the workgroup that finishes last (a self-resetting ticket
+// counter: the one whose increment returns grid - 1) writes cursor + the
+// selected count and zeroes the ticket, so the cursor advances on the device
+// alone (graph replays and calls on different streams hand out fresh rows; rows
+// advance only when a reset runs). The leading scalar arguments are preloaded
+// into SGPRs.
 __device__ __forceinline__ uint32_t nonzero_bytes16(const uint4 v) {  // bit b: byte b of the 16 is nonzero
   uint32_t m = 0;
   const uint32_t w[4] = {v.x, v.y, v.z, v.w};
@@ -1947,8 +1954,8 @@ __device__ __forceinline__ uint32_t nonzero_bytes16(const uint4 v) {  // bit b: 
 
 __global__ __launch_bounds__(256) void k_reset_mask(int n, int n_bank, int rb, int SS, int n_frames, int upt,
                                                     const uint8_t* __restrict__ mask,
-                                                    const unsigned long long* __restrict__ cursor_in,
-                                                    unsigned long long* __restrict__ cursor_out,
+                                                    unsigned long long* __restrict__ cursor,
+                                                    unsigned* __restrict__ ticket,
                                                     uint8_t* __restrict__ recs, const uint8_t* __restrict__ bank,
                                                     const uint8_t* __restrict__ bank_frames,
                                                     uint8_t* __restrict__ ring, KArgs K) {
@@ -1957,7 +1964,7 @@ __global__ __launch_bounds__(256) void k_reset_mask(int n, int n_bank, int rb, i
   int* wsum = pre + 257;                     // [4] wave totals
   uint16_t* um = (uint16_t*)(lds + 1056);    // [256 * upt] unit masks
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const unsigned long long cur = *cursor_in;  // loaded beside the mask
+  const unsigned long long cur = *(volatile const unsigned long long*)cursor;  // loaded beside the mask
   const int nu = (n + 15) >> 4;               // 16-byte units
   const bool vec = ((uintptr_t)mask & 15u) == 0;
   int cnt = 0;
@@ -1988,7 +1995,6 @@ __global__ __launch_bounds__(256) void k_reset_mask(int n, int n_bank, int rb, i
   for (int w = 0; w < wave; ++w) wpre += wsum[w];
   pre[tid] = wpre + inc - cnt;
   const int total = wsum[0] + wsum[1] + wsum[2] + wsum[3];
-  if (blockIdx.x == 0 && tid == 0) *cursor_out = cur + (unsigned long long)total;
   __syncthreads();
   const int pf = reset_pieces(SS), ppe = pf + reset_pieces(rb);
   const int pieces = total * ppe;
@@ -2033,6 +2039,13 @@ __global__ __launch_bounds__(256) void k_reset_mask(int n, int n_bank, int rb, i
       }
     }
     if (c == pf && threadIdx.x == 0 && K.stats != nullptr) K.stats[e].t0 = (double)wall_clock64();
+  }
+  // every thread's reads of the cursor are behind this barrier (the value was used
+  // or discarded); the last workgroup to arrive moves the cursor for the next call
+  __syncthreads();
+  if (tid == 0 && atomicAdd(ticket, 1u) == gridDim.x - 1) {
+    *(volatile unsigned long long*)cursor = cur + (unsigned long long)total;
+    atomicExch(ticket, 0u);
   }
 }
 // k_reset_mask's dynamic LDS: prefixes + wave totals (1056 B) + the unit masks
@@ -3190,10 +3203,9 @@ struct cbev_ctx {
   int ep_ring, ep_n;
   int64_t step_count;         // cbev_step calls since cbev_set_episode_stats
   double tick_s;
-  // bank cursor of cbev_reset_masked, double-buffered by call parity: [cur_parity]
-  // holds the rows taken so far, the next call writes the other one
+  // bank cursor of cbev_reset_masked (cur_dev[0]: rows taken so far) and the
+  // k_reset_mask ticket counter (the low word of cur_dev[1]), both on the device
   unsigned long long* cur_dev;  // [2]
-  int cur_parity;
   const uint8_t* last_term;   // term buffer of the last cbev_step (cbev_reset_terminated's mask)
   int last_n;                 // n of the last cbev_step (0: none yet)
 };
@@ -3721,13 +3733,10 @@ int cbev_reset_masked(cbev_ctx* c, void* records, int n, const uint8_t* mask, co
   const int64_t pieces = (int64_t)n * ppe;
   const int grid = pieces >= RESET_MASK_WGS ? RESET_MASK_WGS : (int)pieces;
   const int upt = reset_mask_upt(n);
-  const unsigned long long* cin = c->cur_dev + c->cur_parity;
-  unsigned long long* cout = c->cur_dev + (c->cur_parity ^ 1);
   hipLaunchKernelGGL(k_reset_mask, dim3(grid), dim3(256), reset_mask_lds(n), (hipStream_t)stream, n, n_bank,
-                     (int)c->L.record_bytes, SS, n_frames, upt, mask, cin, cout, (uint8_t*)records,
-                     (const uint8_t*)bank, bank_frames, frames, K);
+                     (int)c->L.record_bytes, SS, n_frames, upt, mask, c->cur_dev, (unsigned*)(c->cur_dev + 1),
+                     (uint8_t*)records, (const uint8_t*)bank, bank_frames, frames, K);
   HIP_TRY(hipGetLastError());
-  c->cur_parity ^= 1;
   return CBEV_OK;
 }
 
@@ -3744,7 +3753,7 @@ int cbev_bank_cursor(cbev_ctx* c, int64_t* cursor) {
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(hipDeviceSynchronize());  // the resets are queued on the caller's (non-blocking) stream
   unsigned long long v = 0;
-  HIP_TRY(hipMemcpy(&v, c->cur_dev + c->cur_parity, sizeof v, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(&v, c->cur_dev, sizeof v, hipMemcpyDeviceToHost));
   *cursor = (int64_t)v;
   return CBEV_OK;
 }

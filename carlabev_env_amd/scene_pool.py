@@ -141,6 +141,10 @@ def build_scenes(cfg_dict: dict, caps: dict, difficulty: str, seed0: int, record
     gid order), built by `workers` spawned processes: the same bytes the
     in-process HostResetBuilder writes (tests/test_scene_pool.py)."""
     gids = [int(g) for g in gids]
+    if len(set(gids)) != len(gids):  # one output row per gid: a repeated gid would leave a row unfilled
+        from collections import Counter
+        dup = sorted(g for g, c in Counter(gids).items() if c > 1)[:8]
+        raise ValueError(f"build_scenes: repeated scene ids {dup}")
     out = np.zeros((len(gids), record_bytes), np.uint8)
     if not gids:
         return out

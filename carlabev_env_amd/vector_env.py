@@ -89,14 +89,14 @@ class StepInfos(Mapping):
     "episode": ..., "_episode": mask}), built from the device's episode rows the
     first time it is read. Not reading it costs no host work and no sync."""
 
-    __slots__ = ("_env", "_step", "_d", "__weakref__")
+    __slots__ = ("_env", "_step", "_stream", "_d", "__weakref__")
 
-    def __init__(self, env, step: int):
-        self._env, self._step, self._d = env, step, None
+    def __init__(self, env, step: int, stream: int):
+        self._env, self._step, self._stream, self._d = env, step, stream, None
 
     def _get(self) -> dict:
         if self._d is None:
-            self._d = self._env._materialize_infos(self._step)
+            self._d = self._env._materialize_infos(self._step, self._stream)
             self._env = None
         return self._d
 
@@ -248,6 +248,7 @@ class CarlaBEVVectorEnv:
         self._bank_ctx_ids = None  # scenario-context id per bank row set by refresh_bank
         self._retired_ctx: deque = deque()  # ids of overwritten bank rows, released oldest first
         self._stepped = False
+        self._step_stream = 0
         self.auto_obs = True  # reset_from_bank also expands the wire observation
         self._closed = False
 
@@ -556,8 +557,10 @@ class CarlaBEVVectorEnv:
         self.head = (self.head + 1) % self.F
         frames = self._p_full if self.resize else self._p_ring + self.head * self._slot_bytes
         rec, rew, term, trunc, cause, info = self._p_step
+        stream = self._stream()
         check(lib().cbev_step(self._ctx, rec, self.num_envs, a.data_ptr(), frames, rew, term, trunc, cause, info,
-                              self._stream()), "cbev_step")
+                              stream), "cbev_step")
+        self._step_stream = stream.value or 0  # the step's rows are waited for on this stream (StepInfos)
         self._stepped = True
         if self.resize:
             self._resize_into_ring(None, all_slots=False)
@@ -565,8 +568,10 @@ class CarlaBEVVectorEnv:
 
     def errors(self, clear: bool = True) -> int:
         """CBEV_ERR_* bits the kernels raised since the last call (synchronises the
-        device): ERR_ACTION_INDEX = a device action tensor held a discrete index outside
-        [-n, n), the reference's IndexError; that env stepped action 0."""
+        device): ERR_ACTION_INDEX (1) = a device action tensor held a discrete index outside
+        [-n, n), the reference's IndexError; that env stepped action 0.
+        ERR_RASTER_WINDOW (2) = a raster tile's crop window exceeded its LDS bound
+        (an internal invariant the GPU parity tests assert; that frame is not valid)."""
         flags = ctypes.c_int32()
         check(lib().cbev_error_flags(self._ctx, ctypes.byref(flags), 1 if clear else 0), "cbev_error_flags")
         return int(flags.value)
@@ -604,7 +609,7 @@ class CarlaBEVVectorEnv:
         from the device only when accessed; {} otherwise."""
         if self.info_mode != "full":
             return {}
-        infos = StepInfos(self, self._ep_step - 1)
+        infos = StepInfos(self, self._ep_step - 1, self._step_stream)
         self._pending.append((self._ep_step - 1, weakref.ref(infos)))
         return infos
 
@@ -618,15 +623,20 @@ class CarlaBEVVectorEnv:
             if obj is not None:
                 obj._get()
 
-    def _materialize_infos(self, step: int) -> dict:
+    def _materialize_infos(self, step: int, stream: int = 0) -> dict:
         """Vector-env infos of `step` from its device rows (SyncVectorEnv._add_info
         layout: {"episode_info": {key: array, "_key": mask}, "_episode_info": mask,
         "episode": {"r", "l", "t"} + masks, "_episode": mask}; {} when no env
         terminated). The scenario context is merged as carlabev.py:181-182 does.
-        Waits for the device (a step's rows stay valid until EP_RING - 1 newer
-        steps are queued, and _flush_pending reads them before that), so a step
-        enqueues no event or other marker for its infos."""
-        torch.cuda.synchronize(self.device)
+        Waits for the stream the step was launched on (`stream`, its raw handle;
+        0: the legacy default stream), not the whole device: RCCL gathers and the
+        caller's other streams keep running. A step's rows stay valid until
+        EP_RING - 1 newer steps are queued, and _flush_pending reads them before
+        that, so a step enqueues no event or other marker for its infos."""
+        if stream:
+            torch.cuda.ExternalStream(stream, device=self.device).synchronize()
+        else:
+            torch.cuda.default_stream(self.device).synchronize()
         slot = step % EP_RING
         cnt = int(self._ep_counts[slot].item())
         if cnt == 0:

@@ -96,8 +96,62 @@ def info_of(v, cause):
     return o
 
 
+class EpisodeStatsOn:
+    """The device episode statistics (cbev_set_episode_stats) on a context, as
+    the bench's info_mode "full" runs the step: k_ego then updates the per-env
+    Stats accumulators and writes a summary row per termination (the kernel
+    variant the headline measures). `check(step, term, sample, views, causes)`
+    compares this step's rows with the oracle's records of the sampled envs."""
+    RING = 4
+
+    def __init__(self, ctx, n):
+        self.n = n
+        self.stats = torch.zeros((n, LY.STATS_BYTES), dtype=torch.uint8, device="cuda")
+        self.rows = torch.zeros((self.RING, n, len(LY.EP)), dtype=torch.float64, device="cuda")
+        self.counts = torch.zeros(self.RING, dtype=torch.int32, device="cuda")
+        check(lib().cbev_set_episode_stats(ctx, ptr(self.stats), n, ptr(self.rows), ptr(self.counts), self.RING),
+              "episode_stats")
+        self.episodes = np.zeros(n, np.int64)
+        self.rows_seen = 0
+
+    def check(self, step, term_all, sample, views, causes):
+        slot = step % self.RING
+        cnt = int(self.counts[slot].item())
+        assert cnt == int(term_all.sum()), (step, cnt, int(term_all.sum()))
+        rows = self.rows[slot, :cnt].cpu().numpy()
+        by_env = {int(r[LY.EP["ENV"]]): r for r in rows}
+        assert len(by_env) == cnt, (step, "one row per terminated env")
+        for j, e in enumerate(sample):
+            v = views[j]
+            if not v.i("TERM"):
+                assert e not in by_env, (step, e)
+                continue
+            r = by_env[int(e)]
+            assert r[LY.EP["CAUSE"]] == causes[j] == v.i("CAUSE"), (step, e)
+            assert r[LY.EP["EPISODE"]] == self.episodes[e], (step, e)
+            assert r[LY.EP["LENGTH"]] == v.i("EP_LEN"), (step, e)
+            assert np.isclose(r[LY.EP["RETURN"]], v.h("EP_RETURN"), rtol=1e-9, atol=1e-12), (step, e)
+            ln = max(v.i("EP_LEN"), 1)
+            assert np.isclose(r[LY.EP["MEAN_SPEED"]], v.h("EP_SPEED") / ln, rtol=1e-9, atol=1e-12), (step, e)
+            self.rows_seen += 1
+        for e in np.flatnonzero(term_all):
+            self.episodes[e] += 1
+
+
+def error_flags(ctx):
+    f = ctypes.c_int32()
+    check(lib().cbev_error_flags(ctx, ctypes.byref(f), 1), "error_flags")
+    return f.value
+
+
 def run_parity(kinds, n_envs, steps, size=128, profile="discrete9_v1", reward="carl_base_v1", seed0=0, anchor_y=0.5,
-               act_seed=1234, edit=None, fov=False, caps=CAPS_FULL, options=None):
+               act_seed=1234, edit=None, fov=False, caps=CAPS_FULL, options=None, acts=None, on_step=None,
+               stats=False):
+    """Every env of a small batch stepped on the device and by the oracle, compared
+    whole after each step. acts: an explicit (steps, n[, 3]) action array instead of
+    the seeded stream; on_step(t, views, causes): sees the oracle's records after
+    each step (branch-coverage probes); stats: with the device episode statistics
+    on (EpisodeStatsOn), the headline's k_ego variant."""
     cfg, P, padded, layout, builder = world(size, profile, reward, anchor_y, caps=caps)
     if options is None:
         recs, _ = build_records(builder, n_envs, kinds, seed0=seed0)
@@ -127,7 +181,9 @@ def run_parity(kinds, n_envs, steps, size=128, profile="discrete9_v1", reward="c
             h_frames[e][omask] = 8  # CBEV_PX_BLACK
     torch.cuda.synchronize()
     assert np.array_equal(d_frames.cpu().numpy(), h_frames), "reset frames differ"
-    acts = action_stream(P, n_envs, steps, seed=act_seed)
+    if acts is None:
+        acts = action_stream(P, n_envs, steps, seed=act_seed)
+    st = EpisodeStatsOn(dw.ctx, n_envs) if stats else None
     rew = torch.zeros(n_envs, dtype=torch.float64, device="cuda")
     term = torch.zeros(n_envs, dtype=torch.uint8, device="cuda")
     trunc = torch.zeros_like(term)
@@ -160,7 +216,13 @@ def run_parity(kinds, n_envs, steps, size=128, profile="discrete9_v1", reward="c
         got = info.cpu().numpy()
         assert np.array_equal(got[:, 13:], want[:, 13:]), (t, "info ints")
         assert np.allclose(got, want, rtol=1e-6, atol=1e-6), (t, "info")
+        if st is not None:
+            st.check(t, term.cpu().numpy(), np.arange(n_envs), views, h_cause)
+        if on_step is not None:
+            on_step(t, views, h_cause)
         n_term += int(term.sum())
+    # no raster tile exceeded its LDS window bound (CBEV_ERR_RASTER_WINDOW), no bad action index
+    assert error_flags(dw.ctx) == 0
     return n_term
 
 
@@ -417,14 +479,16 @@ def _sample_envs(n, k=160):
 
 
 def run_full_size(kinds, n_envs, size=128, profile="discrete9_v1", seed0=0, steps=16, distinct=160, act_seed=1,
-                  caps=CAPS_FULL):
+                  caps=CAPS_FULL, stats=False, push=0):
     """The HIP path at a benchmarked batch size (grid shapes, XCD placement and
     staging batches of the bench) against the oracle on a sampled subset of envs.
     `distinct` seeded scenes are tiled over the batch (env e gets scene e % distinct);
     every env gets its own action stream, so tiled copies diverge. `caps` are the
     record capacities: bench.CONFIGS' for the bench configurations, so the kernel
     shapes the bench line measures (k_actors skipped at actor_cap 0, the k_ego
-    workgroup size, the record layout) are the ones checked here."""
+    workgroup size, the record layout) are the ones checked here. stats: the device
+    episode statistics on (the bench's info_mode "full", EpisodeStatsOn); push:
+    envs per step moved off the road before the step (terminations in every step)."""
     cfg, P, padded, layout, builder = world(size, profile, "carl_base_v1", 0.5, caps=caps)
     base, _ = build_records(builder, distinct, kinds, seed0=seed0)
     recs = base[np.arange(n_envs) % distinct].copy()
@@ -450,7 +514,19 @@ def run_full_size(kinds, n_envs, size=128, profile="discrete9_v1", seed0=0, step
     trunc = torch.zeros_like(term)
     cause = torch.zeros(n_envs, dtype=torch.int32, device="cuda")
     info = torch.zeros((n_envs, 16), dtype=torch.float32, device="cuda")
+    st = EpisodeStatsOn(dw.ctx, n_envs) if stats else None
+    prng = np.random.default_rng(act_seed + 1)
+    pos = {int(e): j for j, e in enumerate(sample)}
     for t in range(steps):
+        if push:  # the same edit on the device records and the oracle's copies
+            ids = np.unique(np.concatenate([prng.choice(n_envs, size=push, replace=False), sample[t::7][:4]]))
+            sel_p = torch.from_numpy(ids).cuda()
+            h = d_recs[sel_p].cpu().numpy()
+            for k, e in enumerate(ids):
+                LY.RecordView(h[k], layout).hd[LY.HD["X"]] += 60.0
+                if int(e) in pos:
+                    LY.RecordView(h_recs[pos[int(e)]], layout).hd[LY.HD["X"]] += 60.0
+            d_recs[sel_p] = torch.from_numpy(h).cuda()
         a = torch.from_numpy(np.ascontiguousarray(acts[t])).cuda()
         check(L.cbev_step(dw.ctx, ptr(d_recs), n_envs, ptr(a), ptr(d_frames), ptr(rew), ptr(term), ptr(trunc),
                           ptr(cause), ptr(info), None), "step")
@@ -471,6 +547,11 @@ def run_full_size(kinds, n_envs, size=128, profile="discrete9_v1", seed0=0, step
         assert np.allclose(rew[sel].cpu().numpy(), [v.h("REWARD") for v in views], rtol=1e-9, atol=1e-12)
         got, want = info[sel].cpu().numpy(), np.stack([info_of(v, 0) for v in views])
         assert np.array_equal(got[:, 13:], want[:, 13:]) and np.allclose(got, want, rtol=1e-6, atol=1e-6), t
+        if st is not None:
+            st.check(t, term.cpu().numpy(), sample, views, h_cause)
+    assert error_flags(dw.ctx) == 0
+    if st is not None:
+        assert st.rows_seen > 0
     return len(sample)
 
 
@@ -478,6 +559,59 @@ def test_full_size_config2():
     """Config 2 at its bench capacities (actor_cap 0: k_actors is not launched,
     k_ego runs with empty actor groups and its 16-env workgroups)."""
     assert run_full_size(["rt_no_traffic_v1"], 4096, seed0=10_000, caps=bench_caps(2)) >= 128
+
+
+def test_full_size_config2_stats_on():
+    """The headline's kernel variant: config 2 at its bench batch and capacities with
+    the device episode statistics on (info_mode "full": k_ego's d_episode_summary
+    path), oracle-checked per step; envs pushed off the road terminate every step,
+    and each sampled termination's summary row matches the oracle's record."""
+    assert run_full_size(["rt_no_traffic_v1"], 4096, seed0=10_000, steps=12, caps=bench_caps(2), stats=True,
+                         push=300) >= 128
+
+
+def test_parity_stats_on_small():
+    """Every env, every step, with the episode statistics on (odd batch: partial
+    k_ego workgroups), at config 2's and config 5's capacities."""
+    run_parity(["rt_no_traffic_v1"], 37, 120, seed0=10_000, caps=bench_caps(2), stats=True)
+    run_parity(["mix3"], 19, 60, size=256, seed0=30_000, caps=bench_caps(5), stats=True)
+
+
+def test_parity_carl_safety_v1_branches():
+    """carl_safety_v1 (config/reward_profiles.py:25-37) on rt_hard traffic: the
+    lane-centre term with exponent 1.5 (the general pow, carl_reward_fn.py:248),
+    the 0.05 off-lane factor on sidewalk / far-off-lane steps (P > 0 there,
+    carl_reward_fn.py:254) and the TTC threshold of 5 s (carl_reward_fn.py:273);
+    each branch is hit in some step (counted on the oracle's records, which the
+    device records equal)."""
+    hits = {"pow": 0, "off_lane": 0, "off_lane_pos": 0, "ttc": 0}
+
+    def probe(t, views, causes):
+        for v in views:
+            if 0.15 < v.h("P_LANE") < 1.0:
+                hits["pow"] += 1
+            if v.h("P_OFF") == 0.05:
+                hits["off_lane"] += 1
+                hits["off_lane_pos"] += v.h("REWARD") > 0
+            if v.h("P_TTC") == 0.5:
+                hits["ttc"] += 1
+
+    run_parity(["rt_hard_v1"], 29, 100, reward="carl_safety_v1", seed0=20_000, act_seed=7, caps=bench_caps(3),
+               on_step=probe)
+    assert all(v > 0 for v in hits.values()), hits
+
+
+def test_parity_discrete13_every_index():
+    """discrete13_v1 (config/action_profiles.py:51): the 13-entry table, every index
+    0..12 and every negative index -13..-1 (Python's discrete_actions[int(a)]
+    counts from the end, envs/spaces.py:43-47), on rt_medium traffic."""
+    n, steps = 26, 120
+    rng = np.random.default_rng(13)
+    acts = rng.integers(-13, 13, size=(steps, n)).astype(np.int32)
+    acts[0] = np.arange(-13, 13)
+    acts[1] = np.arange(-13, 13)[::-1]
+    assert set(np.unique(acts).tolist()) == set(range(-13, 13))
+    run_parity(["rt_medium_v1"], n, steps, profile="discrete13_v1", seed0=600, caps=bench_caps(4), acts=acts)
 
 
 def test_full_size_config3():
@@ -655,3 +789,41 @@ def test_reset_masked_mass_termination_and_edits():
     assert torch.equal(d_recs, want_r) and torch.equal(ring, want_f)
     cursor += k
     assert _cursor(L, dw) == cursor and cursor > B  # wrapped around the bank
+
+
+def test_reset_cursor_advances_under_graph_replay():
+    """The bank cursor lives on the device: a cbev_reset_terminated
+    captured once in a HIP graph and replayed hands out the next rows on every
+    replay (each replay = the eager call: the k-th selected env gets bank[(cursor +
+    k) % B]) and the cursor moves by the selected count each time."""
+    n, B, F = 45, 17, 2
+    P, layout, dw, d_bank, bf, d_recs, ring = _bank_world(n, B, F, bench_caps(2), ["rt_no_traffic_v1"], 3100, 3900)
+    L = lib()
+    rew = torch.zeros(n, dtype=torch.float64, device="cuda")
+    term = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    trunc = torch.zeros_like(term)
+    cause = torch.zeros(n, dtype=torch.int32, device="cuda")
+    a = torch.zeros(n, dtype=torch.int32, device="cuda")
+    check(L.cbev_step(dw.ctx, ptr(d_recs), n, ptr(a), ptr(ring[0]), ptr(rew), ptr(term), ptr(trunc), ptr(cause),
+                      None, None), "step")
+    torch.cuda.synchronize()
+    sel = (np.arange(n) % 4 == 1)
+    term.copy_(torch.from_numpy(sel.astype(np.uint8)))  # the mask the captured reset reads
+    side = torch.cuda.Stream()
+    g = torch.cuda.CUDAGraph()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        with torch.cuda.graph(g, stream=side):
+            check(L.cbev_reset_terminated(dw.ctx, ptr(d_recs), n, ptr(d_bank), B, ptr(bf), ptr(ring), F,
+                                          P_(torch.cuda.current_stream().cuda_stream)), "reset_term (capture)")
+    torch.cuda.synchronize()
+    cursor = _cursor(L, dw)  # capture runs nothing
+    assert cursor == 0
+    for rep in range(3):
+        want_r, want_f, k = _want_reset(L, dw, d_recs, ring, d_bank, bf, sel, cursor, F)
+        g.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(d_recs, want_r) and torch.equal(ring, want_f), rep
+        cursor += k
+        assert _cursor(L, dw) == cursor, rep
+    assert cursor > B  # wrapped: every replay took fresh rows

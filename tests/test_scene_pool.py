@@ -54,3 +54,14 @@ def test_pool_reports_worker_errors():
 def test_scene_options_mix():
     assert [scene_options("mix3", g)["scene"] for g in range(4)] == ["lead_brake", "jaywalk", "red_light_runner",
                                                                        "lead_brake"]
+
+
+def test_build_scenes_rejects_repeated_ids():
+    """One output row per scene id: a repeated id would leave a row of zeros that
+    looks like a record, so build_scenes refuses it before any work."""
+    import pytest
+    from carlabev_env_amd.scene_pool import build_scenes
+    cfg = EnvConfig(size=128, obs_size=(128, 128), render_mode="rgb_array").model_dump()
+    _, layout = make_builder(cfg, CAPS)
+    with pytest.raises(ValueError, match="repeated scene ids"):
+        build_scenes(cfg, CAPS, "rt_easy_v1", 0, layout.record_bytes, [3, 5, 3], workers=1)
