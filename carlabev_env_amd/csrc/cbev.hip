@@ -1847,7 +1847,8 @@ __global__ __launch_bounds__(256) void k_bank_frames(KArgs K, const uint8_t* __r
 // XCD's env blocks and counts the selected envs' pieces in env order, taking
 // every WPX-th.
 #define RESET_PU 4                      // 16-byte loads per thread in flight
-#define RESET_MASK_WGS 512              // k_reset_mask's grid cap
+#define RESET_MASK_WGS 512              // k_reset_mask's grid cap (and its cursor copies)
+#define CBEV_CURSOR_STRIDE 16           // 128 bytes between the cursor copies
 #define CBEV_RESET_MASK_MAX_N (1 << 20)  // k_reset_mask's unit masks: 2 B per 16 envs of LDS
 #define RESET_PIECE (4096 * RESET_PU)   // bytes per piece
 __host__ __device__ __forceinline__ int reset_pieces(int64_t bytes) {
@@ -1934,12 +1935,14 @@ __global__ __launch_bounds__(256) void k_reset_copy(KArgs K, uint8_t* __restrict
 // 256 thread prefixes, the unit within the thread and the set bit within the
 // unit: O(n / 4096 + log) per workgroup, no pass over the selected envs per
 // piece. Pieces as in k_reset_copy (16 KB, RESET_PU loads per thread in
-// flight), dealt over the grid. One device cursor: every workgroup reads it at
-// its start, and the workgroup that finishes last (a self-resetting ticket
-// counter: the one whose increment returns grid - 1) writes cursor + the
-// selected count and zeroes the ticket, so the cursor advances on the device
-// alone (graph replays and calls on different streams hand out fresh rows; rows
-// advance only when a reset runs). The leading scalar arguments are preloaded
+// flight), dealt over the grid. The cursor lives on the device only, one copy
+// per possible workgroup (RESET_MASK_WGS slots, a 128-byte line each): workgroup
+// w reads slot w at its start and, since every workgroup counts the same
+// selected total, writes cursor + total back to its own slots (w, w + grid, ...)
+// at its end. No workgroup touches another's slot, so there is no ordering
+// between workgroups to arrange and no atomic (a ticket counter taken by all 512
+// workgroups cost 4.5 us per call); graph replays hand out fresh rows, and rows
+// advance only when a reset runs. The leading scalar arguments are preloaded
 // into SGPRs.
 __device__ __forceinline__ uint32_t nonzero_bytes16(const uint4 v) {  // bit b: byte b of the 16 is nonzero
   uint32_t m = 0;
@@ -1955,7 +1958,6 @@ __device__ __forceinline__ uint32_t nonzero_bytes16(const uint4 v) {  // bit b: 
 __global__ __launch_bounds__(256) void k_reset_mask(int n, int n_bank, int rb, int SS, int n_frames, int upt,
                                                     const uint8_t* __restrict__ mask,
                                                     unsigned long long* __restrict__ cursor,
-                                                    unsigned* __restrict__ ticket,
                                                     uint8_t* __restrict__ recs, const uint8_t* __restrict__ bank,
                                                     const uint8_t* __restrict__ bank_frames,
                                                     uint8_t* __restrict__ ring, KArgs K) {
@@ -1964,7 +1966,7 @@ __global__ __launch_bounds__(256) void k_reset_mask(int n, int n_bank, int rb, i
   int* wsum = pre + 257;                     // [4] wave totals
   uint16_t* um = (uint16_t*)(lds + 1056);    // [256 * upt] unit masks
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const unsigned long long cur = *(volatile const unsigned long long*)cursor;  // loaded beside the mask
+  const unsigned long long cur = cursor[CBEV_CURSOR_STRIDE * blockIdx.x];  // this workgroup's copy, beside the mask
   const int nu = (n + 15) >> 4;               // 16-byte units
   const bool vec = ((uintptr_t)mask & 15u) == 0;
   int cnt = 0;
@@ -2040,13 +2042,10 @@ __global__ __launch_bounds__(256) void k_reset_mask(int n, int n_bank, int rb, i
     }
     if (c == pf && threadIdx.x == 0 && K.stats != nullptr) K.stats[e].t0 = (double)wall_clock64();
   }
-  // every thread's reads of the cursor are behind this barrier (the value was used
-  // or discarded); the last workgroup to arrive moves the cursor for the next call
-  __syncthreads();
-  if (tid == 0 && atomicAdd(ticket, 1u) == gridDim.x - 1) {
-    *(volatile unsigned long long*)cursor = cur + (unsigned long long)total;
-    atomicExch(ticket, 0u);
-  }
+  // this workgroup's cursor copies for the next call (total > 0: unchanged otherwise)
+  if (total > 0)
+    for (int w = blockIdx.x + gridDim.x * tid; w < RESET_MASK_WGS; w += gridDim.x * 256)
+      cursor[CBEV_CURSOR_STRIDE * w] = cur + (unsigned long long)total;
 }
 // k_reset_mask's dynamic LDS: prefixes + wave totals (1056 B) + the unit masks
 __host__ __forceinline__ int reset_mask_upt(int n) { return ((n + 15) / 16 + 255) / 256; }
@@ -3203,9 +3202,9 @@ struct cbev_ctx {
   int ep_ring, ep_n;
   int64_t step_count;         // cbev_step calls since cbev_set_episode_stats
   double tick_s;
-  // bank cursor of cbev_reset_masked (cur_dev[0]: rows taken so far) and the
-  // k_reset_mask ticket counter (the low word of cur_dev[1]), both on the device
-  unsigned long long* cur_dev;  // [2]
+  // bank cursor of cbev_reset_masked (rows taken so far): one copy per
+  // k_reset_mask workgroup, all equal between calls
+  unsigned long long* cur_dev;  // [RESET_MASK_WGS * CBEV_CURSOR_STRIDE]
   const uint8_t* last_term;   // term buffer of the last cbev_step (cbev_reset_terminated's mask)
   int last_n;                 // n of the last cbev_step (0: none yet)
 };
@@ -3419,8 +3418,9 @@ int cbev_create(const cbev_params* params, const cbev_caps* caps, int device, cb
   if (e == hipSuccess) e = hipMemset(c->err_dev, 0, sizeof(int32_t));
   if (e == hipSuccess) e = hipMalloc(&c->nterm_dev, sizeof(unsigned long long));
   if (e == hipSuccess) e = hipMemset(c->nterm_dev, 0, sizeof(unsigned long long));
-  if (e == hipSuccess) e = hipMalloc(&c->cur_dev, 2 * sizeof(unsigned long long));
-  if (e == hipSuccess) e = hipMemset(c->cur_dev, 0, 2 * sizeof(unsigned long long));
+  const size_t cur_bytes = (size_t)RESET_MASK_WGS * CBEV_CURSOR_STRIDE * sizeof(unsigned long long);
+  if (e == hipSuccess) e = hipMalloc(&c->cur_dev, cur_bytes);
+  if (e == hipSuccess) e = hipMemset(c->cur_dev, 0, cur_bytes);
   if (e == hipSuccess) {
     int khz = 0;  // wall_clock64() rate
     e = hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device);
@@ -3734,8 +3734,7 @@ int cbev_reset_masked(cbev_ctx* c, void* records, int n, const uint8_t* mask, co
   const int grid = pieces >= RESET_MASK_WGS ? RESET_MASK_WGS : (int)pieces;
   const int upt = reset_mask_upt(n);
   hipLaunchKernelGGL(k_reset_mask, dim3(grid), dim3(256), reset_mask_lds(n), (hipStream_t)stream, n, n_bank,
-                     (int)c->L.record_bytes, SS, n_frames, upt, mask, c->cur_dev, (unsigned*)(c->cur_dev + 1),
-                     (uint8_t*)records, (const uint8_t*)bank, bank_frames, frames, K);
+                     (int)c->L.record_bytes, SS, n_frames, upt, mask, c->cur_dev, (uint8_t*)records, (const uint8_t*)bank, bank_frames, frames, K);
   HIP_TRY(hipGetLastError());
   return CBEV_OK;
 }
