@@ -654,9 +654,21 @@ __device__ unsigned g_hwid[CBEV_NSTAMP][4096];                   // HW_ID (SE / 
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(xcc_));                           \
     g_hwid[kern][w_] = xcc_;                                                                     \
   }
+// k_raster_pipe: thread 0 of workgroup w stamps item j's phases (top of the
+// iteration after the DMA wait, paint done, next item issued, output done)
+__device__ unsigned long long g_pst[1024][32][5];
+__device__ unsigned g_phw[1024];
+#define CBEV_PSTAMP(j, slot)                                                   \
+  if (threadIdx.x == 0 && blockIdx.x < 1024 && (j) < 32) {                    \
+    g_pst[blockIdx.x][j][slot] = __builtin_amdgcn_s_memtime();                \
+    unsigned hw_;                                                              \
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw_));          \
+    g_phw[blockIdx.x] = hw_;                                                   \
+  }
 #else
 #define CBEV_STAMP(kern, slot)
 #define CBEV_STAMPW(kern, slot)
+#define CBEV_PSTAMP(j, slot)
 #endif
 
 // ---- record staging for k_ego. A workgroup owns `ne` envs (a divisor of 64,
@@ -1885,8 +1897,11 @@ __device__ __forceinline__ TileWin pipe_window(const KArgs& K, const RasterJob& 
 #define CBEV_WAIT_VM(N) __builtin_amdgcn_s_waitcnt(0x0F70 | (N))
 
 template <int G, bool JOB>
-__global__ __launch_bounds__(kPipeNT) void k_raster_pipe(KArgs K, PaintJob PJ, uint8_t* __restrict__ recs, int n,
-                                                          uint8_t* __restrict__ frames) {
+__global__ __launch_bounds__(kPipeNT) void k_raster_pipe(KArgs K, PaintJob PJ, const uint8_t* __restrict__ recs_c,
+                                                          int n, uint8_t* __restrict__ frames) {
+  // the records are only read here (const, restrict): their uniform loads (render
+  // set-up, counts) can be scalar loads, which wait on lgkmcnt, not on the DMA's vmcnt
+  uint8_t* recs = (uint8_t*)recs_c;
   extern __shared__ __align__(16) uint8_t lds[];
   using TG = Tiles<G>;
   static_assert(TG::NCH == 2 * (kPipeNT / 64), "two output chunks (two stores) per wave and item");
@@ -1896,18 +1911,21 @@ __global__ __launch_bounds__(kPipeNT) void k_raster_pipe(KArgs K, PaintJob PJ, u
   const int64_t rb = K.L.record_bytes;
   int k = blockIdx.x;
   if (k >= items) return;
+  CBEV_PSTAMP(31, 4);
   int e, t;
   xcd_tile_of_wg(k, n, TG::T, &e, &t);
   RasterJob J = raster_job<false, G>(K, bind_rec(recs + (int64_t)e * rb, K.L, K.C));
   PaintCounts pc = paint_counts(bind_rec(recs + (int64_t)e * rb, K.L, K.C));
   TileWin W = pipe_window<G>(K, J, t);
   pipe_issue<G, JOB>(K, PJ, recs + (int64_t)e * rb, W, lds);
-  for (int b = 0, first = 1;; b ^= 1, first = 0) {
+  for (int b = 0, first = 1, it = 0;; b ^= 1, first = 0, ++it) {
     // this item's DMA: every wave retires its own (only this wave's two output
     // stores of the previous item are younger), then the workgroup's
+    CBEV_PSTAMP(it, 0);
     if (first) CBEV_WAIT_VM(0);
     else CBEV_WAIT_VM(2);
     lds_barrier();
+    CBEV_PSTAMP(it, 1);
     uint8_t* slot = lds + b * slot_bytes;
     {
       const DRec r = bind_rec(recs + (int64_t)e * rb, K.L, K.C);
@@ -1915,6 +1933,7 @@ __global__ __launch_bounds__(kPipeNT) void k_raster_pipe(KArgs K, PaintJob PJ, u
       const PaintPre pq = raster_paint_fetch(rp, pc);
       paint_tile<kPipeNT>(K, rp, pq, J, W, slot);  // ends with a barrier: the other slot's output is over too
     }
+    CBEV_PSTAMP(it, 2);
     // the next item into the other slot, in flight under this item's output
     const int kn = k + (int)gridDim.x;
     int en = 0, tn = 0;
@@ -1928,6 +1947,7 @@ __global__ __launch_bounds__(kPipeNT) void k_raster_pipe(KArgs K, PaintJob PJ, u
       Wn = pipe_window<G>(K, Jn, tn);
       pipe_issue<G, JOB>(K, PJ, recs + (int64_t)en * rb, Wn, lds + (b ^ 1) * slot_bytes);
     }
+    CBEV_PSTAMP(it, 3);
     const int ox0 = (t % TG::NTX) * TG::TC, oy0 = (t / TG::NTX) * TG::TR;
     if (J.fast) {
       tile_out<G, kPipeNT>(K.P, J.R, W, ox0, oy0, slot, frames + e * SS, 1, 0, K.fov, b * slot_bytes);
@@ -1936,6 +1956,7 @@ __global__ __launch_bounds__(kPipeNT) void k_raster_pipe(KArgs K, PaintJob PJ, u
       tile_out_check<G, kPipeNT>(K.P, J.R, W, ox0, oy0, slot, crop_background(K, r, J, true), frames + e * SS, 1, 0,
                                  K.fov);
     }
+    CBEV_PSTAMP(it, 4);
     if (kn >= items) break;
     k = kn;
     e = en;
@@ -3390,6 +3411,7 @@ struct cbev_ctx {
   unsigned long long* cur_dev;  // [RESET_MASK_WGS * CBEV_CURSOR_STRIDE]
   int n_cu;                   // compute units (k_raster_pipe's persistent grid: two workgroups each)
   bool pipe_job;              // k_raster_pipe mirrors the paint job into LDS (pipe_job_fits)
+  bool raster_tile;           // TEMP A/B (CBEV_RASTER_TILE=1): round 4's raster
   const uint8_t* last_term;   // term buffer of the last cbev_step (cbev_reset_terminated's mask)
   int last_n;                 // n of the last cbev_step (0: none yet)
 };
@@ -3545,6 +3567,14 @@ static void launch_raster(const cbev_ctx* c, const KArgs& K, void* records, int 
                        (uint8_t*)records, n, frames);
     return;
   }
+  if (c->raster_tile) {  // TEMP A/B: round 4's one-item-per-workgroup raster
+    const size_t lb = raster_lds_bytes(c->P);
+    if (c->P.size == 128)
+      hipLaunchKernelGGL(k_raster<2>, dim3(n * Tiles<2>::T), dim3(kRasterNT), lb, s, K, (uint8_t*)records, n, frames);
+    else
+      hipLaunchKernelGGL(k_raster<4>, dim3(n * Tiles<4>::T), dim3(kRasterNT), lb, s, K, (uint8_t*)records, n, frames);
+    return;
+  }
   const int items = n * raster_tiles(c->P.size);
   const int cap = 2 * c->n_cu;
   const int grid = items <= cap ? items : cap & ~7;
@@ -3658,6 +3688,7 @@ int cbev_create(const cbev_params* params, const cbev_caps* caps, int device, cb
                             (int)raster_lds_bytes(P));
   if (e == hipSuccess) e = hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, device);
   if (c->n_cu < 8) c->n_cu = 8;
+  c->raster_tile = getenv("CBEV_RASTER_TILE") && atoi(getenv("CBEV_RASTER_TILE")) == 1;
   if (P.size != 64) {
     c->pipe_job = pipe_job_fits(c);
     if (e == hipSuccess)
@@ -4196,6 +4227,12 @@ int cbev_resize_obs(cbev_ctx* c, const uint8_t* frames, int n, const uint8_t* ma
 }
 
 #ifdef CBEV_TIMING
+// timing builds only: k_raster_pipe's stamps [1024][32][5] and HW_IDs [1024]
+int cbev_debug_pipe_times(unsigned long long* st, unsigned* hw) {
+  if (hipMemcpyFromSymbol(st, HIP_SYMBOL(g_pst), sizeof(g_pst)) != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(hw, HIP_SYMBOL(g_phw), sizeof(g_phw)) != hipSuccess) return -1;
+  return 0;
+}
 // timing builds only: copy the phase stamps [6][4096][4] (u64 s_memtime ticks), realtime stamps,
 // XCC ids | HW_ID << 32
 int cbev_debug_times(unsigned long long* out_host) {
