@@ -1360,6 +1360,30 @@ __device__ __forceinline__ RasterJob raster_job(const KArgs& K, const DRec& r) {
   return J;
 }
 
+// k_raster_pipe's view of an env's render set-up and rect counts: the HI ints
+// read through a constant-address-space pointer (the records are not written
+// during the raster), so they are scalar loads; their waits are lgkmcnt ones and
+// never drain the LDS-DMA the pipe keeps in flight on vmcnt
+typedef __attribute__((address_space(4))) const int32_t cint4;
+struct PipeHead {
+  RasterJob J;
+  PaintCounts pc;
+};
+template <int G>
+__device__ __forceinline__ PipeHead pipe_head(const KArgs& K, const uint8_t* rec) {
+  cint4* hi = (cint4*)(rec + K.L.hi);
+  PipeHead h;
+  h.J.xmin = hi[CBEV_HI_RS_XMIN];
+  h.J.ymin = hi[CBEV_HI_RS_YMIN];
+  int32_t* w = (int32_t*)&h.J.R;
+#pragma unroll
+  for (int k = 0; k < CBEV_RS_WORDS; ++k) w[k] = hi[CBEV_HI_RS_R90 + k];
+  h.J.fast = hi[CBEV_HI_RS_FAST] != 0;
+  raster8_affine(h.J.R, raster_row_texels(64 * G, K.P.crop));
+  h.pc = PaintCounts{hi[CBEV_HI_NACT], hi[CBEV_HI_NVEH], hi[CBEV_HI_NROUTE], hi[CBEV_HI_NTL]};
+  return h;
+}
+
 // A tile's window in (u, v) = (x, y), or (y, x) when transposed: crop rows
 // v in [v0, v0 + nv), the 16-byte chunks [c0, c0 + nc) of the (transposed)
 // byte map's row from umin & ~3; crop (u, v) is LDS byte (v - v0) * sb + ou + u.
@@ -1882,11 +1906,11 @@ __device__ __forceinline__ void pipe_issue(const KArgs& K, const PaintJob& PJ, c
 }
 
 template <int G>
-__device__ __forceinline__ TileWin pipe_window(const KArgs& K, const RasterJob& J, int t) {
+__device__ __forceinline__ TileWin pipe_window(const KArgs& K, const RasterJob& J, int t, int32_t* __restrict__ err) {
   using TG = Tiles<G>;
   TileWin W = tile_window<G>(K.P, J, (t % TG::NTX) * TG::TC, (t / TG::NTX) * TG::TR);
   if (W.nv * W.sb > TG::lds_bytes) {  // cannot happen (Tiles::lds_bytes bounds every heading): flag, stay in bounds
-    if (threadIdx.x == 0) atomicOr(K.err, CBEV_ERR_RASTER_WINDOW);
+    if (threadIdx.x == 0) atomicOr(err, CBEV_ERR_RASTER_WINDOW);
     W.nv = TG::lds_bytes / W.sb;
   }
   return W;
@@ -1898,9 +1922,11 @@ __device__ __forceinline__ TileWin pipe_window(const KArgs& K, const RasterJob& 
 
 template <int G, bool JOB>
 __global__ __launch_bounds__(kPipeNT) void k_raster_pipe(KArgs K, PaintJob PJ, const uint8_t* __restrict__ recs_c,
-                                                          int n, uint8_t* __restrict__ frames) {
-  // the records are only read here (const, restrict): their uniform loads (render
-  // set-up, counts) can be scalar loads, which wait on lgkmcnt, not on the DMA's vmcnt
+                                                          int n, uint8_t* __restrict__ frames,
+                                                          int32_t* __restrict__ err) {
+  // the records are only read here (const, restrict; the only stores go to frames
+  // and err, restrict too): their uniform loads (render set-up, counts) can be
+  // scalar loads, which wait on lgkmcnt, not on the DMA's vmcnt
   uint8_t* recs = (uint8_t*)recs_c;
   extern __shared__ __align__(16) uint8_t lds[];
   using TG = Tiles<G>;
@@ -1914,9 +1940,10 @@ __global__ __launch_bounds__(kPipeNT) void k_raster_pipe(KArgs K, PaintJob PJ, c
   CBEV_PSTAMP(31, 4);
   int e, t;
   xcd_tile_of_wg(k, n, TG::T, &e, &t);
-  RasterJob J = raster_job<false, G>(K, bind_rec(recs + (int64_t)e * rb, K.L, K.C));
-  PaintCounts pc = paint_counts(bind_rec(recs + (int64_t)e * rb, K.L, K.C));
-  TileWin W = pipe_window<G>(K, J, t);
+  PipeHead h = pipe_head<G>(K, recs + (int64_t)e * rb);
+  RasterJob J = h.J;
+  PaintCounts pc = h.pc;
+  TileWin W = pipe_window<G>(K, J, t, err);
   pipe_issue<G, JOB>(K, PJ, recs + (int64_t)e * rb, W, lds);
   for (int b = 0, first = 1, it = 0;; b ^= 1, first = 0, ++it) {
     // this item's DMA: every wave retires its own (only this wave's two output
@@ -1926,6 +1953,13 @@ __global__ __launch_bounds__(kPipeNT) void k_raster_pipe(KArgs K, PaintJob PJ, c
     else CBEV_WAIT_VM(2);
     lds_barrier();
     CBEV_PSTAMP(it, 1);
+    // the next item's render set-up and counts (scalar loads, in flight under the paint)
+    const int kn = k + (int)gridDim.x;
+    int en = 0, tn = 0;
+    if (kn < items) {
+      xcd_tile_of_wg(kn, n, TG::T, &en, &tn);
+      h = pipe_head<G>(K, recs + (int64_t)en * rb);
+    }
     uint8_t* slot = lds + b * slot_bytes;
     {
       const DRec r = bind_rec(recs + (int64_t)e * rb, K.L, K.C);
@@ -1935,16 +1969,13 @@ __global__ __launch_bounds__(kPipeNT) void k_raster_pipe(KArgs K, PaintJob PJ, c
     }
     CBEV_PSTAMP(it, 2);
     // the next item into the other slot, in flight under this item's output
-    const int kn = k + (int)gridDim.x;
-    int en = 0, tn = 0;
     RasterJob Jn = J;
     TileWin Wn = W;
     PaintCounts pcn = pc;
     if (kn < items) {
-      xcd_tile_of_wg(kn, n, TG::T, &en, &tn);
-      Jn = raster_job<false, G>(K, bind_rec(recs + (int64_t)en * rb, K.L, K.C));
-      pcn = paint_counts(bind_rec(recs + (int64_t)en * rb, K.L, K.C));
-      Wn = pipe_window<G>(K, Jn, tn);
+      Jn = h.J;
+      pcn = h.pc;
+      Wn = pipe_window<G>(K, Jn, tn, err);
       pipe_issue<G, JOB>(K, PJ, recs + (int64_t)en * rb, Wn, lds + (b ^ 1) * slot_bytes);
     }
     CBEV_PSTAMP(it, 3);
@@ -3582,11 +3613,11 @@ static void launch_raster(const cbev_ctx* c, const KArgs& K, void* records, int 
   const PaintJob PJ = paint_job(c->L, c->C);
   const size_t lb = pipe_lds_bytes(c, job);
   if (c->P.size == 128) {
-    if (job) hipLaunchKernelGGL((k_raster_pipe<2, true>), dim3(grid), dim3(kPipeNT), lb, s, K, PJ, (uint8_t*)records, n, frames);
-    else hipLaunchKernelGGL((k_raster_pipe<2, false>), dim3(grid), dim3(kPipeNT), lb, s, K, PJ, (uint8_t*)records, n, frames);
+    if (job) hipLaunchKernelGGL((k_raster_pipe<2, true>), dim3(grid), dim3(kPipeNT), lb, s, K, PJ, (const uint8_t*)records, n, frames, K.err);
+    else hipLaunchKernelGGL((k_raster_pipe<2, false>), dim3(grid), dim3(kPipeNT), lb, s, K, PJ, (const uint8_t*)records, n, frames, K.err);
   } else {
-    if (job) hipLaunchKernelGGL((k_raster_pipe<4, true>), dim3(grid), dim3(kPipeNT), lb, s, K, PJ, (uint8_t*)records, n, frames);
-    else hipLaunchKernelGGL((k_raster_pipe<4, false>), dim3(grid), dim3(kPipeNT), lb, s, K, PJ, (uint8_t*)records, n, frames);
+    if (job) hipLaunchKernelGGL((k_raster_pipe<4, true>), dim3(grid), dim3(kPipeNT), lb, s, K, PJ, (const uint8_t*)records, n, frames, K.err);
+    else hipLaunchKernelGGL((k_raster_pipe<4, false>), dim3(grid), dim3(kPipeNT), lb, s, K, PJ, (const uint8_t*)records, n, frames, K.err);
   }
 }
 
