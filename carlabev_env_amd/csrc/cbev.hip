@@ -654,21 +654,9 @@ __device__ unsigned g_hwid[CBEV_NSTAMP][4096];                   // HW_ID (SE / 
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(xcc_));                           \
     g_hwid[kern][w_] = xcc_;                                                                     \
   }
-// k_raster_pipe: thread 0 of workgroup w stamps item j's phases (top of the
-// iteration after the DMA wait, paint done, next item issued, output done)
-__device__ unsigned long long g_pst[1024][32][5];
-__device__ unsigned g_phw[1024];
-#define CBEV_PSTAMP(j, slot)                                                   \
-  if (threadIdx.x == 0 && blockIdx.x < 1024 && (j) < 32) {                    \
-    g_pst[blockIdx.x][j][slot] = __builtin_amdgcn_s_memtime();                \
-    unsigned hw_;                                                              \
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw_));          \
-    g_phw[blockIdx.x] = hw_;                                                   \
-  }
 #else
 #define CBEV_STAMP(kern, slot)
 #define CBEV_STAMPW(kern, slot)
-#define CBEV_PSTAMP(j, slot)
 #endif
 
 // ---- record staging for k_ego. A workgroup owns `ne` envs (a divisor of 64,
@@ -1291,23 +1279,12 @@ struct PaintPre {
   uint32_t tvis;  // its vis_draw word
 };
 
-// the rect counts of an env (HI ints)
-struct PaintCounts {
-  int nact, nveh, nt, ntl;
-};
-// (moved to scalar registers at once: a later use then waits on no load, which
-// matters where k_raster_pipe keeps an LDS-DMA in flight)
-__device__ __forceinline__ PaintCounts paint_counts(const DRec& r) {
-  return PaintCounts{__builtin_amdgcn_readfirstlane(r.hi[CBEV_HI_NACT]), __builtin_amdgcn_readfirstlane(r.hi[CBEV_HI_NVEH]),
-                     __builtin_amdgcn_readfirstlane(r.hi[CBEV_HI_NROUTE]),
-                     __builtin_amdgcn_readfirstlane(r.hi[CBEV_HI_NTL])};
-}
-__device__ __forceinline__ PaintPre raster_paint_fetch(const DRec& r, const PaintCounts& c) {
+__device__ __forceinline__ PaintPre raster_paint_fetch(const DRec& r) {
   PaintPre q;
-  q.nact = c.nact;
-  q.nveh = c.nveh;
-  q.nt = c.nt;
-  q.ntl = c.ntl;
+  q.nact = r.hi[CBEV_HI_NACT];
+  q.nveh = r.hi[CBEV_HI_NVEH];
+  q.nt = r.hi[CBEV_HI_NROUTE];
+  q.ntl = r.hi[CBEV_HI_NTL];
   const int k = threadIdx.x >> 2;
   q.ax = q.ay = q.tx = q.ty = 0.0;
   q.asz = 0;
@@ -1358,30 +1335,6 @@ __device__ __forceinline__ RasterJob raster_job(const KArgs& K, const DRec& r) {
   }
   raster8_affine(J.R, rt);
   return J;
-}
-
-// k_raster_pipe's view of an env's render set-up and rect counts: the HI ints
-// read through a constant-address-space pointer (the records are not written
-// during the raster), so they are scalar loads; their waits are lgkmcnt ones and
-// never drain the LDS-DMA the pipe keeps in flight on vmcnt
-typedef __attribute__((address_space(4))) const int32_t cint4;
-struct PipeHead {
-  RasterJob J;
-  PaintCounts pc;
-};
-template <int G>
-__device__ __forceinline__ PipeHead pipe_head(const KArgs& K, const uint8_t* rec) {
-  cint4* hi = (cint4*)(rec + K.L.hi);
-  PipeHead h;
-  h.J.xmin = hi[CBEV_HI_RS_XMIN];
-  h.J.ymin = hi[CBEV_HI_RS_YMIN];
-  int32_t* w = (int32_t*)&h.J.R;
-#pragma unroll
-  for (int k = 0; k < CBEV_RS_WORDS; ++k) w[k] = hi[CBEV_HI_RS_R90 + k];
-  h.J.fast = hi[CBEV_HI_RS_FAST] != 0;
-  raster8_affine(h.J.R, raster_row_texels(64 * G, K.P.crop));
-  h.pc = PaintCounts{hi[CBEV_HI_NACT], hi[CBEV_HI_NVEH], hi[CBEV_HI_NROUTE], hi[CBEV_HI_NTL]};
-  return h;
 }
 
 // A tile's window in (u, v) = (x, y), or (y, x) when transposed: crop rows
@@ -1639,7 +1592,7 @@ __device__ __forceinline__ void overlay16(const cbev_params& P, const uint32_t* 
 template <int G, int NT>
 __device__ __forceinline__ void tile_out(const cbev_params& P, const RotSetup& R, const TileWin& W, int ox0, int oy0,
                                          const uint8_t* __restrict__ lds, uint8_t* __restrict__ out, int nout,
-                                         int64_t out_stride, const uint32_t* __restrict__ fov, int lds_base = 0) {
+                                         int64_t out_stride, const uint32_t* __restrict__ fov) {
   using TG = Tiles<G>;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1647,9 +1600,8 @@ __device__ __forceinline__ void tile_out(const cbev_params& P, const RotSetup& R
   const int Y0 = oy0 + wave * TG::RPC + lrow;
   const int xx = X - R.rx0, yy = Y0 - R.ry0;
   const int sx = R.dx00 + xx * R.icos - yy * R.isin, sy = R.dy00 + xx * R.isin + yy * R.icos;
-  // window coordinates: (u, v) moved by (ou, -v0); the window's LDS byte offset
-  // lds_base (the gathers address the LDS absolutely) rides in u's integer part
-  const int u = (W.tr ? sy : sx) + ((W.ou + lds_base) << 16), v = (W.tr ? sx : sy) - (W.v0 << 16);
+  // window coordinates: (u, v) moved by (ou, -v0)
+  const int u = (W.tr ? sy : sx) + (W.ou << 16), v = (W.tr ? sx : sy) - (W.v0 << 16);
   const int du_c = W.tr ? R.isin : R.icos, dv_c = W.tr ? R.icos : R.isin;    // one output column right
   const int du_r = W.tr ? R.icos : -R.isin, dv_r = W.tr ? -R.isin : R.icos;  // one output row down
   constexpr int NW = NT / 64;  // waves: the chunks are dealt over them
@@ -1659,13 +1611,7 @@ __device__ __forceinline__ void tile_out(const cbev_params& P, const RotSetup& R
   const uint64_t col_step = (uint64_t)(((int64_t)dv_c << 32) + (int64_t)du_c);
   const uint64_t chunk_step = (uint64_t)(((int64_t)(chunk_rows * dv_r) << 32) + (int64_t)(chunk_rows * du_r));
   const int hy0 = P.anchor_y - P.hero_w / 2;
-  // a constant trip count (unrolled): the stores after a k_raster_pipe DMA are
-  // countable, so the compiler's waits honour its counted vmcnt
-  constexpr int NPW = (TG::NCH + NW - 1) / NW;  // chunks per wave
-#pragma unroll
-  for (int j = 0; j < NPW; ++j) {
-    const int ch = wave + j * NW;
-    if (TG::NCH % NW != 0 && ch >= TG::NCH) break;
+  for (int ch = wave; ch < TG::NCH; ch += NW) {
     const int Yc = oy0 + ch * TG::RPC;  // the chunk's first row (uniform)
     const int Y = Yc + lrow;
     const uint32_t vo = (uint32_t)(Y * TG::S + X);
@@ -1720,11 +1666,7 @@ __device__ __forceinline__ void tile_out_check(const cbev_params& P, const RotSe
   }
   const int du_c = W.tr ? R.isin : R.icos, dv_c = W.tr ? R.icos : R.isin;
   const int hy0 = P.anchor_y - P.hero_w / 2;
-  constexpr int NW = NT / 64, NPW = (TG::NCH + NW - 1) / NW;
-#pragma unroll
-  for (int j = 0; j < NPW; ++j) {
-    const int ch = wave + j * NW;
-    if (TG::NCH % NW != 0 && ch >= TG::NCH) break;
+  for (int ch = wave; ch < TG::NCH; ch += NT / 64) {
     const int Yc = oy0 + ch * TG::RPC;
     const int Y = Yc + lrow;
     const uint32_t vo = (uint32_t)(Y * TG::S + X);
@@ -1766,7 +1708,7 @@ __device__ __forceinline__ void raster_tile(const KArgs& K, const DRec& r, const
     W.nv = TG::lds_bytes / W.sb;
   }
   PaintPre pq{};
-  if (PAINT) pq = raster_paint_fetch(r, paint_counts(r));  // in flight under the staging
+  if (PAINT) pq = raster_paint_fetch(r);  // in flight under the staging
   stage_tile<NT>(K, W, lds);
   __syncthreads();
   if (PAINT) {
@@ -1819,183 +1761,6 @@ void k_raster(KArgs K, uint8_t* __restrict__ recs, int n, uint8_t* __restrict__ 
   const RasterJob J = raster_job<false, G>(K, r);
   raster_tile<G, true, kRasterNT>(K, r, J, t, frames + e * SS, 1, 0, lds);
   CBEV_STAMP(2, 3);
-}
-
-// ====================================================== k_raster_pipe: the pipelined step raster
-// The step's raster at S = 128 and 256 (128 x 128 tiles). Round 4's k_raster
-// runs one (env, tile) per 256-thread workgroup as a serial chain: record ->
-// window -> map loads -> LDS stores -> barrier -> paint -> output, and the four
-// workgroups of a CU start together, so they stage together (LDS idle, waiting
-// on L2) and then gather together (LDS bank-bound): the per-CU resources are
-// used in turns. Here a persistent 512-thread workgroup (two per
-// CU, 16 waves) walks its items w, w + grid, ... (xcd_tile_of_wg order: every
-// item on the XCD whose L2 holds its record) with two LDS slots: while its 8
-// waves paint and write item i out of one slot, item i + 1's window rows and
-// paint inputs land in the other by LDS-DMA (global_load_lds_dword: no
-// registers, no LDS store instructions, one instruction per window row). The
-// DMA stays in flight across the paint's barriers (raw s_barrier, counted
-// vmcnt: only item i's own output stores are left outstanding when the next
-// item's DMA is waited for).
-// Paint inputs ("job", JOB): the record ranges paint_tile reads (route cx | cy,
-// vis_draw, actor X | Y rows, actor sizes, traffic lights) are mirrored into the
-// slot behind the window, so the paint reads LDS; without JOB (the ranges do not
-// fit beside two windows) it reads the record, and the compiler's wait for those
-// loads drains the next item's DMA early (correct, slower).
-constexpr int kPipeNT = 512;
-struct PaintJob {
-  int src[5], dst[5], dw[5];  // record byte offset, job byte offset, dwords of each mirrored range
-  int bytes;                  // job bytes (a multiple of 16)
-};
-static PaintJob paint_job(const cbev_layout& L, const cbev_caps& C) {
-  PaintJob J{};
-  const int rc = C.route_cap, A = C.actor_cap, T = C.tl_cap;
-  const int src[5] = {(int)L.cx, (int)(L.vis + 4 * L.vis_words), (int)L.ad, (int)(L.ai + 4 * CBEV_AI_SIZE * A),
-                      (int)L.ti};
-  const int bytes[5] = {(int)(L.cy - L.cx) + 8 * rc, 4 * L.vis_words, 16 * A, 4 * A, 4 * CBEV_TI_COUNT * T};
-  int o = 0;
-  for (int k = 0; k < 5; ++k) {
-    J.src[k] = src[k];
-    J.dst[k] = o;
-    J.dw[k] = bytes[k] / 4;
-    o += (bytes[k] + 15) & ~15;
-  }
-  J.bytes = o;
-  return J;
-}
-// DRec of the mirrored job: the paint's fields in LDS at the record's relative
-// offsets, the rest (hi: counts and render set-up, read by scalar loads) in HBM
-__device__ __forceinline__ DRec bind_job(const DRec& r, uint8_t* job, const PaintJob& PJ, const cbev_layout& L) {
-  DRec j = r;
-  j.cx = (double*)job;
-  j.cy = (double*)(job + (L.cy - L.cx));
-  j.vis_draw = (uint32_t*)(job + PJ.dst[1]);
-  j.ad = (double*)(job + PJ.dst[2]);                             // rows X, Y
-  j.ai = (int32_t*)(job + PJ.dst[3]) - CBEV_AI_SIZE * r.A;       // ai[SIZE * A + a]
-  j.ti = (int32_t*)(job + PJ.dst[4]);
-  return j;
-}
-typedef __attribute__((address_space(3))) void lds_void;
-// item (e, tile) into one slot: the window rows (row v by wave v % 8, lanes
-// [0, 4 nc) one dword each: the 16-byte chunks stage_tile copies) and the job
-template <int G, bool JOB>
-__device__ __forceinline__ void pipe_issue(const KArgs& K, const PaintJob& PJ, const uint8_t* rec, const TileWin& W,
-                                           uint8_t* slot) {
-  constexpr int NW = kPipeNT / 64;
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  if (JOB) {
-    uint8_t* job = slot + Tiles<G>::lds_bytes;
-    const int jd = PJ.bytes / 4;
-    for (int j = wave; 64 * j < jd; j += NW) {
-      const int d = 64 * j + lane;
-      int src = -1;
-#pragma unroll
-      for (int k = 0; k < 5; ++k) {
-        const int q = d - PJ.dst[k] / 4;
-        if (q >= 0 && q < PJ.dw[k]) src = PJ.src[k] + 4 * q;
-      }
-      if (src >= 0) __builtin_amdgcn_global_load_lds((const void*)(rec + src), (lds_void*)(job + 256 * j), 4, 0, 0);
-    }
-  }
-  const uint8_t* map = W.tr ? K.map8T : K.map8;
-  const int pitch = W.tr ? K.p8T : K.p8;
-  const uint8_t* g = map + (int64_t)(W.vmin + W.v0) * pitch + (W.umin & ~3) + 16 * W.c0 + 4 * lane;
-  const bool on = lane < 4 * W.nc;
-  for (int v = wave; v < W.nv; v += NW)
-    if (on) __builtin_amdgcn_global_load_lds((const void*)(g + (int64_t)v * pitch), (lds_void*)(slot + v * W.sb), 4, 0, 0);
-}
-
-template <int G>
-__device__ __forceinline__ TileWin pipe_window(const KArgs& K, const RasterJob& J, int t, int32_t* __restrict__ err) {
-  using TG = Tiles<G>;
-  TileWin W = tile_window<G>(K.P, J, (t % TG::NTX) * TG::TC, (t / TG::NTX) * TG::TR);
-  if (W.nv * W.sb > TG::lds_bytes) {  // cannot happen (Tiles::lds_bytes bounds every heading): flag, stay in bounds
-    if (threadIdx.x == 0) atomicOr(err, CBEV_ERR_RASTER_WINDOW);
-    W.nv = TG::lds_bytes / W.sb;
-  }
-  return W;
-}
-
-// s_waitcnt with only vmcnt(N) (gfx9 encoding: expcnt 7, lgkmcnt 15 = no wait),
-// a builtin the compiler's own wait insertion accounts for
-#define CBEV_WAIT_VM(N) __builtin_amdgcn_s_waitcnt(0x0F70 | (N))
-
-template <int G, bool JOB>
-__global__ __launch_bounds__(kPipeNT) void k_raster_pipe(KArgs K, PaintJob PJ, const uint8_t* __restrict__ recs_c,
-                                                          int n, uint8_t* __restrict__ frames,
-                                                          int32_t* __restrict__ err) {
-  // the records are only read here (const, restrict; the only stores go to frames
-  // and err, restrict too): their uniform loads (render set-up, counts) can be
-  // scalar loads, which wait on lgkmcnt, not on the DMA's vmcnt
-  uint8_t* recs = (uint8_t*)recs_c;
-  extern __shared__ __align__(16) uint8_t lds[];
-  using TG = Tiles<G>;
-  static_assert(TG::NCH == 2 * (kPipeNT / 64), "two output chunks (two stores) per wave and item");
-  const int slot_bytes = TG::lds_bytes + (JOB ? PJ.bytes : 0);
-  const int items = n * TG::T;
-  const int64_t SS = (int64_t)K.P.size * K.P.size;
-  const int64_t rb = K.L.record_bytes;
-  int k = blockIdx.x;
-  if (k >= items) return;
-  CBEV_PSTAMP(31, 4);
-  int e, t;
-  xcd_tile_of_wg(k, n, TG::T, &e, &t);
-  PipeHead h = pipe_head<G>(K, recs + (int64_t)e * rb);
-  RasterJob J = h.J;
-  PaintCounts pc = h.pc;
-  TileWin W = pipe_window<G>(K, J, t, err);
-  pipe_issue<G, JOB>(K, PJ, recs + (int64_t)e * rb, W, lds);
-  for (int b = 0, first = 1, it = 0;; b ^= 1, first = 0, ++it) {
-    // this item's DMA: every wave retires its own (only this wave's two output
-    // stores of the previous item are younger), then the workgroup's
-    CBEV_PSTAMP(it, 0);
-    if (first) CBEV_WAIT_VM(0);
-    else CBEV_WAIT_VM(2);
-    lds_barrier();
-    CBEV_PSTAMP(it, 1);
-    // the next item's render set-up and counts (scalar loads, in flight under the paint)
-    const int kn = k + (int)gridDim.x;
-    int en = 0, tn = 0;
-    if (kn < items) {
-      xcd_tile_of_wg(kn, n, TG::T, &en, &tn);
-      h = pipe_head<G>(K, recs + (int64_t)en * rb);
-    }
-    uint8_t* slot = lds + b * slot_bytes;
-    {
-      const DRec r = bind_rec(recs + (int64_t)e * rb, K.L, K.C);
-      const DRec rp = JOB ? bind_job(r, slot + TG::lds_bytes, PJ, K.L) : r;
-      const PaintPre pq = raster_paint_fetch(rp, pc);
-      paint_tile<kPipeNT>(K, rp, pq, J, W, slot);  // ends with a barrier: the other slot's output is over too
-    }
-    CBEV_PSTAMP(it, 2);
-    // the next item into the other slot, in flight under this item's output
-    RasterJob Jn = J;
-    TileWin Wn = W;
-    PaintCounts pcn = pc;
-    if (kn < items) {
-      Jn = h.J;
-      pcn = h.pc;
-      Wn = pipe_window<G>(K, Jn, tn, err);
-      pipe_issue<G, JOB>(K, PJ, recs + (int64_t)en * rb, Wn, lds + (b ^ 1) * slot_bytes);
-    }
-    CBEV_PSTAMP(it, 3);
-    const int ox0 = (t % TG::NTX) * TG::TC, oy0 = (t / TG::NTX) * TG::TR;
-    if (J.fast) {
-      tile_out<G, kPipeNT>(K.P, J.R, W, ox0, oy0, slot, frames + e * SS, 1, 0, K.fov, b * slot_bytes);
-    } else {
-      const DRec r = bind_rec(recs + (int64_t)e * rb, K.L, K.C);
-      tile_out_check<G, kPipeNT>(K.P, J.R, W, ox0, oy0, slot, crop_background(K, r, J, true), frames + e * SS, 1, 0,
-                                 K.fov);
-    }
-    CBEV_PSTAMP(it, 4);
-    if (kn >= items) break;
-    k = kn;
-    e = en;
-    t = tn;
-    J = Jn;
-    W = Wn;
-    pc = pcn;
-  }
 }
 
 // BaseMap.reset's observation (theta = 0, nothing painted, world.py:92-100) of
@@ -3440,9 +3205,6 @@ struct cbev_ctx {
   // bank cursor of cbev_reset_masked (rows taken so far): one copy per
   // k_reset_mask workgroup, all equal between calls
   unsigned long long* cur_dev;  // [RESET_MASK_WGS * CBEV_CURSOR_STRIDE]
-  int n_cu;                   // compute units (k_raster_pipe's persistent grid: two workgroups each)
-  bool pipe_job;              // k_raster_pipe mirrors the paint job into LDS (pipe_job_fits)
-  bool raster_tile;           // TEMP A/B (CBEV_RASTER_TILE=1): round 4's raster
   const uint8_t* last_term;   // term buffer of the last cbev_step (cbev_reset_terminated's mask)
   int last_n;                 // n of the last cbev_step (0: none yet)
 };
@@ -3575,49 +3337,13 @@ static size_t raster_lds_bytes(const cbev_params& P) {
   return P.size == 64 ? Tiles<1>::lds_bytes : P.size == 128 ? Tiles<2>::lds_bytes : Tiles<4>::lds_bytes;
 }
 static int raster_tiles(int size) { return size == 64 ? Tiles<1>::T : size == 128 ? Tiles<2>::T : Tiles<4>::T; }
-// k_raster_pipe: two slots (window + mirrored paint job) per workgroup, two
-// workgroups per CU; the job is mirrored only while that still fits
-static bool pipe_job_fits(const cbev_ctx* c) {
-  const int win = c->P.size == 128 ? Tiles<2>::lds_bytes : Tiles<4>::lds_bytes;
-  return 2 * (win + paint_job(c->L, c->C).bytes) <= 163840 / 2;
-}
-static const void* pipe_kernel(int size, bool job) {
-  if (size == 128) return job ? (const void*)k_raster_pipe<2, true> : (const void*)k_raster_pipe<2, false>;
-  return job ? (const void*)k_raster_pipe<4, true> : (const void*)k_raster_pipe<4, false>;
-}
-static size_t pipe_lds_bytes(const cbev_ctx* c, bool job) {
-  const int win = c->P.size == 128 ? Tiles<2>::lds_bytes : Tiles<4>::lds_bytes;
-  return 2 * (size_t)(win + (job ? paint_job(c->L, c->C).bytes : 0));
-}
-// One step's observation for n records: k_raster_pipe at S = 128 / 256 (a
-// persistent grid of two workgroups per CU, a multiple of 8: every item stays on
-// its record's XCD), k_raster (one workgroup per env) at S = 64.
+// One step's observation for n records: one workgroup per env.
 static void launch_raster(const cbev_ctx* c, const KArgs& K, void* records, int n, uint8_t* frames, hipStream_t s) {
-  if (c->P.size == 64) {
-    hipLaunchKernelGGL(k_raster<1>, dim3(n * Tiles<1>::T), dim3(kRasterNT), raster_lds_bytes(c->P), s, K,
-                       (uint8_t*)records, n, frames);
-    return;
-  }
-  if (c->raster_tile) {  // TEMP A/B: round 4's one-item-per-workgroup raster
-    const size_t lb = raster_lds_bytes(c->P);
-    if (c->P.size == 128)
-      hipLaunchKernelGGL(k_raster<2>, dim3(n * Tiles<2>::T), dim3(kRasterNT), lb, s, K, (uint8_t*)records, n, frames);
-    else
-      hipLaunchKernelGGL(k_raster<4>, dim3(n * Tiles<4>::T), dim3(kRasterNT), lb, s, K, (uint8_t*)records, n, frames);
-    return;
-  }
-  const int items = n * raster_tiles(c->P.size);
-  const int cap = 2 * c->n_cu;
-  const int grid = items <= cap ? items : cap & ~7;
-  const bool job = c->pipe_job;
-  const PaintJob PJ = paint_job(c->L, c->C);
-  const size_t lb = pipe_lds_bytes(c, job);
-  if (c->P.size == 128) {
-    if (job) hipLaunchKernelGGL((k_raster_pipe<2, true>), dim3(grid), dim3(kPipeNT), lb, s, K, PJ, (const uint8_t*)records, n, frames, K.err);
-    else hipLaunchKernelGGL((k_raster_pipe<2, false>), dim3(grid), dim3(kPipeNT), lb, s, K, PJ, (const uint8_t*)records, n, frames, K.err);
-  } else {
-    if (job) hipLaunchKernelGGL((k_raster_pipe<4, true>), dim3(grid), dim3(kPipeNT), lb, s, K, PJ, (const uint8_t*)records, n, frames, K.err);
-    else hipLaunchKernelGGL((k_raster_pipe<4, false>), dim3(grid), dim3(kPipeNT), lb, s, K, PJ, (const uint8_t*)records, n, frames, K.err);
+  const size_t lb = raster_lds_bytes(c->P);
+  switch (c->P.size) {
+    case 64: hipLaunchKernelGGL(k_raster<1>, dim3(n * Tiles<1>::T), dim3(kRasterNT), lb, s, K, (uint8_t*)records, n, frames); break;
+    case 128: hipLaunchKernelGGL(k_raster<2>, dim3(n * Tiles<2>::T), dim3(kRasterNT), lb, s, K, (uint8_t*)records, n, frames); break;
+    default: hipLaunchKernelGGL(k_raster<4>, dim3(n * Tiles<4>::T), dim3(kRasterNT), lb, s, K, (uint8_t*)records, n, frames); break;
   }
 }
 
@@ -3717,19 +3443,9 @@ int cbev_create(const cbev_params* params, const cbev_caps* caps, int device, cb
   if (e == hipSuccess)
     e = hipFuncSetAttribute(bank_frames_kernel(P.size), hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)raster_lds_bytes(P));
-  if (e == hipSuccess) e = hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, device);
-  if (c->n_cu < 8) c->n_cu = 8;
-  c->raster_tile = getenv("CBEV_RASTER_TILE") && atoi(getenv("CBEV_RASTER_TILE")) == 1;
-  if (P.size != 64) {
-    c->pipe_job = pipe_job_fits(c);
-    if (e == hipSuccess)
-      e = hipFuncSetAttribute(pipe_kernel(P.size, c->pipe_job), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)pipe_lds_bytes(c, c->pipe_job));
-  }
   // the byte-image gathers address the LDS absolutely: the crop image must be the
   // first thing in the workgroup's LDS (no static segment before it)
-  for (const void* kf : {raster_kernel(P.size), reset_kernel(P.size), bank_frames_kernel(P.size),
-                         P.size == 64 ? raster_kernel(64) : pipe_kernel(P.size, c->pipe_job)}) {
+  for (const void* kf : {raster_kernel(P.size), reset_kernel(P.size), bank_frames_kernel(P.size)}) {
     hipFuncAttributes fa;
     if (e == hipSuccess) e = hipFuncGetAttributes(&fa, kf);
     if (e == hipSuccess && fa.sharedSizeBytes != 0) {
@@ -4258,12 +3974,6 @@ int cbev_resize_obs(cbev_ctx* c, const uint8_t* frames, int n, const uint8_t* ma
 }
 
 #ifdef CBEV_TIMING
-// timing builds only: k_raster_pipe's stamps [1024][32][5] and HW_IDs [1024]
-int cbev_debug_pipe_times(unsigned long long* st, unsigned* hw) {
-  if (hipMemcpyFromSymbol(st, HIP_SYMBOL(g_pst), sizeof(g_pst)) != hipSuccess) return -1;
-  if (hipMemcpyFromSymbol(hw, HIP_SYMBOL(g_phw), sizeof(g_phw)) != hipSuccess) return -1;
-  return 0;
-}
 // timing builds only: copy the phase stamps [6][4096][4] (u64 s_memtime ticks), realtime stamps,
 // XCC ids | HW_ID << 32
 int cbev_debug_times(unsigned long long* out_host) {
