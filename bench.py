@@ -343,6 +343,7 @@ def fresh_pass(env, pool, one_step, args, world, n, device, seconds=2.0):
                 pool.request(len(gids))
             if steps % 64 == 0:  # keep the host no more than ~64 steps ahead of the device
                 torch.cuda.current_stream().synchronize()
+    env.flush()
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     resets = env.termination_count() - term0
@@ -437,6 +438,9 @@ def main():
         t0 = time.perf_counter()
         for t in range(args.warmup, total_steps):
             one_step(t, wire)
+        # the last step's reset is folded into no next step here: it runs now, in the
+        # timed region (k_reset_mask), like every other step's reset
+        env.flush()
         host_enqueue = time.perf_counter() - t0
         if gatherer is not None:
             gatherer.wait()  # the last steps' gathers are part of the timed region
@@ -477,6 +481,7 @@ def main():
         for t in range(burn):
             env.step_async_only(acts_all[t])
             env.reset_terminated()
+        env.flush()
         torch.cuda.synchronize()
         snap["records"] = env.records.clone()
         snap["ring"] = env.ring.clone()

@@ -58,6 +58,12 @@ def lib():
     L.cbev_reset_terminated.restype = _I
     L.cbev_bank_cursor.argtypes = [_P, _P]
     L.cbev_bank_cursor.restype = _I
+    L.cbev_set_deferred_reset.argtypes = [_P, _I]
+    L.cbev_set_deferred_reset.restype = _I
+    L.cbev_reset_pending.argtypes = [_P]
+    L.cbev_reset_pending.restype = _I
+    L.cbev_flush.argtypes = [_P]
+    L.cbev_flush.restype = _I
     L.cbev_expand_obs.argtypes = [_P, _P, _I, _I, _I, _I, _I, _P, _P, _P]
     L.cbev_expand_obs.restype = _I
     L.cbev_pack_frames.argtypes = [_P, _P, _I, _P, _P]
@@ -101,6 +107,7 @@ def check(rc: int, what: str = "cbev call"):
 EXPORTED_SYMBOLS = ("cbev_abi_version", "cbev_params_size", "cbev_layout_of", "cbev_field_names", "cbev_last_error",
                     "cbev_create", "cbev_destroy", "cbev_set_map", "cbev_step", "cbev_reset", "cbev_bank_frames",
                     "cbev_reset_frames", "cbev_reset_masked", "cbev_reset_terminated", "cbev_bank_cursor",
+                    "cbev_set_deferred_reset", "cbev_reset_pending", "cbev_flush",
                     "cbev_expand_obs", "cbev_vector_obs", "cbev_set_fov_mask", "cbev_set_obs_size", "cbev_resize_obs", "cbev_profile", "cbev_profile_read",
                     "cbev_profile_raster", "cbev_error_flags", "cbev_set_episode_stats", "cbev_episode_slot",
                     "cbev_wall_clock_hz", "cbev_termination_count", "cbev_pack_frames", "cbev_unpack_frames")

@@ -721,8 +721,10 @@ __device__ __forceinline__ int ego_src(int n0, int raw_x, int c) { return c < n0
 // 16 (k n + c), lane-linear per wave. rb, n0, n, raw_x: passed as leading kernel
 // arguments, which the launch preloads into SGPRs (kernarg preloading,
 // -amdgpu-kernarg-preload-count), so the first load is issued at wave start.
-__device__ __forceinline__ void ego_stage_in(uint8_t* lds, const uint8_t* __restrict__ recs, int e0, int ne, int rb,
-                                             int n0, int n, int raw_x) {
+// src(k): the record env k is staged from (its own, or its bank row when the
+// folded reset takes it, KArgs::rmask)
+template <class Src>
+__device__ __forceinline__ void ego_stage_in(uint8_t* lds, Src src, int ne, int n0, int n, int raw_x) {
   const int total = ne * n;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -731,7 +733,7 @@ __device__ __forceinline__ void ego_stage_in(uint8_t* lds, const uint8_t* __rest
     const int q = b + lane;
     if (q < total) {
       const int k = q / n, c = q - k * n;
-      __builtin_amdgcn_global_load_lds((const void*)(recs + (int64_t)(e0 + k) * rb + ego_src(n0, raw_x, c)),
+      __builtin_amdgcn_global_load_lds((const void*)(src(k) + ego_src(n0, raw_x, c)),
                                        (__attribute__((address_space(3))) void*)(lds + 16 * b), 16, 0, 0);
     }
   }
@@ -1759,7 +1761,38 @@ void k_raster(KArgs K, uint8_t* __restrict__ recs, int n, uint8_t* __restrict__ 
   const int64_t SS = (int64_t)K.P.size * K.P.size;
   const DRec r = bind_rec(recs + (int64_t)e * K.L.record_bytes, K.L, K.C);
   const RasterJob J = raster_job<false, G>(K, r);
+  // the reset folded into this step (KArgs::rmask): a reset env's bank frame,
+  // this tile of it, into every ring slot but the one this step renders
+  // (FrameStackObservation's reset padding), loaded before the render and
+  // stored after it
+  using TG = Tiles<G>;
+  constexpr int CPR = TG::TC / 16, PPT = TG::TC * TG::TR / 16 / kRasterNT;
+  const int row = K.rrow != nullptr ? K.rrow[e] : -1;
+  const bool rf = row >= 0 && K.rn_frames > 1;
+  const int ox0 = (t % TG::NTX) * TG::TC, oy0 = (t / TG::NTX) * TG::TR;
+  uint4 fv[PPT];
+  if (rf) {
+#pragma unroll
+    for (int j = 0; j < PPT; ++j) {
+      const int p = threadIdx.x + kRasterNT * j, pr = p / CPR;
+      fv[j] = *(const uint4*)(K.rbank_frames + (int64_t)row * SS + (oy0 + pr) * K.P.size + ox0 + 16 * (p - pr * CPR));
+    }
+  }
   raster_tile<G, true, kRasterNT>(K, r, J, t, frames + e * SS, 1, 0, lds);
+  if (rf) {
+    for (int f = 0; f < K.rn_frames; ++f) {
+      if (f == K.rslot) continue;
+      uint8_t* dst = K.rring + (int64_t)f * K.rring_stride + e * SS;
+#pragma unroll
+      for (int j = 0; j < PPT; ++j) {
+        const int p = threadIdx.x + kRasterNT * j, pr = p / CPR;
+        const uint4 v = fv[j];
+        store16_frame(dst + (oy0 + pr) * K.P.size + ox0 + 16 * (p - pr * CPR), u32x4_nt{v.x, v.y, v.z, v.w});
+      }
+    }
+  }
+  // the step's termination flags, published once k_ego's reset no longer reads the previous ones
+  if (K.term_pub != nullptr && t == 0 && threadIdx.x == 0) K.term_pub[e] = K.term_scr[e];
   CBEV_STAMP(2, 3);
 }
 
@@ -2499,6 +2532,77 @@ __device__ __forceinline__ void butterfly(int tpe, F&& f) {
   if (tpe > 32) f(std::integral_constant<int, 32>{});
 }
 
+// ---- the canonical reset folded into k_ego (KArgs::rmask; cbev_set_deferred_reset)
+// reset(reset_mask=terminated) between two steps (carlabev.py:96-148,
+// tools/debug_env.py:56-132) without a launch of its own: the next k_ego ranks
+// the mask (the previous step's term buffer, read when this step runs, so
+// in-place edits of it count) exactly as k_reset_mask does, the k-th selected
+// env in id order takes bank row (cursor + k) % n_bank, and each workgroup
+// stages its reset envs from their bank rows instead of their records. Every
+// workgroup loads the whole mask (n bytes) and counts the selected envs before
+// its first env and in total; the cursor copies are k_reset_mask's (slot w of
+// workgroup w, all advanced by the total).
+struct EgoReset {
+  uint64_t bits;            // the workgroup's envs to reset (bit k: env e0 + k)
+  int base, total;          // bank row of the workgroup's first selected env; selected envs in the whole mask
+};
+// bank row of env k of the workgroup (bit k of R.bits set)
+__device__ __forceinline__ int ego_reset_row(const EgoReset& R, int k, int n_bank) {
+  return (int)((unsigned)(R.base + __popcll(R.bits & ((1ull << k) - 1ull))) % (unsigned)n_bank);
+}
+__device__ __forceinline__ EgoReset ego_reset_scan(const KArgs& K, int n, int e0, int ne_eff, int* red) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const unsigned long long cur = K.rcursor[CBEV_CURSOR_STRIDE * blockIdx.x];
+  const int nu = (n + 15) >> 4, u0 = e0 >> 4;
+  const bool vec = ((uintptr_t)K.rmask & 15u) == 0;
+  int cb = 0, ct = 0;
+  for (int u = tid; u < nu; u += 256) {
+    uint32_t m = 0;
+    if (vec && 16 * u + 16 <= n) {
+      m = nonzero_bytes16(*(const uint4*)(K.rmask + 16 * (int64_t)u));
+    } else {
+      for (int b = 0; b < 16; ++b)
+        if (16 * u + b < n && K.rmask[16 * (int64_t)u + b] != 0) m |= 1u << b;
+    }
+    const int c = __popc(m);
+    ct += c;
+    cb += u < u0 ? c : (u == u0 ? __popc(m & ((1u << (e0 & 15)) - 1u)) : 0);
+  }
+  const bool mine = tid < ne_eff && K.rmask[e0 + tid] != 0;  // wave 0: the workgroup's own envs (ne <= 64)
+  const uint64_t bits = __ballot(mine);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    cb += __shfl_xor(cb, o, 64);
+    ct += __shfl_xor(ct, o, 64);
+  }
+  if (lane == 0) {
+    red[2 * wave] = cb;
+    red[2 * wave + 1] = ct;
+  }
+  if (tid == 0) {
+    red[8] = (int)(uint32_t)bits;
+    red[9] = (int)(uint32_t)(bits >> 32);
+  }
+  __syncthreads();
+  EgoReset R;
+  const int before = red[0] + red[2] + red[4] + red[6];
+  R.total = red[1] + red[3] + red[5] + red[7];
+  R.bits = (uint64_t)(uint32_t)red[8] | ((uint64_t)(uint32_t)red[9] << 32);
+  R.base = (int)((cur + (unsigned long long)before) % (unsigned long long)K.rn_bank);
+  // env k's bank row (or -1) for k_raster (the reset frame into the other ring slots)
+  if (tid < ne_eff) {
+    const int row = ((R.bits >> tid) & 1u) ? ego_reset_row(R, tid, K.rn_bank) : -1;
+    K.rrow[e0 + tid] = row;
+    if (row >= 0 && K.stats != nullptr) K.stats[e0 + tid].t0 = (double)wall_clock64();  // episode start
+  }
+  // this workgroup's cursor copies, advanced for the next reset
+  if (R.total > 0)
+    for (int w = blockIdx.x + gridDim.x * tid; w < K.rncur; w += gridDim.x * 256)
+      K.rcursor[CBEV_CURSOR_STRIDE * w] = cur + (unsigned long long)R.total;
+  __syncthreads();
+  return R;
+}
+
 // ============================================================== k_ego
 // The ego half of CarlaBEV.step() (scene.py:90-140, carlabev.py:159-185) for
 // `ne` envs per 256-thread workgroup, in one launch after k_actors and before
@@ -2530,22 +2634,47 @@ __global__ __launch_bounds__(256) void k_ego(uint8_t* __restrict__ recs, int n, 
   CBEV_STAMP(0, 0);
   const int e0 = staged_env0(blockIdx.x, ne, n);
   const int ne_eff = min(ne, n - e0);
+  const EgoPack pk = ego_pack(K.L);
+  uint8_t* scr = lds + ne * pk.bytes;  // [ne] collision scratch (from S4; the folded reset's scan before)
+  // the folded reset: which envs take a bank row
+  EgoReset R{0ull, 0, 0};
+  if (K.rmask != nullptr) R = ego_reset_scan(K, n, e0, ne_eff, (int*)scr);
+  auto src = [&](int k) -> uint8_t* {
+    if (R.bits != 0ull && ((R.bits >> k) & 1ull))
+      return (uint8_t*)K.rbank + (int64_t)ego_reset_row(R, k, K.rn_bank) * st_rb;
+    return recs + (int64_t)(e0 + k) * st_rb;
+  };
   // S0: the staging first (it depends on nothing loaded, and its scalars are
   // preloaded), then the action loads and the actor prefetch, whose latency
   // overlaps the staging's
-  ego_stage_in(lds, recs, e0, ne_eff > 0 ? ne_eff : 0, st_rb, st_n0, st_n, st_raw_x);
+  ego_stage_in(lds, src, ne_eff > 0 ? ne_eff : 0, st_n0, st_n, st_raw_x);
   CBEV_STAMP(3, 0);
   const cbev_params& P = K.P;
-  const EgoPack pk = ego_pack(K.L);
   const int64_t rb = K.L.record_bytes;
   if (ne_eff <= 0) return;
   const CollScratchLayout SL = coll_scratch_layout(K.C, K.L.vis_words);
-  uint8_t* scr = lds + ne * pk.bytes;          // [ne] collision scratch
+  // the folded reset's record ranges k_ego does not write back ([cx, vis) and
+  // past the vis group), bank row -> record: one 16-byte piece per thread
+  // loaded now and stored at S7 (more pieces than threads: copied at S7)
+  const int rsA = (int)((K.L.vis - K.L.cx) / 16), rsB0 = (int)(K.L.vis / 16) + pk.nvis;
+  const int rpp = rsA + (int)(rb / 16) - rsB0;  // pieces per reset env
+  const int nres = __popcll(R.bits);
+  uint4 rest_v = make_uint4(0, 0, 0, 0);
+  int rest_k = -1, rest_o = 0;
+  auto rest_piece = [&](int q, int* k, int* o) {
+    *k = nth_set_bit(R.bits, q / rpp);
+    const int c = q % rpp;
+    *o = c < rsA ? (int)K.L.cx + 16 * c : 16 * (rsB0 + c - rsA);
+  };
+  if ((int)threadIdx.x < nres * rpp) {
+    rest_piece(threadIdx.x, &rest_k, &rest_o);
+    rest_v = *(const uint4*)(src(rest_k) + rest_o);
+  }
   HeroPre* pre = (HeroPre*)(scr + ne * SL.bytes);  // [ne]
   int* best = (int*)(pre + ne);                   // [ne] target search result
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  auto rec = [&](int k) { return bind_ego(lds + k * pk.bytes, recs + (int64_t)(e0 + k) * rb, K, pk); };
+  auto rec = [&](int k) { return bind_ego(lds + k * pk.bytes, src(k), K, pk); };
   if (blockIdx.x == 0 && tid == 0 && K.ep_count_next != nullptr) *K.ep_count_next = 0;
   // S2 + S1 under the staging (waves 0 and 1 issue none of it, so their loads
   // are waited for precisely while the LDS-DMA of waves 2 and 3 stays in
@@ -2560,7 +2689,7 @@ __global__ __launch_bounds__(256) void k_ego(uint8_t* __restrict__ recs, int n, 
   const bool s2 = wave <= 1 && s2k < ne_eff;
   double s2x[S2_PF], s2y[S2_PF], s2hx = 0.0, s2hy = 0.0, s2yaw = 0.0;
   int s2nr = 0;
-  const DRec s2g = bind_rec(recs + (int64_t)(e0 + (s2 ? s2k : 0)) * rb, K.L, K.C);
+  const DRec s2g = bind_rec(src(s2 ? s2k : 0), K.L, K.C);
   if (s2) {
     s2hx = s2g.hd[CBEV_HD_X];
     s2hy = s2g.hd[CBEV_HD_Y];
@@ -2580,7 +2709,7 @@ __global__ __launch_bounds__(256) void k_ego(uint8_t* __restrict__ recs, int n, 
   const int tpe5 = 256 / ne, k5 = tid / tpe5, sub5 = tid - k5 * tpe5;
   double t5x[S5_PF], t5y[S5_PF];
   if (k5 < ne_eff) {
-    const DRec g = bind_rec(recs + (int64_t)(e0 + k5) * rb, K.L, K.C);
+    const DRec g = bind_rec(src(k5), K.L, K.C);
 #pragma unroll
     for (int j = 0; j < S5_PF; ++j) {
       const int i = min(sub5 + j * tpe5, K.C.route_cap - 1);
@@ -2595,7 +2724,7 @@ __global__ __launch_bounds__(256) void k_ego(uint8_t* __restrict__ recs, int n, 
   if (wave >= 2 && lane < ne_eff) {
     float ag, asa, ab;
     d_decode_action(K, actions, e0 + lane, &ag, &asa, &ab);
-    const double* ghd = (const double*)(recs + (int64_t)(e0 + lane) * rb + K.L.hd);
+    const double* ghd = (const double*)(src(lane) + K.L.hd);
     if (wave == 2) {
       pre[lane].g = ag;
       pre[lane].sa = asa;
@@ -2613,7 +2742,7 @@ __global__ __launch_bounds__(256) void k_ego(uint8_t* __restrict__ recs, int n, 
   int pasz = 0;
   if (tid < ne_eff * A) {
     const int k = tid / A, a = tid - k * A;
-    const DRec g = bind_rec(recs + (int64_t)(e0 + k) * rb, K.L, K.C);
+    const DRec g = bind_rec(src(k), K.L, K.C);
     pax = RAD(g, CBEV_AD_X, a);
     pay = RAD(g, CBEV_AD_Y, a);
     payaw = RAD(g, CBEV_AD_YAW, a);
@@ -2855,6 +2984,12 @@ __global__ __launch_bounds__(256) void k_ego(uint8_t* __restrict__ recs, int n, 
   CBEV_STAMP(1, 2);
   // S7
   ego_stage_out(lds, recs, e0, ne_eff, K, pk);
+  if (rest_k >= 0) *(uint4*)(recs + (int64_t)(e0 + rest_k) * rb + rest_o) = rest_v;
+  for (int q = threadIdx.x + 256; q < nres * rpp; q += 256) {
+    int k, o;
+    rest_piece(q, &k, &o);
+    *(uint4*)(recs + (int64_t)(e0 + k) * rb + o) = *(const uint4*)(src(k) + o);
+  }
   CBEV_STAMP(1, 3);
 }
 
@@ -3205,6 +3340,25 @@ struct cbev_ctx {
   // bank cursor of cbev_reset_masked (rows taken so far): one copy per
   // k_reset_mask workgroup, all equal between calls
   unsigned long long* cur_dev;  // [RESET_MASK_WGS * CBEV_CURSOR_STRIDE]
+  // cbev_set_deferred_reset: a cbev_reset_terminated recorded here and folded
+  // into the next cbev_step's k_ego (KArgs::rmask), or launched as k_reset_mask
+  // by the next call that would observe it (flush_pending)
+  int defer_reset;
+  struct {
+    int on;
+    void* records;
+    int n;
+    const uint8_t* mask;
+    const void* bank;
+    int n_bank;
+    const uint8_t* bank_frames;
+    uint8_t* frames;
+    int n_frames;
+    void* stream;
+  } pend;
+  uint8_t* term_scr;          // [scr_n] the folding step's termination flags (k_ego -> k_raster)
+  int32_t* rrow_dev;          // [scr_n] the folding step's bank row per env, -1 (k_ego -> k_raster)
+  int scr_n;
   const uint8_t* last_term;   // term buffer of the last cbev_step (cbev_reset_terminated's mask)
   int last_n;                 // n of the last cbev_step (0: none yet)
 };
@@ -3316,6 +3470,12 @@ static KArgs kargs(const cbev_ctx* c) {
   K.ep_rows = nullptr;
   K.ep_count = K.ep_count_next = nullptr;
   K.tick_s = c->tick_s;
+  K.rmask = K.rbank = K.rbank_frames = K.term_scr = nullptr;
+  K.rring = K.term_pub = nullptr;
+  K.rcursor = nullptr;
+  K.rrow = nullptr;
+  K.rring_stride = 0;
+  K.rn_bank = K.rn_frames = K.rslot = K.rncur = 0;
   return K;
 }
 
@@ -3345,6 +3505,26 @@ static void launch_raster(const cbev_ctx* c, const KArgs& K, void* records, int 
     case 128: hipLaunchKernelGGL(k_raster<2>, dim3(n * Tiles<2>::T), dim3(kRasterNT), lb, s, K, (uint8_t*)records, n, frames); break;
     default: hipLaunchKernelGGL(k_raster<4>, dim3(n * Tiles<4>::T), dim3(kRasterNT), lb, s, K, (uint8_t*)records, n, frames); break;
   }
+}
+
+
+static int launch_reset_mask(cbev_ctx* c, void* records, int n, const uint8_t* mask, const void* bank, int n_bank,
+                             const uint8_t* bank_frames, uint8_t* frames, int n_frames, void* stream);
+// a recorded (deferred) reset, launched now on the stream it was recorded on
+static int flush_pending(cbev_ctx* c) {
+  if (!c->pend.on) return CBEV_OK;
+  c->pend.on = 0;
+  return launch_reset_mask(c, c->pend.records, c->pend.n, c->pend.mask, c->pend.bank, c->pend.n_bank,
+                           c->pend.bank_frames, c->pend.frames, c->pend.n_frames, c->pend.stream);
+}
+#define CBEV_FLUSH(c)                     \
+  do {                                    \
+    const int rc_ = flush_pending(c);     \
+    if (rc_ != CBEV_OK) return rc_;       \
+  } while (0)
+// can k_ego take the reset (no k_actors before it; its workgroups within the cursor copies)?
+static bool fold_ok(const cbev_ctx* c, int n) {
+  return c->C.actor_cap == 0 && (n + c->ego_ne - 1) / c->ego_ne <= RESET_MASK_WGS && n <= CBEV_RESET_MASK_MAX_N;
 }
 
 
@@ -3463,6 +3643,7 @@ int cbev_create(const cbev_params* params, const cbev_caps* caps, int device, cb
 
 int cbev_set_episode_stats(cbev_ctx* c, void* stats, int n, double* rows, int32_t* counts, int ring) {
   if (!c) return set_err(CBEV_EINVAL, "null argument");
+  CBEV_FLUSH(c);  // a deferred reset is applied before anything observes the state
   if (stats && (!rows || !counts || ring < 3 || n <= 0))
     return set_err(CBEV_EINVAL, "episode stats need rows, counts and a ring of at least 3 slots");
   c->stats = (cbev_episode_stats*)stats;
@@ -3536,6 +3717,7 @@ int cbev_profile_read(cbev_ctx* c, double* ms3, int64_t* steps) {
 
 int cbev_profile_raster(cbev_ctx* c, void* records, int n, uint8_t* frames, int reps, void* stream, double* ms) {
   if (!c || !records || !frames || !ms) return set_err(CBEV_EINVAL, "null argument");
+  CBEV_FLUSH(c);  // a deferred reset is applied before anything observes the state
   if (!c->map_dev) return set_err(CBEV_ESTATE, "cbev_set_map not called");
   if (n <= 0 || reps <= 0) return set_err(CBEV_EINVAL, "n and reps must be positive");
   HIP_TRY(hipSetDevice(c->device));
@@ -3559,6 +3741,9 @@ int cbev_profile_raster(cbev_ctx* c, void* records, int n, uint8_t* frames, int 
 
 void cbev_destroy(cbev_ctx* c) {
   if (!c) return;
+  c->pend.on = 0;  // a deferred reset nothing observed is dropped with the context
+  if (c->term_scr) (void)hipFree(c->term_scr);
+  if (c->rrow_dev) (void)hipFree(c->rrow_dev);
   (void)hipSetDevice(c->device);
   if (c->prof_ev) {
     for (int i = 0; i < 4 * CBEV_PROF_MAX; ++i) (void)hipEventDestroy(c->prof_ev[i]);
@@ -3578,6 +3763,7 @@ void cbev_destroy(cbev_ctx* c) {
 
 int cbev_set_map(cbev_ctx* c, const uint8_t* map_host, int64_t bytes) {
   if (!c || !map_host) return set_err(CBEV_EINVAL, "null argument");
+  CBEV_FLUSH(c);  // a deferred reset is applied before anything observes the state
   const int64_t need = (int64_t)c->P.map_pitch * c->P.render_h;
   if (bytes != need) return set_err(CBEV_EINVAL, "map bytes %lld != pitch*render_h %lld", (long long)bytes, (long long)need);
   const int W = c->P.render_w, H = c->P.render_h, pitch = c->P.map_pitch;
@@ -3634,6 +3820,44 @@ int cbev_step(cbev_ctx* c, void* records, int n, const void* actions, uint8_t* f
   if (c->stats && n > c->ep_n) return set_err(CBEV_EINVAL, "n %d exceeds the %d envs of the episode stats", n, c->ep_n);
   hipStream_t s = (hipStream_t)stream;
   KArgs K = kargs(c);
+  // a deferred reset of these records whose ring holds `frames`: k_ego takes it
+  uint8_t* ego_term = term;
+  bool fold = false;
+  if (c->pend.on) {
+    const int64_t stride = (int64_t)n * c->P.size * c->P.size;
+    const int64_t off = frames - c->pend.frames;
+    fold = records == c->pend.records && n == c->pend.n && off >= 0 && off % stride == 0 &&
+           off / stride < c->pend.n_frames && fold_ok(c, n);
+    if (fold && c->scr_n < n) {
+      if (c->term_scr) HIP_TRY(hipFree(c->term_scr));
+      if (c->rrow_dev) HIP_TRY(hipFree(c->rrow_dev));
+      c->term_scr = nullptr;
+      c->rrow_dev = nullptr;
+      c->scr_n = 0;
+      HIP_TRY(hipMalloc(&c->term_scr, n));
+      HIP_TRY(hipMalloc(&c->rrow_dev, 4 * (size_t)n));
+      c->scr_n = n;
+    }
+    if (fold) {
+      K.rmask = c->pend.mask;
+      K.rbank = (const uint8_t*)c->pend.bank;
+      K.rbank_frames = c->pend.bank_frames;
+      K.rring = c->pend.frames;
+      K.rring_stride = stride;
+      K.rn_bank = c->pend.n_bank;
+      K.rn_frames = c->pend.n_frames;
+      K.rslot = (int)(off / stride);
+      K.rcursor = c->cur_dev;
+      K.rncur = RESET_MASK_WGS;
+      K.rrow = c->rrow_dev;
+      K.term_scr = c->term_scr;
+      K.term_pub = term;
+      ego_term = c->term_scr;
+      c->pend.on = 0;
+    } else {
+      CBEV_FLUSH(c);
+    }
+  }
   c->last_term = term;
   c->last_n = n;
   const int wg4 = (n + 3) / 4;
@@ -3651,7 +3875,7 @@ int cbev_step(cbev_ctx* c, void* records, int n, const void* actions, uint8_t* f
   }
   hipLaunchKernelGGL(k_ego, dim3((n + c->ego_ne - 1) / c->ego_ne), dim3(256), (size_t)c->ego_lb, s,
                      (uint8_t*)records, n, c->ego_ne, (int)c->L.record_bytes, ego_pack(c->L).n0, ego_pack(c->L).n,
-                     (int)c->L.raw_x, K, actions, reward, term, trunc, cause, info);
+                     (int)c->L.raw_x, K, actions, reward, ego_term, trunc, cause, info);
   if (ev) HIP_TRY(hipEventRecord(ev[2], s));
   launch_raster(c, K, records, n, frames, s);
   if (ev) HIP_TRY(hipEventRecord(ev[3], s));
@@ -3662,6 +3886,7 @@ int cbev_step(cbev_ctx* c, void* records, int n, const void* actions, uint8_t* f
 int cbev_reset(cbev_ctx* c, void* records, int n, const void* bank, int n_bank, const uint8_t* mask,
                const int32_t* bank_idx, int bank_offset, uint8_t* frames, int n_frames, void* stream) {
   if (!c || !records || !frames) return set_err(CBEV_EINVAL, "null argument");
+  CBEV_FLUSH(c);  // a deferred reset is applied before anything observes the state
   if (!c->map_dev) return set_err(CBEV_ESTATE, "cbev_set_map not called");
   if (bank && n_bank <= 0) return set_err(CBEV_EINVAL, "empty bank");
   if (n_frames < 1) return set_err(CBEV_EINVAL, "n_frames < 1");
@@ -3685,6 +3910,7 @@ int cbev_reset(cbev_ctx* c, void* records, int n, const void* bank, int n_bank, 
 
 int cbev_bank_frames(cbev_ctx* c, const void* bank, int n_bank, uint8_t* frames, void* stream) {
   if (!c || !bank || !frames) return set_err(CBEV_EINVAL, "null argument");
+  CBEV_FLUSH(c);  // a deferred reset is applied before anything observes the state
   if (!c->map_dev) return set_err(CBEV_ESTATE, "cbev_set_map not called");
   if (n_bank <= 0) return CBEV_OK;
   KArgs K = kargs(c);
@@ -3704,6 +3930,7 @@ int cbev_reset_frames(cbev_ctx* c, void* records, int n, const void* bank, int n
                       const int32_t* bank_idx, int bank_offset, const uint8_t* bank_frames, uint8_t* frames,
                       int n_frames, void* stream) {
   if (!c || !records || !bank || !bank_frames || !frames) return set_err(CBEV_EINVAL, "null argument");
+  CBEV_FLUSH(c);  // a deferred reset is applied before anything observes the state
   if (n_bank <= 0) return set_err(CBEV_EINVAL, "empty bank");
   if (n_frames < 1) return set_err(CBEV_EINVAL, "n_frames < 1");
   if (n <= 0) return CBEV_OK;
@@ -3727,6 +3954,12 @@ int cbev_reset_masked(cbev_ctx* c, void* records, int n, const uint8_t* mask, co
   if (n_frames < 1) return set_err(CBEV_EINVAL, "n_frames < 1");
   if (n > CBEV_RESET_MASK_MAX_N) return set_err(CBEV_EINVAL, "n %d exceeds %d", n, CBEV_RESET_MASK_MAX_N);
   if (n <= 0) return CBEV_OK;
+  CBEV_FLUSH(c);
+  return launch_reset_mask(c, records, n, mask, bank, n_bank, bank_frames, frames, n_frames, stream);
+}
+
+static int launch_reset_mask(cbev_ctx* c, void* records, int n, const uint8_t* mask, const void* bank, int n_bank,
+                             const uint8_t* bank_frames, uint8_t* frames, int n_frames, void* stream) {
   KArgs K = kargs(c);
   const int SS = c->P.size * c->P.size;
   const int64_t ppe = reset_pieces((int64_t)SS) + reset_pieces(c->L.record_bytes);
@@ -3744,11 +3977,43 @@ int cbev_reset_terminated(cbev_ctx* c, void* records, int n, const void* bank, i
   if (!c) return set_err(CBEV_EINVAL, "null argument");
   if (c->last_n == 0) return set_err(CBEV_ESTATE, "cbev_reset_terminated before any cbev_step");
   if (n != c->last_n) return set_err(CBEV_EINVAL, "n %d != the %d envs of the last cbev_step", n, c->last_n);
+  if (c->defer_reset && fold_ok(c, n)) {
+    if (!records || !bank || !bank_frames || !frames) return set_err(CBEV_EINVAL, "null argument");
+    if (n_bank <= 0) return set_err(CBEV_EINVAL, "empty bank");
+    if (n_frames < 1) return set_err(CBEV_EINVAL, "n_frames < 1");
+    CBEV_FLUSH(c);  // an earlier one no step took
+    c->pend.on = 1;
+    c->pend.records = records;
+    c->pend.n = n;
+    c->pend.mask = c->last_term;
+    c->pend.bank = bank;
+    c->pend.n_bank = n_bank;
+    c->pend.bank_frames = bank_frames;
+    c->pend.frames = frames;
+    c->pend.n_frames = n_frames;
+    c->pend.stream = stream;
+    return CBEV_OK;
+  }
   return cbev_reset_masked(c, records, n, c->last_term, bank, n_bank, bank_frames, frames, n_frames, stream);
+}
+
+int cbev_set_deferred_reset(cbev_ctx* c, int on) {
+  if (!c) return set_err(CBEV_EINVAL, "null argument");
+  if (!on) CBEV_FLUSH(c);
+  c->defer_reset = on != 0;
+  return CBEV_OK;
+}
+
+int cbev_reset_pending(const cbev_ctx* c) { return c && c->pend.on ? 1 : 0; }
+
+int cbev_flush(cbev_ctx* c) {
+  if (!c) return set_err(CBEV_EINVAL, "null argument");
+  return flush_pending(c);
 }
 
 int cbev_bank_cursor(cbev_ctx* c, int64_t* cursor) {
   if (!c || !cursor) return set_err(CBEV_EINVAL, "null argument");
+  CBEV_FLUSH(c);  // a deferred reset is applied before anything observes the state
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(hipDeviceSynchronize());  // the resets are queued on the caller's (non-blocking) stream
   unsigned long long v = 0;
@@ -3760,6 +4025,7 @@ int cbev_bank_cursor(cbev_ctx* c, int64_t* cursor) {
 int cbev_expand_obs(cbev_ctx* c, const uint8_t* ring, int n, int n_frames, int head, int kind, int n_channels,
                     const uint32_t* lut_host, void* out, void* stream) {
   if (!c || !ring || !out) return set_err(CBEV_EINVAL, "null argument");
+  CBEV_FLUSH(c);  // a deferred reset is applied before anything observes the state
   if (!lut_host && kind != 5) return set_err(CBEV_EINVAL, "null lut");
   if (n_frames < 1 || head < 0 || head >= n_frames) return set_err(CBEV_EINVAL, "bad frame ring");
   const bool sem = kind == 0 || kind == 3 || kind == 4;
@@ -3853,6 +4119,7 @@ static void area_tab(int ssize, int dsize, double scale, std::vector<int32_t>& o
 
 int cbev_pack_frames(cbev_ctx* c, const uint8_t* frames, int n, uint8_t* packed, void* stream) {
   if (!c || !frames || !packed) return set_err(CBEV_EINVAL, "null argument");
+  CBEV_FLUSH(c);  // a deferred reset is applied before anything observes the state
   // 16-byte loads of the ids, 8-byte stores of the packed bytes
   if (((uintptr_t)frames & 15) || ((uintptr_t)packed & 7)) return set_err(CBEV_EINVAL, "misaligned frames / packed");
   if (n <= 0) return CBEV_OK;
@@ -3865,6 +4132,7 @@ int cbev_pack_frames(cbev_ctx* c, const uint8_t* frames, int n, uint8_t* packed,
 
 int cbev_unpack_frames(cbev_ctx* c, const uint8_t* packed, int n, uint8_t* frames, void* stream) {
   if (!c || !frames || !packed) return set_err(CBEV_EINVAL, "null argument");
+  CBEV_FLUSH(c);  // a deferred reset is applied before anything observes the state
   if (((uintptr_t)frames & 15) || ((uintptr_t)packed & 7)) return set_err(CBEV_EINVAL, "misaligned frames / packed");
   if (n <= 0) return CBEV_OK;
   const int64_t n16 = (int64_t)n * c->P.size * c->P.size / 16;
@@ -3876,6 +4144,7 @@ int cbev_unpack_frames(cbev_ctx* c, const uint8_t* packed, int n, uint8_t* frame
 
 int cbev_vector_obs(cbev_ctx* c, const void* records, int n, float* out, void* stream) {
   if (!c || !records || !out) return set_err(CBEV_EINVAL, "null argument");
+  CBEV_FLUSH(c);  // a deferred reset is applied before anything observes the state
   if (n <= 0) return CBEV_OK;
   hipLaunchKernelGGL(k_vector_obs, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, kargs(c),
                      (const uint8_t*)records, n, out);
@@ -3885,6 +4154,7 @@ int cbev_vector_obs(cbev_ctx* c, const void* records, int n, float* out, void* s
 
 int cbev_set_fov_mask(cbev_ctx* c, const uint8_t* mask_host) {
   if (!c) return set_err(CBEV_EINVAL, "null argument");
+  CBEV_FLUSH(c);  // a deferred reset is applied before anything observes the state
   const size_t SS = (size_t)c->P.size * c->P.size;
   HIP_TRY(hipSetDevice(c->device));
   if (!mask_host) {
@@ -3904,6 +4174,7 @@ int cbev_set_fov_mask(cbev_ctx* c, const uint8_t* mask_host) {
 
 int cbev_set_obs_size(cbev_ctx* c, int h, int w) {
   if (!c) return set_err(CBEV_EINVAL, "null argument");
+  CBEV_FLUSH(c);  // a deferred reset is applied before anything observes the state
   const int S = c->P.size;
   if (h < 1 || w < 1) return set_err(CBEV_EINVAL, "obs size %dx%d", h, w);
   if (h > S || w > S)
@@ -3961,6 +4232,7 @@ int cbev_set_obs_size(cbev_ctx* c, int h, int w) {
 int cbev_resize_obs(cbev_ctx* c, const uint8_t* frames, int n, const uint8_t* mask, int gray, uint8_t* out, int n_out,
                     int64_t out_stride, void* stream) {
   if (!c || !frames || !out) return set_err(CBEV_EINVAL, "null argument");
+  CBEV_FLUSH(c);  // a deferred reset is applied before anything observes the state
   if (n_out < 1) return set_err(CBEV_EINVAL, "n_out %d", n_out);
   const int S = c->P.size;
   if (c->obs_h == S && c->obs_w == S) return set_err(CBEV_ESTATE, "cbev_set_obs_size: no resize configured");

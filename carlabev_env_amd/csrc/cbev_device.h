@@ -38,6 +38,23 @@ struct KArgs {
   int32_t* ep_count;          // this step's row count (zeroed by the step before)
   int32_t* ep_count_next;     // the next step's row count, zeroed by this step
   double tick_s;              // seconds per wall_clock64() tick
+  // The canonical reset folded into this step (cbev_set_deferred_reset: a
+  // cbev_reset_terminated recorded, applied by k_ego; rmask null: none). k_ego
+  // ranks the mask, takes each reset env's record from bank row
+  // (cursor + rank) % rn_bank, writes the row to rrow[e] (-1: not reset) and the
+  // step's termination flags to term_scr (the mask is the previous step's
+  // flags); k_raster copies the bank frame into the ring slots other than rslot
+  // and publishes term_pub[e] = term_scr[e].
+  const uint8_t* rmask;
+  const uint8_t* rbank;
+  const uint8_t* rbank_frames;
+  uint8_t* rring;
+  unsigned long long* rcursor;  // the cursor copies (k_reset_mask's): slot w of workgroup w
+  int32_t* rrow;
+  const uint8_t* term_scr;
+  uint8_t* term_pub;
+  int64_t rring_stride;  // bytes between ring slots (n * S * S)
+  int rn_bank, rn_frames, rslot, rncur;
 };
 
 // class id of padded-map texel (x, y)

@@ -117,7 +117,8 @@ class CarlaBEVVectorEnv:
     metadata = {"autoreset_mode": "disabled", "render_modes": ["rgb_array"], "render_fps": 60}
 
     def __init__(self, cfg, *, num_envs: int | None = None, device=None, caps: dict | None = None,
-                 info_mode: str = "full", scene_generator=None, wrappers: bool = True, copy_obs: bool = True):
+                 info_mode: str = "full", scene_generator=None, wrappers: bool = True, copy_obs: bool = True,
+                 defer_reset: bool = True):
         """wrappers=False gives the base `CarlaBEV` observation of every env, as a
         `SyncVectorEnv` of unwrapped `CarlaBEV(cfg)` would: (S, S, 3) uint8 RGB for the
         BEV modes, float32[7] for obs_mode="vector" (carlabev.py:233-244, spaces.py:54-61).
@@ -126,7 +127,12 @@ class CarlaBEVVectorEnv:
         copy_obs=True (default) returns a fresh observation tensor from every step() /
         reset(), as SyncVectorEnv(copy=True) returns fresh arrays; copy_obs=False returns
         the env's own buffer, which the next step() / reset() overwrites in place
-        (throughput loops that consume obs before stepping again)."""
+        (throughput loops that consume obs before stepping again).
+
+        defer_reset=True (default) lets reset_terminated() fold into the next step's
+        first kernel (cbev_set_deferred_reset): every accessor of the env's state
+        (records, ring, term, frames(), observations, render, the bank calls) applies a
+        recorded reset first, so what the caller observes is unchanged."""
         if isinstance(cfg, RunConfig):
             raw = cfg
         elif isinstance(cfg, dict) and "env" in cfg:
@@ -177,22 +183,28 @@ class CarlaBEVVectorEnv:
         if self.resize:
             check(L.cbev_set_obs_size(ctx, self.obs_hw[0], self.obs_hw[1]), "cbev_set_obs_size")
         h, w = self.obs_hw
-        self.records = torch.zeros((N, self.rb), dtype=torch.uint8, device=dev)
-        self.ring = torch.zeros((F, N, h, w), dtype=torch.uint8, device=dev)
+        # records, frame ring and term flags: reached through the properties below,
+        # which apply a deferred reset first
+        self._reset_pending = False
+        self._records = torch.zeros((N, self.rb), dtype=torch.uint8, device=dev)
+        self._ring = torch.zeros((F, N, h, w), dtype=torch.uint8, device=dev)
         # render-size frame of the current step (render(), carlabev.py:233-249); the
         # newest ring slot itself when there is no resize
         self.full = torch.zeros((N, S, S), dtype=torch.uint8, device=dev) if self.resize else None
         self.head = 0
         self.reward = torch.zeros(N, dtype=torch.float64, device=dev)
-        self.term = torch.zeros(N, dtype=torch.uint8, device=dev)
+        self._term = torch.zeros(N, dtype=torch.uint8, device=dev)
         self.trunc = torch.zeros(N, dtype=torch.uint8, device=dev)
         self.cause = torch.zeros(N, dtype=torch.int32, device=dev)
         self.info = torch.zeros((N, 16), dtype=torch.float32, device=dev)
         # device addresses of the per-step buffers (allocated once here): the step's
         # host path passes them as plain ints instead of re-reading tensor metadata
-        self._p_step = tuple(t.data_ptr() for t in (self.records, self.reward, self.term, self.trunc, self.cause,
+        self._p_step = tuple(t.data_ptr() for t in (self._records, self.reward, self._term, self.trunc, self.cause,
                                                       self.info))
-        self._p_ring, self._slot_bytes = self.ring.data_ptr(), N * h * w
+        self._p_ring, self._slot_bytes = self._ring.data_ptr(), N * h * w
+        # the canonical reset folded into the next step (frames are rendered straight
+        # into the ring only without a resize)
+        check(L.cbev_set_deferred_reset(ctx, 1 if (defer_reset and not self.resize) else 0), "cbev_set_deferred_reset")
         self._p_full = self.full.data_ptr() if self.full is not None else None
         self._dev_index = dev.index if dev.index is not None else torch.cuda.current_device()
         # spaces (envs/spaces.py:27-61 + wrapper spaces)
@@ -252,6 +264,29 @@ class CarlaBEVVectorEnv:
         self.auto_obs = True  # reset_from_bank also expands the wire observation
         self._closed = False
 
+    # ------------------------------------------------------------------ state (deferred reset applied first)
+    def flush(self):
+        """Apply a reset_terminated() the next step has not taken yet (cbev_flush;
+        stream-ordered, no sync). Every accessor below calls it."""
+        if self._reset_pending:
+            self._reset_pending = False
+            check(lib().cbev_flush(self._ctx), "cbev_flush")
+
+    @property
+    def records(self) -> torch.Tensor:
+        self.flush()
+        return self._records
+
+    @property
+    def ring(self) -> torch.Tensor:
+        self.flush()
+        return self._ring
+
+    @property
+    def term(self) -> torch.Tensor:
+        self.flush()
+        return self._term
+
     # ------------------------------------------------------------------ helpers
     def _stream(self):
         # the caller's current stream on the env's device (raw handle: no Stream object per call)
@@ -279,6 +314,7 @@ class CarlaBEVVectorEnv:
         without per-reset host work."""
         if bank_records.device != self.device or bank_records.dtype != torch.uint8 or bank_records.shape[1] != self.rb:
             raise ValueError("bank must be a (B, record_bytes) uint8 tensor on the env device")
+        self.flush()  # a deferred reset reads the old bank
         self.bank = bank_records.contiguous()
         self.bank_contexts = contexts
         # reset observations of the bank, rendered once; reset_from_bank then only copies
@@ -304,6 +340,7 @@ class CarlaBEVVectorEnv:
         released (one device read of the records' CTX_ID words)."""
         if self.bank is None:
             raise RuntimeError("no scene bank attached")
+        self.flush()  # a deferred reset reads the rows about to be overwritten
         B, k = self.bank.shape[0], int(records.shape[0])
         if k == 0:
             return slot0
@@ -391,7 +428,9 @@ class CarlaBEVVectorEnv:
             raise RuntimeError("no scene bank attached")
         if not self._stepped:
             raise RuntimeError("reset_terminated before any step()")
-        return self._reset_masked(self.term)
+        out = self._reset_masked(self._term)
+        self._reset_pending = self._reset_pending or bool(lib().cbev_reset_pending(self._ctx))
+        return out
 
     def _reset_masked(self, mask: torch.Tensor):
         N, B = self.num_envs, self.bank.shape[0]
@@ -560,6 +599,7 @@ class CarlaBEVVectorEnv:
         stream = self._stream()
         check(lib().cbev_step(self._ctx, rec, self.num_envs, a.data_ptr(), frames, rew, term, trunc, cause, info,
                               stream), "cbev_step")
+        self._reset_pending = False  # taken by this step (or launched before it)
         self._step_stream = stream.value or 0  # the step's rows are waited for on this stream (StepInfos)
         self._stepped = True
         if self.resize:
@@ -682,7 +722,7 @@ class CarlaBEVVectorEnv:
 
     def frames(self) -> torch.Tensor:
         """Newest render-size palette-id frames (N, S, S) uint8 (compact observation)."""
-        return self.full if self.resize else self.ring[self.head]
+        return self.full if self.resize else self.ring[self.head]  # self.ring applies a deferred reset
 
     def records_host(self) -> np.ndarray:
         return self.records.to("cpu").numpy()

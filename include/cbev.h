@@ -139,6 +139,24 @@ int cbev_reset_terminated(cbev_ctx* ctx, void* records, int n, const void* bank,
 /* Bank rows cbev_reset_masked / cbev_reset_terminated have handed out since
  * cbev_create (synchronises the device). */
 int cbev_bank_cursor(cbev_ctx* ctx, int64_t* cursor);
+/* Deferred canonical reset (off by default). With it on, cbev_reset_terminated
+ * records the reset instead of launching it, and the next cbev_step of the same
+ * records and frame ring folds it into its first kernel (k_ego; the envs take
+ * the same bank rows, records and ring slots end up as cbev_reset_masked leaves
+ * them, the mask is read when that step runs): the canonical loop's
+ * step -> reset(reset_mask=terminated) -> step costs no reset launch. Any other
+ * call on the context that reads or writes its state (every cbev_reset* call,
+ * cbev_expand_obs, cbev_vector_obs, cbev_resize_obs, cbev_pack_frames,
+ * cbev_bank_cursor, cbev_profile_raster, ...) or a cbev_step that cannot take
+ * it first launches it on the stream it was recorded on, as does cbev_flush.
+ * A caller that reads the records, the frame ring or writes the term buffer
+ * itself calls cbev_flush first. Only records without actor slots (k_ego is the
+ * step's first kernel) fold; otherwise cbev_reset_terminated launches at once. */
+int cbev_set_deferred_reset(cbev_ctx* ctx, int on);
+/* 1 when a deferred reset is recorded and not yet applied. */
+int cbev_reset_pending(const cbev_ctx* ctx);
+/* Launch a recorded deferred reset (k_reset_mask) now; no-op otherwise. */
+int cbev_flush(cbev_ctx* ctx);
 
 /* Wrapper stack on the device (wrap_env, envs/__init__.py:62-83). `ring` holds
  * n_frames frames per env (uint8[n_frames][n][h][w], slot `head` the newest;

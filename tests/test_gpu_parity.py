@@ -827,3 +827,133 @@ def test_reset_cursor_advances_under_graph_replay():
         cursor += k
         assert _cursor(L, dw) == cursor, rep
     assert cursor > B  # wrapped: every replay took fresh rows
+
+
+def _deferred_pair(n, B, F, caps, seed0, bank_seed0):
+    """Two contexts on the same scenes and bank: reset_terminated launched at once
+    (A) and deferred into the next step (B, cbev_set_deferred_reset)."""
+    cfg, P, padded, layout, builder = world(caps=caps)
+    recs, _ = build_records(builder, n, ["rt_no_traffic_v1"], seed0=seed0)
+    bank, _ = build_records(builder, B, ["rt_no_traffic_v1"], seed0=bank_seed0)
+    L = lib()
+    S = P.size
+    out = []
+    for deferred in (0, 1):
+        dw = DevWorld(P, padded, caps)
+        check(L.cbev_set_deferred_reset(dw.ctx, deferred), "deferred")
+        d_bank = torch.from_numpy(bank.copy()).cuda()
+        bf = torch.zeros((B, S, S), dtype=torch.uint8, device="cuda")
+        check(L.cbev_bank_frames(dw.ctx, ptr(d_bank), B, ptr(bf), None), "bank_frames")
+        d_recs = torch.from_numpy(recs.copy()).cuda()
+        ring = torch.zeros((F, n, S, S), dtype=torch.uint8, device="cuda")
+        check(L.cbev_reset(dw.ctx, ptr(d_recs), n, None, 0, None, None, 0, ptr(ring), F, None), "reset")
+        bufs = dict(rew=torch.zeros(n, dtype=torch.float64, device="cuda"),
+                    term=torch.zeros(n, dtype=torch.uint8, device="cuda"),
+                    trunc=torch.zeros(n, dtype=torch.uint8, device="cuda"),
+                    cause=torch.zeros(n, dtype=torch.int32, device="cuda"),
+                    info=torch.zeros((n, 16), dtype=torch.float32, device="cuda"))
+        out.append((dw, d_bank, bf, d_recs, ring, bufs))
+    return P, layout, out
+
+
+def test_deferred_reset_matches_immediate():
+    """The canonical reset folded into the next step's k_ego (cbev_set_deferred_reset)
+    leaves exactly the state the immediate k_reset_mask + step leave: records, every
+    frame-stack slot, reward / term / trunc / cause / info and the bank cursor, step
+    after step. Covered: envs pushed off the road (resets in most steps), in-place
+    edits of the term buffer between the step and the reset (the folded reset reads
+    the buffer when the next step runs), a reset read straight away (cbev_flush, and
+    cbev_expand_obs flushing by itself), a step with no reset before it, the frame
+    ring's slots in turn, an odd batch (partial k_ego workgroup)."""
+    for n, B, F in ((45, 13, 4), (4099, 6007, 4)):
+        P, layout, ctxs = _deferred_pair(n, B, F, bench_caps(2), 7000, 17000)
+        L = lib()
+        S = P.size
+        acts = action_stream(P, n, 16, seed=21)
+        rng = np.random.default_rng(3)
+        folded = 0
+        for t in range(16):
+            push = rng.choice(n, size=min(n, int(rng.integers(1, 9)) * max(1, n // 40)), replace=False)
+            extra = torch.from_numpy((rng.random(n) < 0.03).astype(np.uint8)).cuda()
+            folded += L.cbev_reset_pending(ctxs[1][0].ctx)
+            for dw, d_bank, bf, d_recs, ring, b in ctxs:
+                if t % 2 == 0:  # the caller writes the records: it flushes first (cbev.h)
+                    check(L.cbev_flush(dw.ctx), "flush")
+                    h = d_recs.cpu().numpy()
+                    for e in push:
+                        LY.RecordView(h[e], layout).hd[LY.HD["X"]] += 60.0
+                    d_recs.copy_(torch.from_numpy(h))
+                a = torch.from_numpy(np.ascontiguousarray(acts[t])).cuda()
+                check(L.cbev_step(dw.ctx, ptr(d_recs), n, ptr(a), ptr(ring[t % F]), ptr(b["rew"]), ptr(b["term"]),
+                                  ptr(b["trunc"]), ptr(b["cause"]), ptr(b["info"]), None), "step")
+            torch.cuda.synchronize()
+            (dA, _, _, rA, gA, bA), (dB, _, _, rB, gB, bB) = ctxs
+            assert L.cbev_reset_pending(dB.ctx) == 0
+            for k in ("rew", "term", "trunc", "cause", "info"):
+                assert torch.equal(bA[k], bB[k]), (n, t, k)
+            assert torch.equal(rA, rB), (n, t, "records")
+            assert torch.equal(gA, gB), (n, t, "ring")
+            if t % 5 == 4:  # no reset before the next step
+                continue
+            for dw, d_bank, bf, d_recs, ring, b in ctxs:
+                if t % 3 == 1:  # in-place edit of the mask before the reset
+                    b["term"] |= extra
+                check(L.cbev_reset_terminated(dw.ctx, ptr(d_recs), n, ptr(d_bank), B, ptr(bf), ptr(ring), F, None),
+                      "reset_terminated")
+            torch.cuda.synchronize()
+            assert L.cbev_reset_pending(dA.ctx) == 0 and L.cbev_reset_pending(dB.ctx) == 1, t
+            if t % 4 == 2:  # the reset observed right away: flush
+                check(L.cbev_flush(dB.ctx), "flush")
+                torch.cuda.synchronize()
+                assert torch.equal(rA, rB) and torch.equal(gA, gB), (n, t, "flushed reset")
+            elif t % 4 == 3:  # ... or through an observation call, which flushes by itself
+                out = torch.zeros((n, S, S, 3), dtype=torch.uint8, device="cuda")
+                check(L.cbev_expand_obs(dB.ctx, ptr(gB[0][None]), n, 1, 0, 2, 3, rgb_lut().ctypes.data_as(P_),
+                                        ptr(out), None), "expand")
+                torch.cuda.synchronize()
+                assert L.cbev_reset_pending(dB.ctx) == 0
+                assert torch.equal(rA, rB) and torch.equal(gA, gB), (n, t, "observed reset")
+        for dw, *_ in ctxs:
+            check(L.cbev_flush(dw.ctx), "flush")
+        torch.cuda.synchronize()
+        (dA, _, _, rA, gA, bA), (dB, _, _, rB, gB, bB) = ctxs
+        assert torch.equal(rA, rB) and torch.equal(gA, gB)
+        assert _cursor(L, dA) == _cursor(L, dB) and _cursor(L, dA) > 0
+        assert folded >= 3, folded  # steps that took a pending reset
+
+
+def test_vector_env_reads_after_deferred_reset():
+    """CarlaBEVVectorEnv defers reset_terminated into the next step; reading the
+    observation, the records or the term flags straight after it sees the reset
+    (the accessors flush), exactly as an env with the deferral off."""
+    from carlabev_env_amd import EnvConfig, make_env
+    cfg = EnvConfig(size=128, obs_size=(128, 128), render_mode="rgb_array", obs_mode="bev_semantic")
+    import bench
+    envs = [make_env({"env": cfg, "num_envs": 24}, info_mode="none", caps=dict(bench.CONFIGS[2]["caps"]),
+                     defer_reset=d) for d in (False, True)]
+    opts = build_random_navigation_options(RandomNavigationReset(difficulty_id="rt_no_traffic_v1"))
+    for env in envs:
+        env.reset(seed=5, options=opts)
+        env.attach_bank(env.build_bank([900 + k for k in range(11)], opts))
+        env.auto_obs = False
+    rng = np.random.default_rng(2)
+    seen = 0
+    for t in range(60):
+        a = rng.integers(0, 9, 24)
+        outs = []
+        for env in envs:
+            env.step(a)
+            if t % 7 == 0:  # push some envs off the road so resets happen
+                h = env.records_host()
+                for e in range(0, 24, 5):
+                    LY.RecordView(h[e], env.layout).hd[LY.HD["X"]] += 60.0
+                env.records.copy_(torch.from_numpy(h))
+            env.reset_terminated()
+            outs.append((env._obs().clone(), env.records.clone(), env.term.clone()))
+        assert torch.equal(outs[0][0], outs[1][0]), t
+        assert torch.equal(outs[0][1], outs[1][1]), t
+        assert torch.equal(outs[0][2], outs[1][2]), t
+        seen += int(outs[0][2].sum())
+    assert seen > 0
+    for env in envs:
+        env.close()
