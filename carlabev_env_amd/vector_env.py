@@ -428,9 +428,18 @@ class CarlaBEVVectorEnv:
             raise RuntimeError("no scene bank attached")
         if not self._stepped:
             raise RuntimeError("reset_terminated before any step()")
-        out = self._reset_masked(self._term)
-        self._reset_pending = self._reset_pending or bool(lib().cbev_reset_pending(self._ctx))
-        return out
+        if self.resize:
+            return self._reset_masked(self._term)
+        # cbev_reset_terminated: recorded for the next step to fold in (cbev_set_deferred_reset)
+        # or launched at once; its mask is the term buffer of the last step (this env's)
+        check(lib().cbev_reset_terminated(self._ctx, self._p_step[0], self.num_envs, self._p_bank, self.bank.shape[0],
+                                          self._p_bank_frames, self._p_ring, self.F, self._stream()),
+              "cbev_reset_terminated")
+        self._reset_pending = bool(lib().cbev_reset_pending(self._ctx))
+        if not self.auto_obs:
+            return None
+        obs = self._obs()
+        return obs.clone() if self.copy_obs else obs
 
     def _reset_masked(self, mask: torch.Tensor):
         N, B = self.num_envs, self.bank.shape[0]

@@ -937,7 +937,7 @@ def test_vector_env_reads_after_deferred_reset():
         env.attach_bank(env.build_bank([900 + k for k in range(11)], opts))
         env.auto_obs = False
     rng = np.random.default_rng(2)
-    seen = 0
+    seen = folded = 0
     for t in range(60):
         a = rng.integers(0, 9, 24)
         outs = []
@@ -949,11 +949,26 @@ def test_vector_env_reads_after_deferred_reset():
                     LY.RecordView(h[e], env.layout).hd[LY.HD["X"]] += 60.0
                 env.records.copy_(torch.from_numpy(h))
             env.reset_terminated()
+            if env is envs[1]:
+                folded += lib().cbev_reset_pending(env._ctx)  # recorded, not launched
             outs.append((env._obs().clone(), env.records.clone(), env.term.clone()))
         assert torch.equal(outs[0][0], outs[1][0]), t
         assert torch.equal(outs[0][1], outs[1][1]), t
         assert torch.equal(outs[0][2], outs[1][2]), t
         seen += int(outs[0][2].sum())
-    assert seen > 0
+    assert seen > 0 and folded == 60
+    # and a step takes a recorded reset (nothing read in between): the same state
+    for env in envs:
+        env.step(np.zeros(24, np.int64))
+        h = env.records_host()
+        for e in range(0, 24, 3):
+            LY.RecordView(h[e], env.layout).hd[LY.HD["X"]] += 60.0
+        env.records.copy_(torch.from_numpy(h))
+        env.step(np.ones(24, np.int64))
+        env.reset_terminated()
+        env.step(np.ones(24, np.int64))  # takes the reset
+        env.step(np.zeros(24, np.int64))
+    assert torch.equal(envs[0].records, envs[1].records) and torch.equal(envs[0].ring, envs[1].ring)
+    assert torch.equal(envs[0].reward, envs[1].reward)
     for env in envs:
         env.close()
