@@ -1761,36 +1761,7 @@ void k_raster(KArgs K, uint8_t* __restrict__ recs, int n, uint8_t* __restrict__ 
   const int64_t SS = (int64_t)K.P.size * K.P.size;
   const DRec r = bind_rec(recs + (int64_t)e * K.L.record_bytes, K.L, K.C);
   const RasterJob J = raster_job<false, G>(K, r);
-  // the reset folded into this step (KArgs::rmask): a reset env's bank frame,
-  // this tile of it, into every ring slot but the one this step renders
-  // (FrameStackObservation's reset padding), loaded before the render and
-  // stored after it
-  using TG = Tiles<G>;
-  constexpr int CPR = TG::TC / 16, PPT = TG::TC * TG::TR / 16 / kRasterNT;
-  const int row = K.rrow != nullptr ? K.rrow[e] : -1;
-  const bool rf = row >= 0 && K.rn_frames > 1;
-  const int ox0 = (t % TG::NTX) * TG::TC, oy0 = (t / TG::NTX) * TG::TR;
-  uint4 fv[PPT];
-  if (rf) {
-#pragma unroll
-    for (int j = 0; j < PPT; ++j) {
-      const int p = threadIdx.x + kRasterNT * j, pr = p / CPR;
-      fv[j] = *(const uint4*)(K.rbank_frames + (int64_t)row * SS + (oy0 + pr) * K.P.size + ox0 + 16 * (p - pr * CPR));
-    }
-  }
   raster_tile<G, true, kRasterNT>(K, r, J, t, frames + e * SS, 1, 0, lds);
-  if (rf) {
-    for (int f = 0; f < K.rn_frames; ++f) {
-      if (f == K.rslot) continue;
-      uint8_t* dst = K.rring + (int64_t)f * K.rring_stride + e * SS;
-#pragma unroll
-      for (int j = 0; j < PPT; ++j) {
-        const int p = threadIdx.x + kRasterNT * j, pr = p / CPR;
-        const uint4 v = fv[j];
-        store16_frame(dst + (oy0 + pr) * K.P.size + ox0 + 16 * (p - pr * CPR), u32x4_nt{v.x, v.y, v.z, v.w});
-      }
-    }
-  }
   // the step's termination flags, published once k_ego's reset no longer reads the previous ones
   if (K.term_pub != nullptr && t == 0 && threadIdx.x == 0) K.term_pub[e] = K.term_scr[e];
   CBEV_STAMP(2, 3);
@@ -2542,6 +2513,7 @@ __device__ __forceinline__ void butterfly(int tpe, F&& f) {
 // workgroup loads the whole mask (n bytes) and counts the selected envs before
 // its first env and in total; the cursor copies are k_reset_mask's (slot w of
 // workgroup w, all advanced by the total).
+__device__ __forceinline__ int P_size_sq(const KArgs& K) { return K.P.size * K.P.size; }
 struct EgoReset {
   uint64_t bits;            // the workgroup's envs to reset (bit k: env e0 + k)
   int base, total;          // bank row of the workgroup's first selected env; selected envs in the whole mask
@@ -2589,10 +2561,9 @@ __device__ __forceinline__ EgoReset ego_reset_scan(const KArgs& K, int n, int e0
   R.total = red[1] + red[3] + red[5] + red[7];
   R.bits = (uint64_t)(uint32_t)red[8] | ((uint64_t)(uint32_t)red[9] << 32);
   R.base = (int)((cur + (unsigned long long)before) % (unsigned long long)K.rn_bank);
-  // env k's bank row (or -1) for k_raster (the reset frame into the other ring slots)
+  // the reset envs' episode start
   if (tid < ne_eff) {
     const int row = ((R.bits >> tid) & 1u) ? ego_reset_row(R, tid, K.rn_bank) : -1;
-    K.rrow[e0 + tid] = row;
     if (row >= 0 && K.stats != nullptr) K.stats[e0 + tid].t0 = (double)wall_clock64();  // episode start
   }
   // this workgroup's cursor copies, advanced for the next reset
@@ -2669,6 +2640,19 @@ __global__ __launch_bounds__(256) void k_ego(uint8_t* __restrict__ recs, int n, 
   if ((int)threadIdx.x < nres * rpp) {
     rest_piece(threadIdx.x, &rest_k, &rest_o);
     rest_v = *(const uint4*)(src(rest_k) + rest_o);
+  }
+  // and its bank frame into every ring slot but the one this step renders
+  // (FrameStackObservation's reset padding): the first reset env's frame loaded
+  // now (16 bytes x SS / 4096 per thread) and stored at S7, any further ones at S7
+  const int64_t SSf = (int64_t)P_size_sq(K);
+  const int fpt = (int)(SSf / (16 * 256));  // 16-byte pieces per thread of one frame
+  uint4 fr_v[4];
+  const int fr_k = nres > 0 && K.rn_frames > 1 ? nth_set_bit(R.bits, 0) : -1;
+  if (fr_k >= 0 && fpt <= 4) {
+    const uint8_t* fsrc = K.rbank_frames + (int64_t)ego_reset_row(R, fr_k, K.rn_bank) * SSf;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (j < fpt) fr_v[j] = *(const uint4*)(fsrc + 16 * (threadIdx.x + 256 * j));
   }
   HeroPre* pre = (HeroPre*)(scr + ne * SL.bytes);  // [ne]
   int* best = (int*)(pre + ne);                   // [ne] target search result
@@ -2989,6 +2973,27 @@ __global__ __launch_bounds__(256) void k_ego(uint8_t* __restrict__ recs, int n, 
     int k, o;
     rest_piece(q, &k, &o);
     *(uint4*)(recs + (int64_t)(e0 + k) * rb + o) = *(const uint4*)(src(k) + o);
+  }
+  if (fr_k >= 0) {
+    for (uint64_t m = R.bits; m; m &= m - 1) {
+      const int k = __builtin_ctzll(m);
+      const uint8_t* fsrc = K.rbank_frames + (int64_t)ego_reset_row(R, k, K.rn_bank) * SSf;
+      uint8_t* fdst = K.rring + (int64_t)(e0 + k) * SSf;
+      auto put = [&](int64_t o, const uint4& v) {
+        for (int f = 0; f < K.rn_frames; ++f)
+          if (f != K.rslot) store16_frame(fdst + (int64_t)f * K.rring_stride + o, u32x4_nt{v.x, v.y, v.z, v.w});
+      };
+      if (k == fr_k && fpt <= 4) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (j < fpt) put(16 * (int64_t)(threadIdx.x + 256 * j), fr_v[j]);
+      } else {
+        for (int j = 0; j < fpt; ++j) {
+          const int64_t o = 16 * (int64_t)(threadIdx.x + 256 * j);
+          put(o, *(const uint4*)(fsrc + o));
+        }
+      }
+    }
   }
   CBEV_STAMP(1, 3);
 }
@@ -3357,7 +3362,6 @@ struct cbev_ctx {
     void* stream;
   } pend;
   uint8_t* term_scr;          // [scr_n] the folding step's termination flags (k_ego -> k_raster)
-  int32_t* rrow_dev;          // [scr_n] the folding step's bank row per env, -1 (k_ego -> k_raster)
   int scr_n;
   const uint8_t* last_term;   // term buffer of the last cbev_step (cbev_reset_terminated's mask)
   int last_n;                 // n of the last cbev_step (0: none yet)
@@ -3473,7 +3477,6 @@ static KArgs kargs(const cbev_ctx* c) {
   K.rmask = K.rbank = K.rbank_frames = K.term_scr = nullptr;
   K.rring = K.term_pub = nullptr;
   K.rcursor = nullptr;
-  K.rrow = nullptr;
   K.rring_stride = 0;
   K.rn_bank = K.rn_frames = K.rslot = K.rncur = 0;
   return K;
@@ -3743,7 +3746,6 @@ void cbev_destroy(cbev_ctx* c) {
   if (!c) return;
   c->pend.on = 0;  // a deferred reset nothing observed is dropped with the context
   if (c->term_scr) (void)hipFree(c->term_scr);
-  if (c->rrow_dev) (void)hipFree(c->rrow_dev);
   (void)hipSetDevice(c->device);
   if (c->prof_ev) {
     for (int i = 0; i < 4 * CBEV_PROF_MAX; ++i) (void)hipEventDestroy(c->prof_ev[i]);
@@ -3830,12 +3832,9 @@ int cbev_step(cbev_ctx* c, void* records, int n, const void* actions, uint8_t* f
            off / stride < c->pend.n_frames && fold_ok(c, n);
     if (fold && c->scr_n < n) {
       if (c->term_scr) HIP_TRY(hipFree(c->term_scr));
-      if (c->rrow_dev) HIP_TRY(hipFree(c->rrow_dev));
       c->term_scr = nullptr;
-      c->rrow_dev = nullptr;
       c->scr_n = 0;
       HIP_TRY(hipMalloc(&c->term_scr, n));
-      HIP_TRY(hipMalloc(&c->rrow_dev, 4 * (size_t)n));
       c->scr_n = n;
     }
     if (fold) {
@@ -3849,7 +3848,6 @@ int cbev_step(cbev_ctx* c, void* records, int n, const void* actions, uint8_t* f
       K.rslot = (int)(off / stride);
       K.rcursor = c->cur_dev;
       K.rncur = RESET_MASK_WGS;
-      K.rrow = c->rrow_dev;
       K.term_scr = c->term_scr;
       K.term_pub = term;
       ego_term = c->term_scr;

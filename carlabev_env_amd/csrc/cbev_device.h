@@ -41,16 +41,14 @@ struct KArgs {
   // The canonical reset folded into this step (cbev_set_deferred_reset: a
   // cbev_reset_terminated recorded, applied by k_ego; rmask null: none). k_ego
   // ranks the mask, takes each reset env's record from bank row
-  // (cursor + rank) % rn_bank, writes the row to rrow[e] (-1: not reset) and the
-  // step's termination flags to term_scr (the mask is the previous step's
-  // flags); k_raster copies the bank frame into the ring slots other than rslot
-  // and publishes term_pub[e] = term_scr[e].
+  // (cursor + rank) % rn_bank, copies the bank frame into the ring slots other
+  // than rslot and writes the step's termination flags to term_scr (the mask is
+  // the previous step's flags); k_raster publishes term_pub[e] = term_scr[e].
   const uint8_t* rmask;
   const uint8_t* rbank;
   const uint8_t* rbank_frames;
   uint8_t* rring;
   unsigned long long* rcursor;  // the cursor copies (k_reset_mask's): slot w of workgroup w
-  int32_t* rrow;
   const uint8_t* term_scr;
   uint8_t* term_pub;
   int64_t rring_stride;  // bytes between ring slots (n * S * S)
