@@ -112,14 +112,14 @@ def build_scene_sets(cfgd, n, rank, cache=None):
     return host, bank
 
 
-def build_env(cfgd, n, rank, device, info_mode="full", scenes=None):
+def build_env(cfgd, n, rank, device, info_mode="full", scenes=None, defer_reset=True):
     """Vector env with every env reset to its seeded start scene and the reset
     bank attached (terminated envs take its rows in order)."""
     from carlabev_env_amd.vector_env import CarlaBEVVectorEnv
     import torch
     host, bank = scenes if scenes is not None else build_scene_sets(cfgd, n, rank)
     env = CarlaBEVVectorEnv({"env": env_config(cfgd), "num_envs": n}, device=device, caps=cfgd["caps"],
-                            info_mode=info_mode)
+                            info_mode=info_mode, defer_reset=defer_reset)
     env.attach_bank(torch.from_numpy(bank).to(device))
     env.auto_obs = False
     start = torch.from_numpy(host).to(device)
@@ -373,6 +373,8 @@ def main():
                     help="canonical-loop steps before the timed passes, which all start from the state they leave")
     ap.add_argument("--repeats", type=int, default=5,
                     help="timed passes of exactly --steps steps each (re-seeded between); value = their median")
+    ap.add_argument("--no-defer-reset", action="store_true",
+                    help="launch every canonical reset at once (k_reset_mask) instead of folding it into the next step")
     ap.add_argument("--info-mode", default="full", choices=("none", "full"),
                     help="full (default, as the reference's step() always runs Stats.step, carlabev.py:226-227): "
                          "device episode statistics + a StepInfos per step (not read); none: statistics off")
@@ -402,7 +404,8 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=device)
     from carlabev_env_amd._lib import check, lib
-    env, host_recs, start_recs = build_env(cfgd, n, rank, device, args.info_mode, scenes)
+    env, host_recs, start_recs = build_env(cfgd, n, rank, device, args.info_mode, scenes,
+                                           defer_reset=not args.no_defer_reset)
     del scenes
     P = env.params
     total_steps = args.warmup + args.steps
@@ -575,6 +578,9 @@ def main():
             "dtype": "f64 state / u8 frames",
             "data": "synthetic seeded scenes (host scene-gen on the Town01 class map), seeded action streams",
             "info_mode": args.info_mode,
+            "reset": ("folded into the next step's k_ego (cbev_set_deferred_reset)"
+                      if bool(lib().cbev_reset_pending is not None) and not args.no_defer_reset
+                      and cfgd["caps"]["actor_cap"] == 0 else "k_reset_mask launch per step"),
             "config": {"workload": cfgd["workload"] if gather or "workload_n1" not in cfgd else cfgd["workload_n1"],
                        "config_id": args.config, "envs_per_gpu": n,
                        "global_envs": n * world, "obs_size": S, "obs_mode": cfgd["obs_mode"],

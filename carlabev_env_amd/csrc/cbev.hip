@@ -2640,6 +2640,7 @@ __global__ __launch_bounds__(256) void k_ego(uint8_t* __restrict__ recs, int n, 
   if ((int)threadIdx.x < nres * rpp) {
     rest_piece(threadIdx.x, &rest_k, &rest_o);
     rest_v = *(const uint4*)(src(rest_k) + rest_o);
+    asm volatile("" ::"v"(rest_v.x), "v"(rest_v.y), "v"(rest_v.z), "v"(rest_v.w));  // issued here, not sunk to S7
   }
   // and its bank frame into every ring slot but the one this step renders
   // (FrameStackObservation's reset padding): the first reset env's frame loaded
@@ -2653,6 +2654,9 @@ __global__ __launch_bounds__(256) void k_ego(uint8_t* __restrict__ recs, int n, 
 #pragma unroll
     for (int j = 0; j < 4; ++j)
       if (j < fpt) fr_v[j] = *(const uint4*)(fsrc + 16 * (threadIdx.x + 256 * j));
+#pragma unroll
+    for (int j = 0; j < 4; ++j)  // issued here, not sunk to S7
+      if (j < fpt) asm volatile("" ::"v"(fr_v[j].x), "v"(fr_v[j].y), "v"(fr_v[j].z), "v"(fr_v[j].w));
   }
   HeroPre* pre = (HeroPre*)(scr + ne * SL.bytes);  // [ne]
   int* best = (int*)(pre + ne);                   // [ne] target search result
