@@ -2523,55 +2523,75 @@ __device__ __forceinline__ int ego_reset_row(const EgoReset& R, int k, int n_ban
   return (int)((unsigned)(R.base + __popcll(R.bits & ((1ull << k) - 1ull))) % (unsigned)n_bank);
 }
 __device__ __forceinline__ EgoReset ego_reset_scan(const KArgs& K, int n, int e0, int ne_eff, int* red) {
+  // waves 0 and 1 load and count the mask (waves 2 and 3 keep their staging
+  // LDS-DMA in flight: raw barriers, no vmcnt drain)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const unsigned long long cur = K.rcursor[CBEV_CURSOR_STRIDE * blockIdx.x];
-  const int nu = (n + 15) >> 4, u0 = e0 >> 4;
-  const bool vec = ((uintptr_t)K.rmask & 15u) == 0;
-  int cb = 0, ct = 0;
-  for (int u = tid; u < nu; u += 256) {
-    uint32_t m = 0;
-    if (vec && 16 * u + 16 <= n) {
-      m = nonzero_bytes16(*(const uint4*)(K.rmask + 16 * (int64_t)u));
-    } else {
-      for (int b = 0; b < 16; ++b)
-        if (16 * u + b < n && K.rmask[16 * (int64_t)u + b] != 0) m |= 1u << b;
+  if (wave < 2) {
+    const int nu = (n + 15) >> 4, u0 = e0 >> 4;
+    const bool vec = ((uintptr_t)K.rmask & 15u) == 0;
+    int cb = 0, ct = 0;
+    for (int u = tid; u < nu; u += 128) {
+      uint32_t m = 0;
+      if (vec && 16 * u + 16 <= n) {
+        m = nonzero_bytes16(*(const uint4*)(K.rmask + 16 * (int64_t)u));
+      } else {
+        for (int b = 0; b < 16; ++b)
+          if (16 * u + b < n && K.rmask[16 * (int64_t)u + b] != 0) m |= 1u << b;
+      }
+      const int c = __popc(m);
+      ct += c;
+      cb += u < u0 ? c : (u == u0 ? __popc(m & ((1u << (e0 & 15)) - 1u)) : 0);
     }
-    const int c = __popc(m);
-    ct += c;
-    cb += u < u0 ? c : (u == u0 ? __popc(m & ((1u << (e0 & 15)) - 1u)) : 0);
-  }
-  const bool mine = tid < ne_eff && K.rmask[e0 + tid] != 0;  // wave 0: the workgroup's own envs (ne <= 64)
-  const uint64_t bits = __ballot(mine);
+    const bool mine = wave == 0 && tid < ne_eff && K.rmask[e0 + tid] != 0;  // the workgroup's own envs (ne <= 64)
+    const uint64_t bits = __ballot(mine);
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    cb += __shfl_xor(cb, o, 64);
-    ct += __shfl_xor(ct, o, 64);
+    for (int o = 32; o > 0; o >>= 1) {
+      cb += __shfl_xor(cb, o, 64);
+      ct += __shfl_xor(ct, o, 64);
+    }
+    if (lane == 0) {
+      red[2 * wave] = cb;
+      red[2 * wave + 1] = ct;
+    }
+    if (tid == 0) {
+      red[8] = (int)(uint32_t)bits;
+      red[9] = (int)(uint32_t)(bits >> 32);
+    }
   }
-  if (lane == 0) {
-    red[2 * wave] = cb;
-    red[2 * wave + 1] = ct;
-  }
-  if (tid == 0) {
-    red[8] = (int)(uint32_t)bits;
-    red[9] = (int)(uint32_t)(bits >> 32);
-  }
-  __syncthreads();
+  lds_barrier();
   EgoReset R;
-  const int before = red[0] + red[2] + red[4] + red[6];
-  R.total = red[1] + red[3] + red[5] + red[7];
+  const int before = red[0] + red[2];
+  R.total = red[1] + red[3];
   R.bits = (uint64_t)(uint32_t)red[8] | ((uint64_t)(uint32_t)red[9] << 32);
   R.base = (int)((cur + (unsigned long long)before) % (unsigned long long)K.rn_bank);
   // the reset envs' episode start
-  if (tid < ne_eff) {
-    const int row = ((R.bits >> tid) & 1u) ? ego_reset_row(R, tid, K.rn_bank) : -1;
-    if (row >= 0 && K.stats != nullptr) K.stats[e0 + tid].t0 = (double)wall_clock64();  // episode start
-  }
+  if (tid < ne_eff && ((R.bits >> tid) & 1u) && K.stats != nullptr) K.stats[e0 + tid].t0 = (double)wall_clock64();
   // this workgroup's cursor copies, advanced for the next reset
   if (R.total > 0)
     for (int w = blockIdx.x + gridDim.x * tid; w < K.rncur; w += gridDim.x * 256)
       K.rcursor[CBEV_CURSOR_STRIDE * w] = cur + (unsigned long long)R.total;
-  __syncthreads();
+  lds_barrier();  // red is the collision scratch from S4 on
   return R;
+}
+
+// the reset envs' staged ranges again, from their bank rows (waves 2 and 3,
+// the same pieces and LDS bytes as ego_stage_in): each wave waits for its own
+// first DMA, so the bank bytes land after the record's
+template <class Src>
+__device__ __forceinline__ void ego_restage(uint8_t* lds, Src src, uint64_t bits, int ne, int n0, int n, int raw_x) {
+  const int total = ne * n;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (wave < 2) return;
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's record DMA has landed
+  for (int b = (wave - 2) * 64; b < total; b += 128) {
+    const int q = b + lane;
+    const int k = q / n, c = q - k * n;
+    if (q < total && ((bits >> k) & 1ull))
+      __builtin_amdgcn_global_load_lds((const void*)(src(k) + ego_src(n0, raw_x, c)),
+                                       (__attribute__((address_space(3))) void*)(lds + 16 * b), 16, 0, 0);
+  }
 }
 
 // ============================================================== k_ego
@@ -2607,7 +2627,13 @@ __global__ __launch_bounds__(256) void k_ego(uint8_t* __restrict__ recs, int n, 
   const int ne_eff = min(ne, n - e0);
   const EgoPack pk = ego_pack(K.L);
   uint8_t* scr = lds + ne * pk.bytes;  // [ne] collision scratch (from S4; the folded reset's scan before)
-  // the folded reset: which envs take a bank row
+  // S0: the staging first (it depends on nothing loaded, and its scalars are
+  // preloaded), then the action loads and the actor prefetch, whose latency
+  // overlaps the staging's. With a folded reset the records are staged
+  // regardless (most envs keep theirs) and the reset envs again from their bank
+  // rows once the mask is ranked.
+  auto src_rec = [&](int k) -> uint8_t* { return recs + (int64_t)(e0 + k) * st_rb; };
+  ego_stage_in(lds, src_rec, ne_eff > 0 ? ne_eff : 0, st_n0, st_n, st_raw_x);
   EgoReset R{0ull, 0, 0};
   if (K.rmask != nullptr) R = ego_reset_scan(K, n, e0, ne_eff, (int*)scr);
   auto src = [&](int k) -> uint8_t* {
@@ -2615,10 +2641,7 @@ __global__ __launch_bounds__(256) void k_ego(uint8_t* __restrict__ recs, int n, 
       return (uint8_t*)K.rbank + (int64_t)ego_reset_row(R, k, K.rn_bank) * st_rb;
     return recs + (int64_t)(e0 + k) * st_rb;
   };
-  // S0: the staging first (it depends on nothing loaded, and its scalars are
-  // preloaded), then the action loads and the actor prefetch, whose latency
-  // overlaps the staging's
-  ego_stage_in(lds, src, ne_eff > 0 ? ne_eff : 0, st_n0, st_n, st_raw_x);
+  if (R.bits != 0ull) ego_restage(lds, src, R.bits, ne_eff, st_n0, st_n, st_raw_x);
   CBEV_STAMP(3, 0);
   const cbev_params& P = K.P;
   const int64_t rb = K.L.record_bytes;
