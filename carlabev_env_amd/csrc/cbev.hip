@@ -1333,7 +1333,7 @@ __device__ __forceinline__ RasterJob raster_job(const KArgs& K, const DRec& r) {
     int32_t* w = (int32_t*)&J.R;
 #pragma unroll
     for (int k = 0; k < CBEV_RS_WORDS; ++k) w[k] = r.hi[CBEV_HI_RS_R90 + k];
-    J.fast = r.hi[CBEV_HI_RS_FAST] != 0;
+    J.fast = (r.hi[CBEV_HI_RS_FAST] & 1) != 0;  // bits 1..: a folded reset's bank row + 1 (k_ego)
   }
   raster8_affine(J.R, rt);
   return J;
@@ -1761,7 +1761,35 @@ void k_raster(KArgs K, uint8_t* __restrict__ recs, int n, uint8_t* __restrict__ 
   const int64_t SS = (int64_t)K.P.size * K.P.size;
   const DRec r = bind_rec(recs + (int64_t)e * K.L.record_bytes, K.L, K.C);
   const RasterJob J = raster_job<false, G>(K, r);
+  // a reset k_ego folded into this step (KArgs::rmask; RS_FAST bits 1.. = its bank
+  // row + 1): this tile of the bank frame into every ring slot but the one this
+  // step renders (FrameStackObservation's reset padding), loaded before the
+  // render and stored after it
+  using TG = Tiles<G>;
+  constexpr int CPR = TG::TC / 16, PPT = TG::TC * TG::TR / 16 / kRasterNT;
+  const int row = K.rbank_frames != nullptr && K.rn_frames > 1 ? (r.hi[CBEV_HI_RS_FAST] >> 1) - 1 : -1;
+  const int ox0 = (t % TG::NTX) * TG::TC, oy0 = (t / TG::NTX) * TG::TR;
+  uint4 fv[PPT];
+  if (row >= 0) {
+#pragma unroll
+    for (int j = 0; j < PPT; ++j) {
+      const int p = threadIdx.x + kRasterNT * j, pr = p / CPR;
+      fv[j] = *(const uint4*)(K.rbank_frames + (int64_t)row * SS + (oy0 + pr) * K.P.size + ox0 + 16 * (p - pr * CPR));
+    }
+  }
   raster_tile<G, true, kRasterNT>(K, r, J, t, frames + e * SS, 1, 0, lds);
+  if (row >= 0) {
+    for (int f = 0; f < K.rn_frames; ++f) {
+      if (f == K.rslot) continue;
+      uint8_t* dst = K.rring + (int64_t)f * K.rring_stride + e * SS;
+#pragma unroll
+      for (int j = 0; j < PPT; ++j) {
+        const int p = threadIdx.x + kRasterNT * j, pr = p / CPR;
+        store16_frame(dst + (oy0 + pr) * K.P.size + ox0 + 16 * (p - pr * CPR),
+                      u32x4_nt{fv[j].x, fv[j].y, fv[j].z, fv[j].w});
+      }
+    }
+  }
   // the step's termination flags, published once k_ego's reset no longer reads the previous ones
   if (K.term_pub != nullptr && t == 0 && threadIdx.x == 0) K.term_pub[e] = K.term_scr[e];
   CBEV_STAMP(2, 3);
@@ -2665,22 +2693,6 @@ __global__ __launch_bounds__(256) void k_ego(uint8_t* __restrict__ recs, int n, 
     rest_v = *(const uint4*)(src(rest_k) + rest_o);
     asm volatile("" ::"v"(rest_v.x), "v"(rest_v.y), "v"(rest_v.z), "v"(rest_v.w));  // issued here, not sunk to S7
   }
-  // and its bank frame into every ring slot but the one this step renders
-  // (FrameStackObservation's reset padding): the first reset env's frame loaded
-  // now (16 bytes x SS / 4096 per thread) and stored at S7, any further ones at S7
-  const int64_t SSf = (int64_t)P_size_sq(K);
-  const int fpt = (int)(SSf / (16 * 256));  // 16-byte pieces per thread of one frame
-  uint4 fr_v[4];
-  const int fr_k = nres > 0 && K.rn_frames > 1 ? nth_set_bit(R.bits, 0) : -1;
-  if (fr_k >= 0 && fpt <= 4) {
-    const uint8_t* fsrc = K.rbank_frames + (int64_t)ego_reset_row(R, fr_k, K.rn_bank) * SSf;
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-      if (j < fpt) fr_v[j] = *(const uint4*)(fsrc + 16 * (threadIdx.x + 256 * j));
-#pragma unroll
-    for (int j = 0; j < 4; ++j)  // issued here, not sunk to S7
-      if (j < fpt) asm volatile("" ::"v"(fr_v[j].x), "v"(fr_v[j].y), "v"(fr_v[j].z), "v"(fr_v[j].w));
-  }
   HeroPre* pre = (HeroPre*)(scr + ne * SL.bytes);  // [ne]
   int* best = (int*)(pre + ne);                   // [ne] target search result
   const int tid = threadIdx.x;
@@ -2816,7 +2828,11 @@ __global__ __launch_bounds__(256) void k_ego(uint8_t* __restrict__ recs, int n, 
     if (wave == 1) {
       hero_env_comfort(rec(lane));
     } else if (wave == 2) {
-      hero_env_render_setup(K, rec(lane));
+      const DRec rr = rec(lane);
+      hero_env_render_setup(K, rr);
+      // a folded reset's bank row for k_raster (the reset frame into the other ring
+      // slots), beside the fast bit it reads anyway: RS_FAST bits 1.. = row + 1
+      if ((R.bits >> lane) & 1ull) rr.hi[CBEV_HI_RS_FAST] |= (ego_reset_row(R, lane, K.rn_bank) + 1) << 1;
     } else if (wave == 3) {  // the updated yaw's cos / sin for the actors' TTCs (S5)
       const double yaw = ((const double*)(lds + lane * pk.bytes + K.L.hd))[CBEV_HD_YAW];
       d_sincos(yaw, &pre[lane].syaw, &pre[lane].cyaw);
@@ -3000,27 +3016,6 @@ __global__ __launch_bounds__(256) void k_ego(uint8_t* __restrict__ recs, int n, 
     int k, o;
     rest_piece(q, &k, &o);
     *(uint4*)(recs + (int64_t)(e0 + k) * rb + o) = *(const uint4*)(src(k) + o);
-  }
-  if (fr_k >= 0) {
-    for (uint64_t m = R.bits; m; m &= m - 1) {
-      const int k = __builtin_ctzll(m);
-      const uint8_t* fsrc = K.rbank_frames + (int64_t)ego_reset_row(R, k, K.rn_bank) * SSf;
-      uint8_t* fdst = K.rring + (int64_t)(e0 + k) * SSf;
-      auto put = [&](int64_t o, const uint4& v) {
-        for (int f = 0; f < K.rn_frames; ++f)
-          if (f != K.rslot) store16_frame(fdst + (int64_t)f * K.rring_stride + o, u32x4_nt{v.x, v.y, v.z, v.w});
-      };
-      if (k == fr_k && fpt <= 4) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          if (j < fpt) put(16 * (int64_t)(threadIdx.x + 256 * j), fr_v[j]);
-      } else {
-        for (int j = 0; j < fpt; ++j) {
-          const int64_t o = 16 * (int64_t)(threadIdx.x + 256 * j);
-          put(o, *(const uint4*)(fsrc + o));
-        }
-      }
-    }
   }
   CBEV_STAMP(1, 3);
 }
