@@ -1745,6 +1745,31 @@ __device__ __forceinline__ void xcd_tile_of_wg(int w, int n, int T, int* e, int*
   *e = 64 * (8 * blk + x) + i;
 }
 
+// A folded reset's bank frame, tile t of it, into the ring slots the step does
+// not render (KArgs::rmask)
+template <int G>
+__device__ __forceinline__ void raster_reset_frame(const KArgs& K, int row, int e, int t) {
+  using TG = Tiles<G>;
+  constexpr int CPR = TG::TC / 16, PPT = TG::TC * TG::TR / 16 / 256;
+  const int64_t SS = (int64_t)K.P.size * K.P.size;
+  const int ox0 = (t % TG::NTX) * TG::TC, oy0 = (t / TG::NTX) * TG::TR;
+  uint4 fv[PPT];
+#pragma unroll
+  for (int j = 0; j < PPT; ++j) {
+    const int p = threadIdx.x + 256 * j, pr = p / CPR;
+    fv[j] = *(const uint4*)(K.rbank_frames + (int64_t)row * SS + (oy0 + pr) * K.P.size + ox0 + 16 * (p - pr * CPR));
+  }
+  for (int f = 0; f < K.rn_frames; ++f) {
+    if (f == K.rslot) continue;
+    uint8_t* dst = K.rring + (int64_t)f * K.rring_stride + e * SS;
+#pragma unroll
+    for (int j = 0; j < PPT; ++j) {
+      const int p = threadIdx.x + 256 * j, pr = p / CPR;
+      store16_frame(dst + (oy0 + pr) * K.P.size + ox0 + 16 * (p - pr * CPR), u32x4_nt{fv[j].x, fv[j].y, fv[j].z, fv[j].w});
+    }
+  }
+}
+
 // One (env, tile) per workgroup; register target from the LDS-limited residency
 // (Tiles::wgs_per_cu workgroups of 4 waves per CU = waves per SIMD). The raster
 // kernels declare no static LDS: the gathers address the LDS absolutely.
@@ -1763,35 +1788,17 @@ void k_raster(KArgs K, uint8_t* __restrict__ recs, int n, uint8_t* __restrict__ 
   const RasterJob J = raster_job<false, G>(K, r);
   // a reset k_ego folded into this step (KArgs::rmask; RS_FAST bits 1.. = its bank
   // row + 1): this tile of the bank frame into every ring slot but the one this
-  // step renders (FrameStackObservation's reset padding), loaded before the
-  // render and stored after it
-  using TG = Tiles<G>;
-  constexpr int CPR = TG::TC / 16, PPT = TG::TC * TG::TR / 16 / kRasterNT;
+  // step renders (FrameStackObservation's reset padding), by the few reset
+  // items only, after the render (loads and stores there: no register is held
+  // across the render for it)
   const int row = K.rbank_frames != nullptr && K.rn_frames > 1 ? (r.hi[CBEV_HI_RS_FAST] >> 1) - 1 : -1;
-  const int ox0 = (t % TG::NTX) * TG::TC, oy0 = (t / TG::NTX) * TG::TR;
-  uint4 fv[PPT];
-  if (row >= 0) {
-#pragma unroll
-    for (int j = 0; j < PPT; ++j) {
-      const int p = threadIdx.x + kRasterNT * j, pr = p / CPR;
-      fv[j] = *(const uint4*)(K.rbank_frames + (int64_t)row * SS + (oy0 + pr) * K.P.size + ox0 + 16 * (p - pr * CPR));
-    }
-  }
+  // the step's termination flags, published once k_ego's reset no longer reads
+  // the previous ones (loaded now, stored after the render)
+  const bool pub = K.term_pub != nullptr && t == 0 && threadIdx.x == 0;
+  const uint8_t tflag = pub ? K.term_scr[e] : 0;
   raster_tile<G, true, kRasterNT>(K, r, J, t, frames + e * SS, 1, 0, lds);
-  if (row >= 0) {
-    for (int f = 0; f < K.rn_frames; ++f) {
-      if (f == K.rslot) continue;
-      uint8_t* dst = K.rring + (int64_t)f * K.rring_stride + e * SS;
-#pragma unroll
-      for (int j = 0; j < PPT; ++j) {
-        const int p = threadIdx.x + kRasterNT * j, pr = p / CPR;
-        store16_frame(dst + (oy0 + pr) * K.P.size + ox0 + 16 * (p - pr * CPR),
-                      u32x4_nt{fv[j].x, fv[j].y, fv[j].z, fv[j].w});
-      }
-    }
-  }
-  // the step's termination flags, published once k_ego's reset no longer reads the previous ones
-  if (K.term_pub != nullptr && t == 0 && threadIdx.x == 0) K.term_pub[e] = K.term_scr[e];
+  if (row >= 0) raster_reset_frame<G>(K, row, e, t);
+  if (pub) K.term_pub[e] = tflag;
   CBEV_STAMP(2, 3);
 }
 
