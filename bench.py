@@ -36,10 +36,10 @@ CONFIGS = {
             seed0=10_000, act_seed=1234, caps=dict(route_cap=64, actor_cap=0, actor_route_cap=2, tl_cap=0),
             workload="ego-only empty scene (rt_no_traffic_v1), 4096 envs/GPU, 128x128 semantic 6-class"),
     3: dict(envs=4096, size=128, obs_mode="bev_rgb", difficulty="rt_hard_v1", action="discrete9_v1",
-            seed0=20_000, act_seed=7, caps=dict(route_cap=64, actor_cap=25, actor_route_cap=64, tl_cap=0),
+            seed0=20_000, act_seed=7, caps=dict(route_cap=64, actor_cap=25, actor_route_cap=288, tl_cap=0),
             workload="random traffic (rt_hard_v1, 25 vehicles), 4096 envs/GPU, 128x128 RGB->gray 4-stack"),
     4: dict(envs=8192, size=128, obs_mode="bev_semantic", difficulty="rt_medium_v1", action="continuous_gsb_v1",
-            seed0=40_000, act_seed=99, caps=dict(route_cap=64, actor_cap=16, actor_route_cap=64, tl_cap=0),
+            seed0=40_000, act_seed=99, caps=dict(route_cap=64, actor_cap=16, actor_route_cap=288, tl_cap=0),
             gather=True, workload="rt_medium_v1, continuous, 8192 envs/GPU, RCCL frame gather to rank 0",
             workload_n1="rt_medium_v1, continuous, 8192 envs/GPU (one shard; no gather at N=1)"),
     5: dict(envs=2048, size=256, obs_mode="bev_semantic", difficulty="mix3", action="discrete9_v1",

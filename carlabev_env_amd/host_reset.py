@@ -65,7 +65,7 @@ class HostResetBuilder:
             raise RuntimeError(f"Failed to reset into a valid initial state after {max_attempts} attempts: {info}")
         # the scene scalars episode_info reports (carlabev.py:180-181), carried by the record
         view.hd[LY.HD["NUM_VEH"]] = float(len(spec.vehicles))
-        view.hd[LY.HD["LEN_ROUTE_M"]] = route_length_m(spec)
+        view.hd[LY.HD["LEN_ROUTE_M"]] = spec.len_route_m if spec.len_route_m is not None else route_length_m(spec)
         ctx = dict(spec.context)
         for k in ("scene", "level", "difficulty_id"):
             if options.get(k) is not None:

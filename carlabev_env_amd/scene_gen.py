@@ -6,17 +6,21 @@ What is restated from the reference, same RNG streams and draw order:
   jaywalk scenario sampler             src/scenes/scenarios/jaywalk.py:28-117
   scenario level draw                  src/managers/scene_generator.py:170-182
 
-What is synthetic (and why): the reference's random-traffic routes and the
-red-light-runner routes are shortest paths on lane graphs that ship only as
-Python pickles (`assets/Town01/*.pkl`, loaded with `pickle.load` at
-`src/planning/map_graph.py:13-19`). Unpickling reference files is not allowed
-here, so `RoadGrid` plans routes on the drivable pixels of the Town01 class
-map instead: a grid of road-centre cells (cells whose distance to the road edge
-exceeds a margin), breadth-first shortest paths from a seeded set of source
-cells, waypoints every `cell` px. Routes are in 128-surface coordinates for
-every map size, as in the reference (`scene_generator.py:71-75,334`). Ego route
-length ranges, vehicle counts and the rule that a background vehicle needs >5
-route points follow `scene_generator.py:196-344`.
+  random traffic (ego route, vehicles)  src/managers/scene_generator.py:196-344,
+                                       src/scenes/utils.py:74-211
+  route profile metrics                src/control/route_profile.py:55-182
+  red_light_runner sampler             src/scenes/scenarios/red_light_running.py:13-245
+The routes are planned on the reference's Town01 lane graphs (lane_graph.py,
+JSON extracted from `assets/Town01/*.pkl` without unpickling), so a seeded
+reset draws the reference's scene; tests/test_lane_graph.py pins the scenes
+against tests/golden/scenes_graph.json (the reference's own generator on the
+same graphs and seeds).
+
+One deliberate deviation: for S != 128 the scenario samplers get anchors that
+are drivable on the size-S map (`scenario_anchors`), since the reference's
+literal S=256 semantics (128-scale positions on the 256 map) spawn the ego off
+the road; the red-light runner is then placed on synthetic straight routes
+through the anchor.
 
 The generator produces `SceneSpec`s; `scene_pack.pack_scene` turns them into
 device records. Step parity is defined on realised scenes (the record), which
@@ -32,12 +36,10 @@ from dataclasses import dataclass
 
 import numpy as np
 
-from scipy import ndimage
-from scipy.sparse import csr_matrix
-from scipy.sparse.csgraph import shortest_path
-
+from . import lane_graph
 from .authored import load_authored_scene, normalize_scenario_config, read_scene_file, scenario_options_from_config
 from .params import load_class_map
+from .routes import smooth_and_compute
 from .scene_pack import ActorSpec, SceneSpec, TrafficLightSpec
 
 _SEED_MODULUS = 2 ** 31 - 1
@@ -82,107 +84,9 @@ def _rng_state(g: np.random.Generator) -> dict:
     return g.bit_generator.state
 
 
-class RoadGrid:
-    """Road-centre cell graph over the 128-scale Town01 class map."""
-
-    def __init__(self, map_name: str = "Town01", size: int = 128, cell: int = 4, margin: float = 6.0,
-                 stride: int = 3, n_sources: int = 128, seed: int = 12345):
-        # routes live in 128-surface coordinates for every map size (scene_generator.py:71-75), so
-        # plan on the part of the size-S map those coordinates cover (the whole map at S=128)
-        classes = window_128(load_class_map(map_name, size))
-        self.h, self.w = classes.shape
-        drivable = classes == 1
-        dist = ndimage.distance_transform_edt(drivable)
-        self.cell = cell
-        self.stride = stride  # waypoint every stride*cell px (12.5 px lane-graph spacing in the reference)
-        gh, gw = self.h // cell, self.w // cell
-        cy = (np.arange(gh) * cell + cell // 2)
-        cx = (np.arange(gw) * cell + cell // 2)
-        ok = dist[np.ix_(cy, cx)] >= margin
-        ids = -np.ones((gh, gw), dtype=np.int64)
-        nodes = np.argwhere(ok)
-        ids[ok] = np.arange(len(nodes))
-        self.node_xy = np.stack([cx[nodes[:, 1]], cy[nodes[:, 0]]], axis=1).astype(float)
-        rows, cols = [], []
-        for dy, dx in ((0, 1), (1, 0)):
-            a = ids[: gh - dy, : gw - dx]
-            b = ids[dy:, dx:]
-            m = (a >= 0) & (b >= 0)
-            rows += [a[m], b[m]]
-            cols += [b[m], a[m]]
-        r = np.concatenate(rows)
-        c = np.concatenate(cols)
-        n = len(nodes)
-        self.graph = csr_matrix((np.ones(len(r)), (r, c)), shape=(n, n))
-        # keep the largest connected component only
-        from scipy.sparse.csgraph import connected_components
-        _, lab = connected_components(self.graph, directed=False)
-        big = np.bincount(lab).argmax()
-        self.valid = np.flatnonzero(lab == big)
-        rng = np.random.default_rng(seed)
-        self.sources = rng.choice(self.valid, size=min(n_sources, len(self.valid)), replace=False)
-        d, pred = shortest_path(self.graph, directed=False, unweighted=True, indices=self.sources,
-                                return_predecessors=True)
-        self.dist = d
-        self.pred = pred
-
-    def path(self, si: int, target: int) -> np.ndarray:
-        """Waypoints (surface px) of the BFS path from source index si to node target."""
-        out = []
-        node = int(target)
-        src = int(self.sources[si])
-        while node != src and node >= 0:
-            out.append(node)
-            node = int(self.pred[si, node])
-        out.append(src)
-        nodes = out[::-1]
-        keep = nodes[::self.stride]
-        if keep[-1] != nodes[-1]:
-            keep.append(nodes[-1])
-        return self.node_xy[np.array(keep)]
-
-    def route_in_range(self, rng: random.Random, min_m: float, max_m: float, max_attempts: int = 100):
-        """Random ego route whose length is within [min_m, max_m] meters
-        (find_route_in_range, scenes/utils.py:125-211)."""
-        for _ in range(max_attempts):
-            si = rng.randrange(len(self.sources))
-            d = self.dist[si]
-            lo = min_m / MPP / self.cell
-            hi = max_m / MPP / self.cell
-            cand = np.flatnonzero((d >= lo) & (d <= hi))
-            if len(cand) == 0:
-                continue
-            target = int(cand[rng.randrange(len(cand))])
-            pts = self.path(si, target)
-            length = float(np.sum(np.hypot(np.diff(pts[:, 0]), np.diff(pts[:, 1])))) * MPP
-            if min_m <= length <= max_m and len(pts) >= 2:
-                return pts
-        return None
-
-    def random_route(self, rng: random.Random, min_points: int = 6, max_points: int = 48):
-        si = rng.randrange(len(self.sources))
-        d = self.dist[si]
-        hops = self.stride
-        cand = np.flatnonzero(np.isfinite(d) & (d >= (min_points - 1) * hops) & (d <= (max_points - 2) * hops))
-        if len(cand) == 0:
-            return None
-        target = int(cand[rng.randrange(len(cand))])
-        return self.path(si, target)
-
-
-_GRIDS: dict = {}
-
-
 def window_128(classes: np.ndarray) -> np.ndarray:
     """The region of a size-S class map addressed by 128-surface coordinates."""
     return classes[:1280, :1024]
-
-
-def road_grid(map_name: str = "Town01", size: int = 128) -> RoadGrid:
-    key = (map_name, size)
-    if key not in _GRIDS:
-        _GRIDS[key] = RoadGrid(map_name, size)
-    return _GRIDS[key]
 
 
 def _all_drivable(ii, y0, y1, x0, x1) -> bool:
@@ -216,43 +120,219 @@ def _m2s(m: float) -> float:
     return float(m) / MPP
 
 
+def route_length_meters(rx, ry) -> float:
+    """envs/geometry.py:61-69 (segment lengths summed in order, then scaled)."""
+    if len(rx) != len(ry):
+        raise ValueError("Route coordinates mismatch.")
+    total = 0.0
+    for i in range(1, len(rx)):
+        total += np.hypot(float(rx[i]) - float(rx[i - 1]), float(ry[i]) - float(ry[i - 1]))
+    return float(total) * MPP
+
+
+_STRAIGHT = {"straight_fraction": 1.0, "left_turn_fraction": 0.0, "right_turn_fraction": 0.0, "turn_count": 0,
+             "has_left_turn": False, "has_right_turn": False, "intersection_like": False,
+             "route_profile": "mostly_straight"}
+
+
+def route_profile_metrics(ax, ay, turn_rate_thresh: float = 0.12, min_turn_segment_m: float = 4.0) -> dict:
+    """compute_route_profile_metrics (control/route_profile.py:55-159): turn
+    labels from the heading rate of the smoothed route, turn segments of at least
+    `min_turn_segment_m`, and the profile label they make."""
+    cx, cy, cyaw, _, _ = smooth_and_compute(ax, ay, window=11, poly=3)
+    cx, cy = np.asarray(cx, dtype=float), np.asarray(cy, dtype=float)
+    cyaw = np.unwrap(np.asarray(cyaw, dtype=float))
+    if cx.size < 2 or cy.size < 2 or cyaw.size < 2:
+        return dict(_STRAIGHT)
+    ds = np.hypot(np.diff(cx), np.diff(cy)) * MPP
+    valid = ds > 1e-6
+    if not np.any(valid):
+        return dict(_STRAIGHT)
+    dth = (np.diff(cyaw) + np.pi) % (2.0 * np.pi) - np.pi
+    ds_v, rate = ds[valid], dth[valid] / ds[valid]
+    labels = np.where(rate > turn_rate_thresh, 1, np.where(rate < -turn_rate_thresh, -1, 0))
+    total = float(ds_v.sum())
+    if total <= 1e-9:
+        return dict(_STRAIGHT)
+    # _normalize_turn_segments (route_profile.py:21-52): runs of one turn sign
+    segs, sign_c, length = [], 0, 0.0
+    for sign, seg in zip(labels, ds_v):
+        sign = int(sign)
+        if sign != sign_c or sign == 0:
+            if sign_c != 0 and length >= min_turn_segment_m:
+                segs.append(sign_c)
+            sign_c, length = sign, (float(seg) if sign != 0 else 0.0)
+        else:
+            length += float(seg)
+    if sign_c != 0 and length >= min_turn_segment_m:
+        segs.append(sign_c)
+    straight = float(ds_v[labels == 0].sum()) / total
+    left = float(ds_v[labels == 1].sum()) / total
+    right = float(ds_v[labels == -1].sum()) / total
+    turns = len(segs)
+    has_l, has_r = any(g > 0 for g in segs), any(g < 0 for g in segs)
+    if turns == 0 or straight >= 0.9:
+        prof = "mostly_straight"
+    elif turns == 1 and left >= right:
+        prof = "single_left"
+    elif turns == 1 and right > left:
+        prof = "single_right"
+    elif turns >= 2:
+        prof = "multi_turn"
+    else:
+        prof = "mixed"
+    return {"straight_fraction": straight, "left_turn_fraction": left, "right_turn_fraction": right,
+            "turn_count": turns, "has_left_turn": has_l, "has_right_turn": has_r,
+            "intersection_like": turns >= 2 or (has_l and has_r), "route_profile": prof}
+
+
+def matches_route_profile(m: dict, route_profile=None, min_turns=None, max_turns=None,
+                          intersection_required=None) -> bool:
+    """control/route_profile.py:162-182."""
+    if route_profile is not None and route_profile != "any" and m.get("route_profile") != route_profile:
+        return False
+    turns = int(m.get("turn_count", 0))
+    if min_turns is not None and turns < min_turns:
+        return False
+    if max_turns is not None and turns > max_turns:
+        return False
+    inter = bool(m.get("intersection_like", False))
+    if intersection_required is True and not inter:
+        return False
+    if intersection_required is False and inter:
+        return False
+    return True
+
+
+# generate_random's ego graph choice (scene_generator.py:254-270): planner, node class
+EGO_ROUTE_GRAPHS = {"full_vehicle": ("vehicle-full", "vehicle"), "right_lane": ("vehicle-R", "R"),
+                    "left_lane": ("vehicle-L", "L")}
+
+
 class SceneGenerator:
     """build_scene(options, rng_bundle) -> SceneSpec (scene_generator.py:95-191)."""
+
+    # RedLightRunningScenario.intersections, (y, x) raw (red_light_running.py:23-40)
+    INTERSECTIONS_RAW = [(8642, 1564), (8654, 6755), (7250, 1552), (7241, 2446), (7242, 3652), (7242, 4704),
+                         (7257, 6773), (6199, 1552), (6197, 2439), (3349, 1545), (3350, 2456), (3350, 3639),
+                         (3335, 4714), (3315, 6773), (2456, 1563), (2446, 6757)]
 
     def __init__(self, cfg=None, map_name: str = "Town01"):
         self.cfg = cfg
         self.map_name = map_name
         self.size = int(getattr(cfg, "size", 128)) if cfg is not None else 128
-        self.grid = road_grid(map_name, self.size)
+        self.planners = lane_graph.planners(map_name)
         self._anchors = scenario_anchors(map_name, self.size) if self.size != 128 else None
         self.max_vehicles = getattr(cfg, "max_vehicles", 25) if cfg is not None else 25
         self.traffic_enabled = getattr(cfg, "traffic_enabled", True) if cfg is not None else True
+        self._red_light_routes: dict = {}
 
     # ------------------------------------------------------------ random traffic
+    def route_in_range(self, rng: random.Random, planner_key: str, node_cls: str, min_m: float, max_m: float,
+                       route_profile=None, min_turns=None, max_turns=None, intersection_required=None,
+                       max_attempts: int = 100):
+        """find_route_in_range with an explicit planner (scenes/utils.py:125-211):
+        random start/end nodes of `node_cls`, the planner's merged shortest path,
+        waypoints path[1:] in surface px; accepted when its length is within
+        [min_m, max_m] m and its profile matches. -> (rx, ry, length_m, metrics) | None"""
+        g = self.planners[planner_key]
+        for _ in range(max_attempts):
+            start = g.random_node(node_cls, rng)
+            end = g.random_node(node_cls, rng)
+            if start == end:
+                continue
+            path, _ = g.find_path(start, end)
+            if not path or len(path) < 2:
+                continue
+            rx, ry = [], []
+            for n in path[1:]:
+                x, y = g.node_pos_surface(n)
+                rx.append(x)
+                ry.append(y)
+            length = route_length_meters(rx, ry)
+            if min_m <= length <= max_m:
+                metrics = route_profile_metrics(rx, ry)
+                if not matches_route_profile(metrics, route_profile, min_turns, max_turns, intersection_required):
+                    continue
+                return rx, ry, length, metrics
+        return None
+
+    def actor_route(self, lane: str, rng: random.Random):
+        """get_actor("vehicle", lane) + find_route (scene_generator.py:330-344,
+        scenes/utils.py:74-101): two random nodes of the lane's own graph, the
+        interior nodes of the merged path between them; None unless > 5 points."""
+        g = self.planners[f"vehicle-{lane}"]
+        start = g.random_node(lane, rng)
+        end = g.random_node(lane, rng)
+        path, _ = g.find_path(start, end)
+        rx, ry = [], []
+        for n in path[1:-1]:
+            x, y = g.node_pos_surface(n)
+            rx.append(x)
+            ry.append(y)
+        return (rx, ry) if len(rx) > 5 else None
+
     def generate_random(self, num_cars, dist_range, bundle: RNGBundle, traffic_enabled=True, ego_target_speed=12.0,
-                        max_retries=20) -> SceneSpec:
+                        max_retries=20, route_profile=None, route_profile_mix=None, min_turns=None, max_turns=None,
+                        intersection_required=None, ego_route_graph="full_vehicle") -> SceneSpec:
+        """SceneGenerator.generate_random (scene_generator.py:196-327)."""
         num_cars = num_cars if traffic_enabled else 0
-        pts = None
+        ego_target_speed = float(ego_target_speed)
+        ctx = {"scene": "rdm", "scenario_param_num_vehicles": int(num_cars),
+               "scenario_param_route_dist_range": list(dist_range),
+               "scenario_param_ego_route_graph": str(ego_route_graph)}
+        profile = route_profile
+        if route_profile_mix:
+            labels = list(route_profile_mix.keys())
+            weights = [float(route_profile_mix[k]) for k in labels]
+            if any(w < 0.0 for w in weights):
+                raise ValueError(f"route_profile_mix must use non-negative weights: {route_profile_mix}")
+            if sum(weights) <= 0.0:
+                raise ValueError(f"route_profile_mix must contain at least one positive weight: {route_profile_mix}")
+            profile = bundle.route_rng.choices(labels, weights=weights, k=1)[0]
+            ctx["scenario_param_route_profile_mix"] = dict(route_profile_mix)
+        if profile is not None:
+            ctx["scenario_param_requested_route_profile"] = profile
+        if min_turns is not None:
+            ctx["scenario_param_min_turns"] = int(min_turns)
+        if max_turns is not None:
+            ctx["scenario_param_max_turns"] = int(max_turns)
+        if intersection_required is not None:
+            ctx["scenario_param_intersection_required"] = bool(intersection_required)
+        if max_retries is not None:
+            ctx["scenario_param_max_route_attempts"] = int(max_retries)
+        if ego_route_graph not in EGO_ROUTE_GRAPHS:
+            raise ValueError(f"Unsupported ego_route_graph={ego_route_graph!r}. "
+                             "Expected one of: full_vehicle, right_lane, left_lane.")
+        key, node_cls = EGO_ROUTE_GRAPHS[ego_route_graph]
+        found = None
         for _ in range(max_retries):
-            pts = self.grid.route_in_range(bundle.route_rng, float(dist_range[0]), float(dist_range[1]))
-            if pts is not None and len(pts) > 1:
+            found = self.route_in_range(bundle.route_rng, key, node_cls, dist_range[0], dist_range[1], profile,
+                                        min_turns, max_turns, intersection_required)
+            if found is not None and len(found[0]) > 1:
                 break
-        if pts is None:
+            found = None
+        if found is None:
             raise RuntimeError(f"Failed to generate a valid ego route in range {dist_range} after {max_retries} "
                                "attempts.")
+        rx, ry, length, m = found
+        ctx.update({"route_profile": m["route_profile"], "route_turn_count": int(m["turn_count"]),
+                    "route_intersection_like": bool(m["intersection_like"]), "route_length_m": float(length),
+                    "route_left_turn_fraction": float(m["left_turn_fraction"]),
+                    "route_right_turn_fraction": float(m["right_turn_fraction"]),
+                    "route_straight_fraction": float(m["straight_fraction"])})
         vehicles = []
         for _ in range(num_cars):
-            _lane = bundle.traffic_rng.choice(["L", "R"])
-            vp = self.grid.random_route(bundle.traffic_rng)
-            if vp is None or len(vp) <= 5:
-                continue
-            vehicles.append(ActorSpec("vehicle", list(vp[:, 0]), list(vp[:, 1]), 12.0))
-        spec = SceneSpec(list(pts[:, 0]), list(pts[:, 1]), 0.0, float(ego_target_speed), vehicles=vehicles,
-                         hero_jitter_seed=None, actor_jitter_seed=None)
+            lane = bundle.traffic_rng.choice(["L", "R"])
+            route = self.actor_route(lane, bundle.traffic_rng)
+            if route is not None:
+                vehicles.append(ActorSpec("vehicle", route[0], route[1], 12.0))
+        spec = SceneSpec(rx, ry, 0.0, ego_target_speed, vehicles=vehicles, hero_jitter_seed=None,
+                         actor_jitter_seed=None)
         spec.hero_rng_state = _rng_state(bundle.route_np_rng)
         spec.actor_rng_state = _rng_state(bundle.traffic_np_rng)
-        spec.context = {"scene": "rdm", "scenario_param_num_vehicles": int(num_cars),
-                        "scenario_param_route_dist_range": list(dist_range)}
+        spec.context = ctx
+        spec.len_route_m = float(length)
         return spec
 
     # ------------------------------------------------------------ lead_brake
@@ -323,24 +403,106 @@ class SceneGenerator:
                                       rear_speed, None))
         return SceneSpec(ego_rx, ego_ry, ego_speed, ego_speed, vehicles=vehicles, pedestrians=peds)
 
-    # ------------------------------------------------------------ red light runner (synthetic geometry)
-    INTERSECTIONS_RAW = [(8642, 1564), (8654, 6755), (7250, 1552), (7241, 2446), (7242, 3652), (7242, 4704),
-                         (7257, 6773), (6199, 1552), (6197, 2439), (3349, 1545), (3350, 2456), (3350, 3639),
-                         (3335, 4714), (3315, 6773), (2456, 1563), (2446, 6757)]
+    # ------------------------------------------------------------ red light runner
+    @staticmethod
+    def _direction_key(dx: float, dy: float) -> str:
+        if abs(dx) > abs(dy):
+            return "east" if dx > 0 else "west"
+        return "south" if dy > 0 else "north"
+
+    def _intersection_graph(self):
+        return self.planners["vehicle"]  # the 2-lane graph (red_light_running.py:42-45)
+
+    def _select_intersection(self, index=None, anchor_x=None, anchor_y=None) -> np.ndarray:
+        """_select_intersection (red_light_running.py:74-107): the first candidate
+        (nearest the requested intersection / anchor, else list order) whose
+        1200-unit neighbourhood has lane nodes in all four directions."""
+        raw = [np.array([float(x), float(y)]) for y, x in self.INTERSECTIONS_RAW]
+        if index is not None:
+            if not 0 <= int(index) < len(raw):
+                raise IndexError(f"intersection_index {int(index)} out of range for red_light_runner.")
+            ref = raw[int(index)]
+            order = [i for _, i in sorted((np.linalg.norm(c - ref), i) for i, c in enumerate(raw))]
+        elif anchor_x is not None and anchor_y is not None:
+            ref = np.array([anchor_x * 8.0, anchor_y * 8.0], dtype=float)
+            order = [i for _, i in sorted((np.linalg.norm(c - ref), i) for i, c in enumerate(raw))]
+        else:
+            order = list(range(len(raw)))
+        g = self._intersection_graph()
+        pos = np.array([np.asarray(p, dtype=float) for p in g.pos])
+        for i in order:
+            counts = {"north": 0, "south": 0, "east": 0, "west": 0}
+            for p in pos:
+                d = p - raw[i]
+                if np.linalg.norm(d) >= 1200.0:
+                    continue
+                counts[self._direction_key(d[0], d[1])] += 1
+            if all(counts[k] > 0 for k in ("north", "south", "east", "west")):
+                return raw[i]
+        raise RuntimeError("No valid 4-way intersection candidate found for red_light_runner.")
+
+    def _straight_route(self, center: np.ndarray, start_dir: str, end_dir: str):
+        """_sample_straight_route (red_light_running.py:109-161): the best-scored
+        start/end lane nodes (distance near 950 units, small lateral offset) whose
+        shortest path passes within 180 units of the centre and has >= 6 nodes;
+        the route is the path's raw positions / 8."""
+        g = self._intersection_graph()
+
+        def candidates(direction):
+            out = []
+            for n, p in zip(g.ids, g.pos):
+                p = np.asarray(p, dtype=float)
+                d = p - center
+                dist = np.linalg.norm(d)
+                if not 150.0 <= dist <= 1500.0 or self._direction_key(d[0], d[1]) != direction:
+                    continue
+                lateral = abs(d[0]) if direction in ("north", "south") else abs(d[1])
+                out.append((abs(dist - 950.0) + 0.2 * lateral, n))
+            out.sort(key=lambda item: item[0])
+            return [n for _, n in out[:25]]
+
+        ends = candidates(end_dir)
+        for s in candidates(start_dir):
+            for t in ends:
+                try:
+                    path = g.shortest_path(s, t)
+                except lane_graph.NoPath:
+                    continue
+                coords = [np.asarray(g.pos[g.index[n]], dtype=float) for n in path]
+                if min(np.linalg.norm(c - center) for c in coords) > 180.0 or len(coords) < 6:
+                    continue
+                return [float(c[0]) / 8.0 for c in coords], [float(c[1]) / 8.0 for c in coords]
+        raise RuntimeError(f"Unable to build a valid {start_dir}->{end_dir} route through the selected 4-way "
+                           "intersection.")
 
     def red_light_runner(self, level: int, g: np.random.Generator, kw: dict) -> SceneSpec:
-        """Ego drives south->north through a 4-way intersection on green while an
-        adversary crosses west->east on red (red_light_running.py:201-245). The
-        intersection list is the reference's; routes are straight lines through
-        its centre sampled every 12.5 px instead of lane-graph paths."""
-        idx = kw.get("intersection_index")
-        if idx is None:
-            idx = int(g.integers(0, len(self.INTERSECTIONS_RAW)))
-        if "center" in kw:
-            cx, cy = (float(v) for v in kw["center"])
-        else:
-            ry_raw, rx_raw = self.INTERSECTIONS_RAW[int(idx)]
-            cx, cy = rx_raw / 8.0, ry_raw / 8.0
+        """RedLightRunningScenario.sample (red_light_running.py:195-245): the ego
+        drives south->north through a 4-way intersection on green while an
+        adversary crosses west->east on red. Nothing in it is random: the routes
+        depend on the selected intersection only, and are cached per centre."""
+        if "center" in kw:  # S != 128 anchor (module docstring): synthetic straight routes
+            return self._red_light_synthetic(kw)
+        center = self._select_intersection(kw.get("intersection_index"), kw.get("anchor_x"), kw.get("anchor_y"))
+        key = (float(center[0]), float(center[1]))
+        if key not in self._red_light_routes:
+            self._red_light_routes[key] = (self._straight_route(center, "south", "north"),
+                                           self._straight_route(center, "west", "east"))
+        (ego_rx, ego_ry), (adv_rx, adv_ry) = self._red_light_routes[key]
+        ego_speed = kw.get("ego_speed", 10.0)
+        adv_speed = kw.get("adv_speed", 16.0)
+        cx, cy = float(center[0]) / 8.0, float(center[1]) / 8.0
+        off, length, width = _m2s(4.0), _m2s(8.0), _m2s(0.45) + 1.0
+        tls = [TrafficLightSpec(cx, cy + off, "horizontal", "green", width, length),
+               TrafficLightSpec(cx - off, cy, "vertical", "red", width, length)]
+        spec = SceneSpec(list(ego_rx), list(ego_ry), ego_speed, ego_speed,
+                         vehicles=[ActorSpec("vehicle", list(adv_rx), list(adv_ry), adv_speed, None)],
+                         traffic_lights=tls)
+        spec.len_route_m = route_length_meters(ego_rx, ego_ry)
+        return spec
+
+    def _red_light_synthetic(self, kw: dict) -> SceneSpec:
+        """The S != 128 stand-in: straight 20-point routes through the anchor."""
+        cx, cy = (float(v) for v in kw["center"])
         span = 950.0 / 8.0
         n = 20
         ego_ry = list(np.linspace(cy + span, cy - span, n))
@@ -349,9 +511,7 @@ class SceneGenerator:
         adv_ry = [cy + _m2s(1.75)] * n
         ego_speed = kw.get("ego_speed", 10.0)
         adv_speed = kw.get("adv_speed", 16.0)
-        off = _m2s(4.0)
-        length = _m2s(8.0)
-        width = _m2s(0.45) + 1.0
+        off, length, width = _m2s(4.0), _m2s(8.0), _m2s(0.45) + 1.0
         tls = [TrafficLightSpec(cx, cy + off, "horizontal", "green", width, length),
                TrafficLightSpec(cx - off, cy, "vertical", "red", width, length)]
         return SceneSpec(ego_rx, ego_ry, ego_speed, ego_speed,
@@ -377,15 +537,22 @@ class SceneGenerator:
             sub = scenario_options_from_config(normalize_scenario_config(data), options)
             return self.build_scene(sub, bundle)
         if scene == "rdm":
-            spec = self.generate_random(
+            attempts = options.get("max_route_attempts")
+            target = options.get("ego_target_speed")
+            return self.generate_random(
                 options.get("num_vehicles", self.max_vehicles),
                 options.get("route_dist_range", [30, 100]),
                 bundle,
                 traffic_enabled=options.get("traffic_enabled", self.traffic_enabled),
-                ego_target_speed=options.get("ego_target_speed", 12.0) or 12.0,
-                max_retries=int(options.get("max_route_attempts") or 20),
+                ego_target_speed=12.0 if target is None else target,
+                max_retries=20 if attempts is None else int(attempts),
+                route_profile=options.get("route_profile"),
+                route_profile_mix=options.get("route_profile_mix"),
+                min_turns=options.get("min_turns"),
+                max_turns=options.get("max_turns"),
+                intersection_required=options.get("intersection_required"),
+                ego_route_graph=options.get("ego_route_graph", "full_vehicle"),
             )
-            return spec
         if scene in ("lead_brake", "jaywalk", "red_light_runner"):
             level = options.get("level")
             if level is None:

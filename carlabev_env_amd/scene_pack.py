@@ -77,6 +77,7 @@ class SceneSpec:
     hero_rng_state: dict | None = None      # or the exact generator state to draw the jitter from
     actor_rng_state: dict | None = None
     context: dict = field(default_factory=dict)
+    len_route_m: float | None = None        # the len_route build_scene returns, when the sampler reports one
 
     def caps_needed(self):
         n_route = len(self.agent_rx)

@@ -40,7 +40,7 @@ from . import obs_pipeline as OP
 from .fov_mask import fov_corner_mask
 from .spaces import batch_space, make_box, make_discrete
 
-DEFAULT_CAPS = dict(route_cap=128, actor_cap=32, actor_route_cap=64, tl_cap=4)
+DEFAULT_CAPS = dict(route_cap=128, actor_cap=32, actor_route_cap=288, tl_cap=4)
 
 
 def _ptr(t: torch.Tensor | None):

@@ -9,7 +9,7 @@ from carlabev_env_amd.host_reset import HostResetBuilder
 from carlabev_env_amd.params import build_params, load_class_map, padded_map
 from carlabev_env_amd.scene_gen import SceneGenerator
 
-CAPS_FULL = LY.Caps(128, 32, 64, 4)
+CAPS_FULL = LY.Caps(128, 32, 288, 4)
 
 
 def bench_caps(config: int) -> LY.Caps:

@@ -452,7 +452,7 @@ def test_profile_raster_rerenders_the_step():
         assert np.array_equal(got, want), size
 
 
-CAPS_WIDE = LY.Caps(128, 96, 128, 4)
+CAPS_WIDE = LY.Caps(128, 96, 288, 4)
 
 
 def test_parity_wide_actor_kernel():

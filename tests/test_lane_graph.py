@@ -1,0 +1,101 @@
+"""Lane-graph planning and planned scenes against the reference's own planners.
+
+Fixture: tests/golden/scenes_graph.json, written by
+tests/golden/make_golden_scenes.py, which ran the reference's MapGraph /
+GraphPlanner / SceneGenerator / RedLightRunningScenario (networkx 3.4.2) on the
+graphs tools/convert_graphs.py extracted from assets/Town01/*.pkl:
+  - node classes of every planner           map_graph.py:21-43
+  - 200 seeded shortest paths + merged paths graph_planner.py:92-116
+  - 52 seeded random-traffic scenes          scene_generator.py:95-327 (all rt_* presets,
+    right/left-lane ego graphs, a route profile and an intersection/turn filter)
+  - 5 red-light-runner scenes                red_light_running.py:74-245
+Everything is compared exactly (the planner's arithmetic is raw/8 and the
+same float sums in the same order), including how far each RNG stream was
+advanced.
+"""
+from __future__ import annotations
+
+import json
+import os
+
+import numpy as np
+import pytest
+
+from carlabev_env_amd import lane_graph
+from carlabev_env_amd.scene_gen import SceneGenerator, build_rng_bundle
+
+GOLD = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "scenes_graph.json")))
+
+
+@pytest.fixture(scope="module")
+def gen():
+    return SceneGenerator(None)
+
+
+def test_node_classes_match_reference():
+    graphs = lane_graph.planners("Town01")
+    by_file = {stem: graphs[key] for key, stem in lane_graph.PLANNER_FILES.items()}
+    for stem, classes in GOLD["node_classes"].items():
+        assert by_file[stem].nodes == classes, stem
+
+
+def test_shortest_and_merged_paths_match_reference():
+    graphs = lane_graph.planners("Town01")
+    by_file = {stem: graphs[key] for key, stem in lane_graph.PLANNER_FILES.items()}
+    n_nopath = 0
+    for case in GOLD["paths"]:
+        g = by_file[case["graph"]]
+        if case["path"] is None:
+            n_nopath += 1
+            with pytest.raises(lane_graph.NoPath):
+                g.shortest_path(case["source"], case["target"])
+        else:
+            assert g.shortest_path(case["source"], case["target"]) == case["path"], case
+        merged, coords = g.find_path(case["source"], case["target"])
+        assert merged == case["merged"]
+        assert [[float(v) for v in c] for c in coords] == case["coords"]
+    assert n_nopath < len(GOLD["paths"])
+
+
+def test_random_traffic_scenes_match_reference(gen):
+    for case in GOLD["random"]:
+        bundle = build_rng_bundle(scene_seed=case["seed"])
+        spec = gen.build_scene(dict(case["options"]), bundle)
+        ag = case["agent"]
+        assert [float(v) for v in spec.agent_rx] == ag["rx"] and [float(v) for v in spec.agent_ry] == ag["ry"]
+        assert spec.initial_speed_mps == ag["speed"] and spec.target_speed_mps == ag["target_speed"]
+        assert spec.len_route_m == case["len_route"]
+        assert len(spec.vehicles) == len(case["vehicles"])
+        for a, ref in zip(spec.vehicles, case["vehicles"]):
+            assert [float(v) for v in a.rx] == ref["rx"] and [float(v) for v in a.ry] == ref["ry"]
+            assert a.speed_mps == ref["cruise_mps"]
+        for k, v in case["context"].items():
+            assert spec.context.get(k) == v, (case["seed"], k)
+        # every RNG stream advanced exactly as far as the reference's
+        assert bundle.route_rng.random() == case["route_rng_next"]
+        assert bundle.traffic_rng.random() == case["traffic_rng_next"]
+        assert float(bundle.traffic_np_rng.random()) == case["traffic_np_next"]
+
+
+def test_red_light_runner_matches_reference(gen):
+    for case in GOLD["red_light"]:
+        spec = gen.red_light_runner(1, np.random.default_rng(0), dict(case["kwargs"]))
+        ag, adv = case["agent"], case["adversary"]
+        assert spec.agent_rx == ag["rx"] and spec.agent_ry == ag["ry"]
+        assert spec.initial_speed_mps == ag["speed"] and spec.target_speed_mps == ag["target_speed"]
+        assert spec.len_route_m == case["len_route"]
+        (v,) = spec.vehicles
+        assert v.rx == adv["rx"] and v.ry == adv["ry"] and v.speed_mps == adv["cruise_mps"]
+        state = {"red": 0, "yellow": 1, "green": 2}
+        got = [{"x": t.x, "y": t.y, "orientation": t.orientation, "state": state[t.state], "width": t.width,
+                "length": t.length} for t in spec.traffic_lights]
+        assert got == case["traffic_light"]
+
+
+def test_shortest_path_edge_cases():
+    g = lane_graph.planners("Town01")["vehicle-R"]
+    n0 = g.ids[5]
+    assert g.shortest_path(n0, n0) == [n0]
+    assert g.find_path(n0, n0)[0] == [n0]
+    with pytest.raises(KeyError):
+        g.shortest_path("no-such-node", n0)

@@ -8,7 +8,7 @@ import numpy as np
 from carlabev_env_amd.config import EnvConfig
 from carlabev_env_amd.scene_pool import ScenePool, make_builder, scene_options
 
-CAPS = dict(route_cap=64, actor_cap=20, actor_route_cap=64, tl_cap=4)
+CAPS = dict(route_cap=64, actor_cap=20, actor_route_cap=288, tl_cap=4)
 
 
 def test_pool_records_match_in_process_builder():
