@@ -1236,6 +1236,10 @@ __host__ __device__ constexpr int tile_cols(int S) { return S < 128 ? S : 128; }
 // window -> map-load chain, which at S = 256 reads a 9.2 MB byte map from
 // beyond the L2, fewer times)
 __host__ __device__ constexpr int tile_rows(int S) { return S <= 64 ? 64 : 128; }
+// traffic lights that miss a tile's window skip their paint and barrier
+#ifndef CBEV_TL_SKIP
+#define CBEV_TL_SKIP 0
+#endif
 template <int G>
 struct Tiles {
   static constexpr int S = 64 * G;
@@ -1492,6 +1496,17 @@ __device__ __forceinline__ void paint_tile(const KArgs& K, const DRec& r, const 
     const int rw = r.ti[CBEV_TI_RW * r.T + t], rh = r.ti[CBEV_TI_RH * r.T + t];
     const uint8_t col = (uint8_t)r.ti[CBEV_TI_COLOR * r.T + t];
     const int ru = W.tr ? ry : rx, rv = W.tr ? rx : ry, su = W.tr ? rh : rw, sv = W.tr ? rw : rh;
+#if CBEV_TL_SKIP
+    // the light's rect clipped to the crop and to this tile's window; a light
+    // that misses the window (most lights at S = 256, where an env has 4 tiles)
+    // paints nothing and needs no barrier (the test is uniform: every thread
+    // reads the same ints)
+    const int u0 = max(max(ru, 0), -W.ou), u1 = min(min(ru + su, C), -W.ou + 16 * W.nc);
+    const int v0 = max(max(rv, 0), W.v0), v1 = min(min(rv + sv, C), W.v0 + W.nv);
+    if (u0 >= u1 || v0 >= v1) continue;
+    for (int pv = v0 + (int)(threadIdx.x >> 4); pv < v1; pv += NT / 16)
+      for (int pu = u0 + (int)(threadIdx.x & 15); pu < u1; pu += 16) lds[(pv - W.v0) * W.sb + W.ou + pu] = col;
+#else
     for (int qv = threadIdx.x >> 4; qv < sv; qv += NT / 16)
       for (int qu = threadIdx.x & 15; qu < su; qu += 16) {
         const int pu = ru + qu, pv = rv + qv;
@@ -1499,6 +1514,7 @@ __device__ __forceinline__ void paint_tile(const KArgs& K, const DRec& r, const 
             pv < W.v0 + W.nv)
           lds[(pv - W.v0) * W.sb + W.ou + pu] = col;
       }
+#endif
     lds_barrier();
   }
 }

@@ -246,7 +246,7 @@ class SceneGenerator:
                 continue
             rx, ry = [], []
             for n in path[1:]:
-                x, y = g.node_pos_surface(n)
+                x, y = g.node_xy_surface(n)
                 rx.append(x)
                 ry.append(y)
             length = route_length_meters(rx, ry)
@@ -267,7 +267,7 @@ class SceneGenerator:
         path, _ = g.find_path(start, end)
         rx, ry = [], []
         for n in path[1:-1]:
-            x, y = g.node_pos_surface(n)
+            x, y = g.node_xy_surface(n)
             rx.append(x)
             ry.append(y)
         return (rx, ry) if len(rx) > 5 else None

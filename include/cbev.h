@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define CBEV_ABI_VERSION 5
+#define CBEV_ABI_VERSION 6
 
 typedef struct cbev_ctx cbev_ctx;
 

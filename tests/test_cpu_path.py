@@ -22,7 +22,7 @@ def test_library_loads_and_exports_every_symbol():
     L = _lib.lib()
     for name in _lib.EXPORTED_SYMBOLS:
         assert hasattr(L, name), name
-    assert L.cbev_abi_version() == 5
+    assert L.cbev_abi_version() == 6
     assert L.cbev_params_size() == ctypes.sizeof(CbevParams)
 
 
