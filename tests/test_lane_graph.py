@@ -99,3 +99,30 @@ def test_shortest_path_edge_cases():
     assert g.find_path(n0, n0)[0] == [n0]
     with pytest.raises(KeyError):
         g.shortest_path("no-such-node", n0)
+
+
+def test_route_profile_metrics_reference_cases():
+    """The reference's own route-profile tests (tests/test_route_profile.py:33-54)."""
+    from carlabev_env_amd.scene_gen import matches_route_profile, route_profile_metrics
+    m = route_profile_metrics([0, 10, 20, 30, 40, 50], [0, 0, 0, 0, 0, 0])
+    assert m["route_profile"] == "mostly_straight" and m["turn_count"] == 0 and m["straight_fraction"] > 0.99
+    assert matches_route_profile(m, route_profile="mostly_straight")
+    assert not matches_route_profile(m, route_profile="single_left")
+    m = route_profile_metrics([0, 10, 20, 20, 20, 30, 40], [0, 0, 0, 10, 20, 20, 20])
+    assert m["turn_count"] >= 1 and m["route_profile"] in {"single_left", "multi_turn", "mixed"}
+    assert matches_route_profile(m, min_turns=1)
+
+
+def test_route_profile_mix_draws_from_the_route_stream(gen):
+    """A route_profile_mix picks the requested profile with route_rng.choices
+    (scene_generator.py:79-93,229-234) before the ego route is searched."""
+    import random
+    opts = {"scene": "rdm", "num_vehicles": 0, "route_dist_range": [30, 130],
+            "route_profile_mix": {"mostly_straight": 0.0, "single_right": 1.0}}
+    spec = gen.build_scene(dict(opts), build_rng_bundle(scene_seed=77))
+    assert spec.context["scenario_param_requested_route_profile"] == "single_right"
+    assert spec.context["route_profile"] == "single_right"
+    r = random.Random(build_rng_bundle(scene_seed=77).route_seed)
+    assert r.choices(["mostly_straight", "single_right"], weights=[0.0, 1.0], k=1)[0] == "single_right"
+    with pytest.raises(ValueError):
+        gen.build_scene(dict(opts, route_profile_mix={"mostly_straight": -1.0}), build_rng_bundle(scene_seed=1))
