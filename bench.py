@@ -576,7 +576,7 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f64 state / u8 frames",
-            "data": "synthetic seeded scenes (host scene-gen on the Town01 class map), seeded action streams",
+            "data": "synthetic seeded scenes (the reference's scene generator restated on its Town01 lane graphs), seeded action streams",
             "info_mode": args.info_mode,
             "reset": ("folded into the next step's k_ego (cbev_set_deferred_reset)"
                       if bool(lib().cbev_reset_pending is not None) and not args.no_defer_reset

@@ -114,3 +114,4 @@ EXPORTED_SYMBOLS = ("cbev_abi_version", "cbev_params_size", "cbev_layout_of", "c
 
 ERR_ACTION_INDEX = 1  # CBEV_ERR_ACTION_INDEX (include/cbev.h)
 ERR_RASTER_WINDOW = 2  # CBEV_ERR_RASTER_WINDOW (include/cbev.h)
+ERR_RETREAT_ROUTE = 4  # CBEV_ERR_RETREAT_ROUTE (include/cbev.h)

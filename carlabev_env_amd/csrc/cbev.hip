@@ -227,8 +227,9 @@ __device__ __forceinline__ double lane_value(double v, int k) {
   return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
 }
 
-// d_start_retreat by the whole wave for actor a when its route fits the lanes
-// (RA <= 64: lane i holds route point i). Every per-point expression of
+// d_start_retreat by the whole wave for actor a when its rebuilt route fits the
+// lanes (at most 64 points: lane i holds route point i; returns false, touching
+// nothing, for a longer one). Every per-point expression of
 // d_smooth_route is evaluated as there, one point per lane; the two serial sums
 // (arc lengths, np.unwrap corrections) are accumulated in index order through
 // shuffles and the target search reduces the same candidates, so the result is
@@ -241,7 +242,7 @@ __device__ __forceinline__ void wave_mem_fence() { __builtin_amdgcn_fence(__ATOM
 // Takes the record base and the byte offsets of the groups it touches as plain
 // ints: a DRec (or KArgs) reference makes every k_actors wave spill that struct
 // to scratch at launch (12 KB per wave), retreat or not.
-__device__ __noinline__ void wave_start_retreat(uint8_t* base, int o_ad, int o_ai, int o_aix, int o_aiy, int o_arx,
+__device__ __noinline__ bool wave_start_retreat(uint8_t* base, int o_ad, int o_ai, int o_aix, int o_aiy, int o_arx,
                                                 int o_ary, int o_acx, int o_acy, int o_acyaw, int o_acf, int A, int RA,
                                                 int a, int lane) {
   wave_mem_fence();  // the owner lane's behaviour stores come first
@@ -263,6 +264,7 @@ __device__ __noinline__ void wave_start_retreat(uint8_t* base, int o_ad, int o_a
   if (cur < 0) cur = 0;
   int n = cur + 2;
   if (n > RA) n = RA;
+  if (n > 64) return false;  // uniform: every lane read the same fields
   const double* ix = r.aix + (int64_t)a * RA;
   const double* iy = r.aiy + (int64_t)a * RA;
   // raw route [pos] + initial_route[:cur + 1][::-1] (jaywalk.py:43-54)
@@ -413,6 +415,7 @@ __device__ __noinline__ void wave_start_retreat(uint8_t* base, int o_ad, int o_a
     d_bset(r, a, CBEV_BST_RETREATING, RAD(r, CBEV_AD_CRUISE_MPS, a));
   }
   wave_mem_fence();  // the other lanes read these record fields next
+  return true;
 }
 
 // Behaviour.apply (lead_brake.py:10-15, jaywalk.py:56-138). DEFER: a due
@@ -1075,12 +1078,14 @@ __device__ __forceinline__ int actor_search(const DRec& r, int nact, uint64_t li
   return best;
 }
 
-// WIDE: the context's capacities allow more than 64 actors or more than 64
-// actor route points, which take the serial per-lane paths (d_actor_step,
-// d_start_retreat). Contexts within 64 / 64 launch k_actors<false>, which
-// compiles without them: 134 instead of 246 VGPRs, 3 waves per SIMD instead of 2
-// (asking for 4 waves per SIMD, amdgpu_waves_per_eu(4), still leaves 130 VGPRs
-// and spills 12).
+// WIDE: the context's capacity allows more than 64 actors, which take the
+// serial per-lane path (d_actor_step). Contexts within 64 actor slots launch
+// k_actors<false>, which compiles without it: 134 instead of 246 VGPRs, 3 waves
+// per SIMD instead of 2 (asking for 4 waves per SIMD, amdgpu_waves_per_eu(4),
+// still leaves 130 VGPRs and spills 12). Both rebuild a StopReturn retreat with
+// the whole wave (wave_start_retreat: at most 64 points, which scene_pack
+// guarantees); a serial rebuild compiled into the narrow kernel would take it
+// from 134 to 200 VGPRs.
 template <bool WIDE>
 __global__ __launch_bounds__(256) void k_actors(KArgs K, uint8_t* __restrict__ recs, int n) {
   const int lane = threadIdx.x & 63;
@@ -1124,17 +1129,20 @@ __global__ __launch_bounds__(256) void k_actors(KArgs K, uint8_t* __restrict__ r
     // behaviours; a due retreat rebuilds the actor's route with the whole wave
     const bool retreat = beh != CBEV_BEH_NONE && d_behavior<true>(r, a, t);
     uint64_t rm = __ballot(retreat);
-    if (rm) {
-      if (RA <= 64) {
-        while (rm) {
-          const int k = __builtin_ctzll(rm);
-          rm &= rm - 1;
-          wave_start_retreat(recs + (int64_t)e * K.L.record_bytes, (int)K.L.ad, (int)K.L.ai, (int)K.L.aix,
-                             (int)K.L.aiy, (int)K.L.arx, (int)K.L.ary, (int)K.L.acx, (int)K.L.acy,
-                             (int)K.L.acyaw, (int)K.L.acf, r.A, RA, k, lane);
+    while (rm) {
+      const int k = __builtin_ctzll(rm);
+      rm &= rm - 1;
+      uint8_t* base = recs + (int64_t)e * K.L.record_bytes;
+      if (!wave_start_retreat(base, (int)K.L.ad, (int)K.L.ai, (int)K.L.aix, (int)K.L.aiy, (int)K.L.arx, (int)K.L.ary,
+                              (int)K.L.acx, (int)K.L.acy, (int)K.L.acyaw, (int)K.L.acf, r.A, RA, k, lane)) {
+        // a rebuilt route of more than 64 points: scene_pack refuses such actors
+        // (a StopReturn route of at most 63 points); a record written otherwise
+        // is rebuilt serially by the wide kernel, flagged by the narrow one
+        if (WIDE) {
+          if (lane == k) d_start_retreat(r, k);
+        } else if (lane == k) {
+          atomicOr(K.err, CBEV_ERR_RETREAT_ROUTE);
         }
-      } else if (WIDE) {
-        if (retreat) d_start_retreat(r, a);
         wave_mem_fence();
       }
     }
@@ -1236,10 +1244,6 @@ __host__ __device__ constexpr int tile_cols(int S) { return S < 128 ? S : 128; }
 // window -> map-load chain, which at S = 256 reads a 9.2 MB byte map from
 // beyond the L2, fewer times)
 __host__ __device__ constexpr int tile_rows(int S) { return S <= 64 ? 64 : 128; }
-// traffic lights that miss a tile's window skip their paint and barrier
-#ifndef CBEV_TL_SKIP
-#define CBEV_TL_SKIP 0
-#endif
 template <int G>
 struct Tiles {
   static constexpr int S = 64 * G;
@@ -1496,7 +1500,6 @@ __device__ __forceinline__ void paint_tile(const KArgs& K, const DRec& r, const 
     const int rw = r.ti[CBEV_TI_RW * r.T + t], rh = r.ti[CBEV_TI_RH * r.T + t];
     const uint8_t col = (uint8_t)r.ti[CBEV_TI_COLOR * r.T + t];
     const int ru = W.tr ? ry : rx, rv = W.tr ? rx : ry, su = W.tr ? rh : rw, sv = W.tr ? rw : rh;
-#if CBEV_TL_SKIP
     // the light's rect clipped to the crop and to this tile's window; a light
     // that misses the window (most lights at S = 256, where an env has 4 tiles)
     // paints nothing and needs no barrier (the test is uniform: every thread
@@ -1506,15 +1509,6 @@ __device__ __forceinline__ void paint_tile(const KArgs& K, const DRec& r, const 
     if (u0 >= u1 || v0 >= v1) continue;
     for (int pv = v0 + (int)(threadIdx.x >> 4); pv < v1; pv += NT / 16)
       for (int pu = u0 + (int)(threadIdx.x & 15); pu < u1; pu += 16) lds[(pv - W.v0) * W.sb + W.ou + pu] = col;
-#else
-    for (int qv = threadIdx.x >> 4; qv < sv; qv += NT / 16)
-      for (int qu = threadIdx.x & 15; qu < su; qu += 16) {
-        const int pu = ru + qu, pv = rv + qv;
-        if (pu >= 0 && pv >= 0 && pu < C && pv < C && pu >= -W.ou && pu < -W.ou + 16 * W.nc && pv >= W.v0 &&
-            pv < W.v0 + W.nv)
-          lds[(pv - W.v0) * W.sb + W.ou + pu] = col;
-      }
-#endif
     lds_barrier();
   }
 }
@@ -3529,7 +3523,7 @@ static KArgs kargs(const cbev_ctx* c) {
 
 typedef void (*ActorsKernel)(KArgs, uint8_t*, int);
 static ActorsKernel actors_kernel(const cbev_caps& C) {
-  return (C.actor_cap > 64 || C.actor_route_cap > 64) ? k_actors<true> : k_actors<false>;
+  return C.actor_cap > 64 ? k_actors<true> : k_actors<false>;
 }
 static const void* raster_kernel(int size) {
   return size == 64 ? (const void*)k_raster<1> : size == 128 ? (const void*)k_raster<2> : (const void*)k_raster<4>;

@@ -124,11 +124,12 @@ def init_actor_slot(view: LY.RecordView, a: int, spec: ActorSpec, np_rng, map_si
     if n > ra or len(rx) > ra:
         raise ValueError(f"actor route of {max(n, len(rx))} points exceeds actor_route_cap={ra}")
     beh, p0, p1 = behavior_fields(spec.behavior)
-    if beh == LY.BEH["yield_return"] and len(rx) + 1 > ra:
+    if beh == LY.BEH["yield_return"] and len(rx) + 1 > min(ra, 64):
         # a StopReturn retreat rebuilds the route as [pos] + initial_route[:idx + 1][::-1]
-        # (jaywalk.py:43-54): up to len(rx) + 1 points, which must fit the slot
-        raise ValueError(f"yield_return actor route of {len(rx)} points leaves no room for its retreat route "
-                         f"({len(rx) + 1} points) within actor_route_cap={ra}")
+        # (jaywalk.py:43-54): up to len(rx) + 1 points, which must fit the slot and the
+        # device's wave-wide rebuild (one point per lane: at most 64)
+        raise ValueError(f"yield_return actor route of {len(rx)} points: its retreat route ({len(rx) + 1} points) "
+                         f"must fit actor_route_cap={ra} and 64 points")
     ad, ai = view.ad, view.ai
     ad[LY.AD["X"], a], ad[LY.AD["Y"], a], ad[LY.AD["YAW"], a], ad[LY.AD["V"], a] = ci.x, ci.y, ci.yaw, ci.v
     ad[LY.AD["CT_SPEED"], a] = cruise            # Controller(self.target_speed)

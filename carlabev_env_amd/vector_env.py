@@ -620,7 +620,9 @@ class CarlaBEVVectorEnv:
         device): ERR_ACTION_INDEX (1) = a device action tensor held a discrete index outside
         [-n, n), the reference's IndexError; that env stepped action 0.
         ERR_RASTER_WINDOW (2) = a raster tile's crop window exceeded its LDS bound
-        (an internal invariant the GPU parity tests assert; that frame is not valid)."""
+        (an internal invariant the GPU parity tests assert; that frame is not valid).
+        ERR_RETREAT_ROUTE (4) = a StopReturn actor's retreat route would exceed 64
+        points (records not written by scene_pack, which refuses such actors)."""
         flags = ctypes.c_int32()
         check(lib().cbev_error_flags(self._ctx, ctypes.byref(flags), 1 if clear else 0), "cbev_error_flags")
         return int(flags.value)

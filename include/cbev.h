@@ -96,6 +96,11 @@ int cbev_termination_count(cbev_ctx* ctx, int64_t* count);
 /*   CBEV_ERR_RASTER_WINDOW a raster tile's crop window exceeded its LDS bound
  *                          (an internal invariant; the frame is not valid). */
 #define CBEV_ERR_RASTER_WINDOW 2
+/*   CBEV_ERR_RETREAT_ROUTE a StopReturn retreat would rebuild a route of more
+ *                          than 64 points in a context of at most 64 actor
+ *                          slots (scene packing refuses such actors; that actor
+ *                          keeps its route) */
+#define CBEV_ERR_RETREAT_ROUTE 4
 int cbev_error_flags(cbev_ctx* ctx, int32_t* flags_host, int clear);
 
 /* Reset the envs selected by mask (uint8[n], NULL = all):

@@ -154,3 +154,22 @@ def test_create_refuses_records_k_ego_cannot_stage():
     ctx = ctypes.c_void_p()
     rc = L.cbev_create(ctypes.byref(P), ctypes.byref(LY.Caps(4096, 0, 2, 0).c()), 0, ctypes.byref(ctx))
     assert rc == -1 and b"k_ego" in L.cbev_last_error()
+
+
+def test_pack_refuses_retreat_routes_beyond_the_wave_rebuild():
+    """A StopReturn (yield_return) actor's retreat route ([pos] + initial_route[:idx+1][::-1],
+    jaywalk.py:43-54) is rebuilt by one wave, one point per lane: scene_pack refuses
+    initial routes whose retreat could exceed 64 points, whatever actor_route_cap is."""
+    from carlabev_env_amd.scene_pack import ActorSpec, SceneSpec, pack_scene
+    layout = LY.Layout.make(CAPS_FULL)
+    assert CAPS_FULL.actor_route_cap > 64
+    beh = {"type": "yield_return", "params": {"start_delay": 0.5, "yield_duration": 1.0}}
+    for n, ok in ((63, True), (64, False)):
+        ped = ActorSpec("pedestrian", [300.0 + 0.5 * i for i in range(n)], [400.0] * n, 1.6, beh)
+        spec = SceneSpec([500.0, 500.0, 500.0], [700.0, 690.0, 680.0], 0.0, 12.0, pedestrians=[ped])
+        buf = np.zeros(layout.record_bytes, np.uint8)
+        if ok:
+            pack_scene(LY.RecordView(buf, layout), spec, 128)
+        else:
+            with pytest.raises(ValueError, match="64 points"):
+                pack_scene(LY.RecordView(buf, layout), spec, 128)

@@ -456,11 +456,10 @@ CAPS_WIDE = LY.Caps(128, 96, 288, 4)
 
 
 def test_parity_wide_actor_kernel():
-    """k_actors<true>: capacities above 64 actors / 64 route points select the wide kernel.
-    More than 64 vehicles take the per-lane d_actor_step path; jaywalk scenes with a
-    128-point actor route capacity rebuild a retreating pedestrian's route on one lane
-    (serial d_start_retreat) instead of the wave-wide rebuild (stanley_controller.py:100-123,
-    behavior/jaywalk.py:43-54)."""
+    """k_actors<true>: more than 64 actor slots select the wide kernel. More than 64
+    vehicles take the per-lane d_actor_step path (stanley_controller.py:100-123); jaywalk
+    scenes in the wide kernel rebuild a retreating pedestrian's route with the whole wave,
+    as the narrow kernel does (behavior/jaywalk.py:43-54), with a 288-point route capacity."""
     many = dict(build_random_navigation_options(RandomNavigationReset(difficulty_id="rt_hard_v1")), num_vehicles=72)
     run_parity(None, 6, 40, seed0=50_000, caps=CAPS_WIDE, options=[many])
     run_parity(["jaywalk"], 24, 80, seed0=30_000, caps=CAPS_WIDE)

@@ -77,6 +77,11 @@ def main():
         print(f"{name}: {used.sum()} WGs; cycles mean phase1 {d[:, 0].mean():.0f} (max {d[:, 0].max():.0f})  phase2 {d[:, 1].mean():.0f} "
               f"(max {d[:, 1].max():.0f})  phase3 {d[:, 2].mean():.0f}; WG total mean {(st[:, 3] - st[:, 0]).mean():.0f}; "
               )
+        tot = st[:, 3] - st[:, 0]
+        ends = (rt[:, 3] - rt[:, 0].min()) / 100
+        print(f"   WG cycles p10/p50/p90/p99/max {np.percentile(tot, [10, 50, 90, 99]).round().tolist()} {tot.max()}; "
+              f"end time (us after the first start) p50 {np.percentile(ends, 50):.2f} p90 {np.percentile(ends, 90):.2f} "
+              f"p99 {np.percentile(ends, 99):.2f} max {ends.max():.2f}")
         idx = np.flatnonzero(used)
         xs = xcc[k][used] & 0xF
         print(f"   XCC id: workgroups with xcc == w % 8: {(xs == (idx % 8)).mean() * 100:.1f}%; first 16: {list(xs[:16])}")
