@@ -123,6 +123,20 @@ class Layout:
         return Layout(caps, off, _align(o, 256), vis_words)
 
 
+def check_library_layout(L, caps: Caps) -> "Layout":
+    """This header's layout for `caps`, refused unless the loaded library (L, the
+    ctypes handle) computes the same one: a library built from another version of
+    include/cbev_layout.h would read records of a different shape."""
+    py = Layout.make(caps)
+    out = CbevLayout()
+    rc = L.cbev_layout_of(ctypes.byref(caps.c()), ctypes.byref(out))
+    bad = [n for n, o in py.off.items() if getattr(out, n) != o]
+    if rc != 0 or bad or out.record_bytes != py.record_bytes or out.vis_words != py.vis_words:
+        raise RuntimeError(f"the loaded libcbev.so lays records out differently from {HEADER} "
+                           f"({', '.join(bad) or 'record_bytes'}): rebuild it (python -m carlabev_env_amd.build)")
+    return py
+
+
 class RecordView:
     """Named numpy views into one record (a writable uint8 buffer)."""
 

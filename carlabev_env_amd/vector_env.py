@@ -163,9 +163,9 @@ class CarlaBEVVectorEnv:
         c["actor_cap"] = max(c["actor_cap"], int(self.cfg.max_vehicles) + 4)
         c.update(caps or {})
         self.caps = LY.Caps(**c)
-        self.layout = LY.Layout.make(self.caps)
-        self.rb = self.layout.record_bytes
         L = lib()
+        self.layout = LY.check_library_layout(L, self.caps)
+        self.rb = self.layout.record_bytes
         ctx = ctypes.c_void_p()
         check(L.cbev_create(ctypes.byref(self.params), ctypes.byref(self.caps.c()), self.device.index or 0,
                             ctypes.byref(ctx)), "cbev_create")

@@ -173,3 +173,20 @@ def test_pack_refuses_retreat_routes_beyond_the_wave_rebuild():
         else:
             with pytest.raises(ValueError, match="64 points"):
                 pack_scene(LY.RecordView(buf, layout), spec, 128)
+
+
+def test_library_layout_check_refuses_a_mismatch():
+    """check_library_layout: the header's layout when the library agrees; a refusal
+    naming the groups when a library computes another (a stale build)."""
+    L = _lib.lib()
+    lay = LY.check_library_layout(L, CAPS_FULL)
+    assert lay.record_bytes == LY.Layout.make(CAPS_FULL).record_bytes
+
+    class Shifted:  # a library whose actor groups sit 64 bytes later
+        @staticmethod
+        def cbev_layout_of(c, out):
+            rc = L.cbev_layout_of(c, out)
+            out._obj.ai += 64
+            return rc
+    with pytest.raises(RuntimeError, match="ai"):
+        LY.check_library_layout(Shifted, CAPS_FULL)

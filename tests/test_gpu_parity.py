@@ -35,6 +35,7 @@ def ptr(t):
 class DevWorld:
     def __init__(self, P, padded, caps):
         L = lib()
+        LY.check_library_layout(L, caps)  # records are packed with the header's layout
         self.ctx = P_()
         check(L.cbev_create(ctypes.byref(P), ctypes.byref(caps.c()), 0, ctypes.byref(self.ctx)), "create")
         check(L.cbev_set_map(self.ctx, padded.ctypes.data_as(P_), padded.nbytes), "set_map")
@@ -81,6 +82,10 @@ def compare_records(a: np.ndarray, b: np.ndarray, layout, tag=""):
         # pass) follows every rebuild of the smoothed route
         assert np.array_equal(va.acf[a, :m, 0], va.acx[a, :m].astype(np.float32)), (tag, "acf x", a)
         assert np.array_equal(va.acf[a, :m, 1], va.acy[a, :m].astype(np.float32)), (tag, "acf y", a)
+        # and its longest segment (the search's chunk pruning bound, AD SEGMAX)
+        if m > 1:
+            seg = np.hypot(np.diff(va.acx[a, :m]), np.diff(va.acy[a, :m])).max()
+            assert np.isclose(va.ad[LY.AD["SEGMAX"], a], seg, rtol=1e-12, atol=1e-12), (tag, "segmax", a)
 
 
 def info_of(v, cause):
