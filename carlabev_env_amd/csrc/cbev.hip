@@ -192,13 +192,10 @@ __device__ __noinline__ void d_start_retreat(DRec& r, int a) {
   const double* cy = r.acy + (int64_t)a * RA;
   const double* cyaw = r.acyaw + (int64_t)a * RA;
   float* cf = r.acf + 2 * (int64_t)a * RA;  // the search's float32 copy follows the route
-  double segmax = 0.0;                      // and its longest segment (the search's pruning)
   for (int i = 0; i < m; ++i) {
     cf[2 * i] = (float)cx[i];
     cf[2 * i + 1] = (float)cy[i];
-    if (i > 0) segmax = fmax(segmax, hypot(cx[i] - cx[i - 1], cy[i] - cy[i - 1]));
   }
-  RAD(r, CBEV_AD_SEGMAX, a) = segmax;
   double v0 = RAD(r, CBEV_AD_V, a);
   RAD(r, CBEV_AD_X, a) = cx[0];
   RAD(r, CBEV_AD_Y, a) = cy[0];
@@ -385,10 +382,6 @@ __device__ __noinline__ bool wave_start_retreat(uint8_t* base, int o_ad, int o_a
     cf[0] = (float)cxv;
     cf[1] = (float)cyv;
   }
-  // the rebuilt route's longest segment (the target search's pruning bound)
-  double segm = (lane > 0 && lane < nd) ? hypot(cxv - pcx, cyv - pcy) : 0.0;
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) segm = fmax(segm, __shfl_xor(segm, off, 64));
   // ---- Actor.set_route_surface / Controller.set_route(jitter_start=False): pose at the
   // smoothed start, target index from there (calc_target_index), heading cyaw[idx]
   const int m = nd;
@@ -419,7 +412,6 @@ __device__ __noinline__ bool wave_start_retreat(uint8_t* base, int o_ad, int o_a
     RAD(r, CBEV_AD_Y, a) = y0;
     RAI(r, CBEV_AI_TIDX, a) = tidx;
     RAD(r, CBEV_AD_YAW, a) = yaw_new;
-    RAD(r, CBEV_AD_SEGMAX, a) = segm;
     d_bset(r, a, CBEV_BST_RETREATING, RAD(r, CBEV_AD_CRUISE_MPS, a));
   }
   wave_mem_fence();  // the other lanes read these record fields next
@@ -955,25 +947,17 @@ __device__ __forceinline__ void hero_env_render_setup(const KArgs& K, DRec r) {
 // More than 64 actors: d_actor_step per lane.
 // calc_target_index of every live actor of one env (nact <= 64): AW lanes per
 // actor, 64 / AW actors per round; returns lane a's result for actor a
-// The points of an actor's route are taken in chunks of ACTOR_CH consecutive
-// points, chunk k by lane k % AW of the actor's group. Routes of more than
-// 2 ACTOR_CH points are pruned first (pass 0): one sample per chunk (its middle
-// point, clamped to the route), the group's smallest sample distance D, and a
-// chunk is scanned only if its sample's distance minus its farthest point's
-// index offset times the route's longest segment (AD SEGMAX, the smoothed
-// route's, kept with it by scene packing and both retreat rebuilds) is within
-// reach of D: by the triangle inequality along the route, every point of a
-// skipped chunk lies farther than D + 3 eps (+ float32 margins) from the front
-// axle, so it is never a candidate of pass 1 (whose minimum is at most D).
-// Lanes owning more than ACTOR_QMAX chunks (very long routes at many actors)
-// skip the pruning and scan every chunk.
-constexpr bool kActorF32 = true;  // the float32 first pass (false: the float64 scan alone, tools/micro/actor_f64_only.patch)
-constexpr int ACTOR_CH = 8;       // route points per chunk (loaded at once)
-constexpr int ACTOR_QMAX = 16;    // chunks per lane the pruning pass holds
-constexpr int ACTOR_BATCH64 = 8;  // route points per lane loaded at once in the float64 rescan
+// the float32 first pass (false: the float64 scan alone, tools/micro/actor_f64_only.patch)
+constexpr bool kActorF32 = true;
+// route points per lane loaded at once: 24 in the float32 pass (the lane-graph
+// routes of round 5 have 124 points at the median; 8: 47.7 us at config 3, 16:
+// 44.8, 24: 42.0, 32 spills the residency to 2 waves per SIMD), 8 in the rare
+// float64 rescan
+constexpr int ACTOR_BATCH = 24;
+constexpr int ACTOR_BATCH64 = 8;
 template <int AW>
 __device__ __forceinline__ int actor_search(const DRec& r, int nact, uint64_t livem, double fx, double fy, int nrt,
-                                            double segmax, int lane) {
+                                            int lane) {
   constexpr int AG = 64 / AW;
   const int RA = r.RA;
   const int g = lane / AW, sub = lane - g * AW;
@@ -982,67 +966,38 @@ __device__ __forceinline__ int actor_search(const DRec& r, int nact, uint64_t li
     const int aa = r0 + g;  // this group's actor
     const double gfx = __shfl(fx, aa & 63), gfy = __shfl(fy, aa & 63);
     const int gn = __shfl(nrt, aa & 63);
-    const float gseg = (float)__shfl(segmax, aa & 63);
     const bool glive = aa < nact && ((livem >> (aa & 63)) & 1ull);
     const double* cx = r.acx + (int64_t)(aa & 63) * RA;
     const double* cy = r.acy + (int64_t)(aa & 63) * RA;
-    const float2* cf = (const float2*)r.acf + (int64_t)(aa & 63) * RA;
-    const float ffx = (float)gfx, ffy = (float)gfy;
-    const int nch = (gn + ACTOR_CH - 1) / ACTOR_CH;
-    const int nq = sub < nch ? (nch - sub + AW - 1) / AW : 0;  // this lane's chunks: sub, sub + AW, ...
-    // pass 0: the chunks this lane scans (bit q: chunk sub + q AW)
-    uint64_t keep = nq >= 64 ? ~0ull : ((1ull << nq) - 1ull);
-    const bool prune = kActorF32 && gn > 2 * ACTOR_CH;  // uniform within the group
-    if (glive && prune && nq <= ACTOR_QMAX) {
-      float dk[ACTOR_QMAX];
-#pragma unroll
-      for (int q = 0; q < ACTOR_QMAX; ++q) {  // every sample's load first (index clamped: no branch around a load)
-        const int k = sub + q * AW, c = min(ACTOR_CH * k + ACTOR_CH / 2, gn - 1);
-        const float2 p = cf[q < nq ? c : 0];
-        const float dx = ffx - p.x, dy = ffy - p.y;
-        dk[q] = q < nq ? dx * dx + dy * dy : INFINITY;
-      }
-      float dmin = INFINITY;
-#pragma unroll
-      for (int q = 0; q < ACTOR_QMAX; ++q) dmin = dk[q] < dmin ? dk[q] : dmin;
-#pragma unroll
-      for (int off = AW / 2; off > 0; off >>= 1) {
-        const float o = __shfl_xor(dmin, off, 64);
-        dmin = o < dmin ? o : dmin;
-      }
-      const float reach = sqrtf(dmin) + 0.15f + 0.1f;  // pass 1's 3 eps + float32 margins
-      keep = 0;
-#pragma unroll
-      for (int q = 0; q < ACTOR_QMAX; ++q) {
-        const int k = sub + q * AW, c = min(ACTOR_CH * k + ACTOR_CH / 2, gn - 1);
-        const int h = max(c - ACTOR_CH * k, min(ACTOR_CH * k + ACTOR_CH - 1, gn - 1) - c);  // farthest index offset
-        if (q < nq && sqrtf(dk[q]) - (float)h * gseg <= reach) keep |= 1ull << q;
-      }
-    }
     // pass 1: the smallest squared distance (first index) and the runner-up's,
     // exactly as a serial float64 scan finds them -- from the float32 copy of
-    // the route first (8 instead of 16 bytes a point). Each lane keeps its three
+    // the route first (8 instead of 16 bytes a point: the search is bound by
+    // the route bytes, 105 MB per launch at config 3). Each lane keeps its three
     // smallest float32 distances; the float64 scan then runs over the points
     // within 3 eps of the group's float32 minimum distance only: |d_f32 - d| <=
     // eps = 0.05 px for coordinates below 4096 px (float32 rounding of both
     // points and of the squares, about 2e-3 px), so the exact arg-min is among
     // them, and every other point lies more than eps beyond it (its squared
     // distance exceeds the (1 + 1e-14) tolerance of pass 2: the runner-up test
-    // is unchanged). A lane with three or more such points scans its chunks'
-    // points in float64.
+    // is unchanged). A lane with three or more such points scans all its points
+    // in float64.
     double m2 = INFINITY, s2 = INFINITY;
     int i2 = 0x7fffffff;
     float f1 = INFINITY, f2 = INFINITY, f3 = INFINITY;
     int j1 = -1, j2 = -1;
     if (glive && kActorF32) {
-      for (uint64_t kq = keep; kq; kq &= kq - 1) {
-        const int i0 = ACTOR_CH * (sub + __builtin_ctzll(kq) * AW);
-        float2 p[ACTOR_CH];
+      const float2* cf = (const float2*)r.acf + (int64_t)(aa & 63) * RA;
+      const float ffx = (float)gfx, ffy = (float)gfy;
+      for (int i0 = sub; i0 < gn; i0 += ACTOR_BATCH * AW) {
+        float2 p[ACTOR_BATCH];
 #pragma unroll
-        for (int u = 0; u < ACTOR_CH; ++u) p[u] = cf[min(i0 + u, gn - 1)];
+        for (int u = 0; u < ACTOR_BATCH; ++u) {
+          const int i = i0 + u * AW;
+          p[u] = cf[i < gn ? i : gn - 1];
+        }
 #pragma unroll
-        for (int u = 0; u < ACTOR_CH; ++u) {
-          const int i = i0 + u;
+        for (int u = 0; u < ACTOR_BATCH; ++u) {
+          const int i = i0 + u * AW;
           const float dx = ffx - p[u].x, dy = ffy - p[u].y;
           const float d = i < gn ? dx * dx + dy * dy : INFINITY;
           const bool l1 = d < f1, l2 = d < f2;
@@ -1069,19 +1024,18 @@ __device__ __forceinline__ int actor_search(const DRec& r, int nact, uint64_t li
       m2 = lt ? d2 : m2;
       i2 = lt ? i : i2;
     };
-    if (glive && (!kActorF32 || f3 <= thr)) {  // three or more candidates in this lane: the float64 scan of its chunks
-      for (uint64_t kq = keep; kq; kq &= kq - 1) {
-        const int i0 = ACTOR_CH * (sub + __builtin_ctzll(kq) * AW);
+    if (glive && (!kActorF32 || f3 <= thr)) {  // three or more candidates in this lane: the float64 scan
+      for (int i0 = sub; i0 < gn; i0 += ACTOR_BATCH64 * AW) {
         double px[ACTOR_BATCH64], py[ACTOR_BATCH64];
 #pragma unroll
         for (int u = 0; u < ACTOR_BATCH64; ++u) {
-          const int ic = min(i0 + u, gn - 1);
+          const int i = i0 + u * AW, ic = i < gn ? i : gn - 1;
           px[u] = cx[ic];
           py[u] = cy[ic];
         }
 #pragma unroll
         for (int u = 0; u < ACTOR_BATCH64; ++u) {
-          const int i = i0 + u;
+          const int i = i0 + u * AW;
           const double dx = gfx - px[u], dy = gfy - py[u];
           const double d2 = i < gn ? dx * dx + dy * dy : INFINITY;
           const bool lt = d2 < m2;  // serial order: if (d2 < m2) {...} else if (d2 < s2) s2 = d2
@@ -1148,12 +1102,11 @@ __global__ __launch_bounds__(256) void k_actors(KArgs K, uint8_t* __restrict__ r
   bool live = false;
   int nrt = 0, tid0 = 0, beh = CBEV_BEH_NONE;
   double s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  double fx = 0.0, fy = 0.0, ts = 0.0, segmax = 0.0;
+  double fx = 0.0, fy = 0.0, ts = 0.0;
   // the fields the step reads; behaviours may change them, so a wave with any
   // behaviour reads them again after running those
   auto load_fields = [&]() {
     ts = RAD(r, CBEV_AD_T_SPEED, a);
-    segmax = RAD(r, CBEV_AD_SEGMAX, a);
     nrt = RAI(r, CBEV_AI_NROUTE, a);
     tid0 = RAI(r, CBEV_AI_TIDX, a);
 #pragma unroll
@@ -1168,7 +1121,7 @@ __global__ __launch_bounds__(256) void k_actors(KArgs K, uint8_t* __restrict__ r
   }
   const int nact = r.hi[CBEV_HI_NACT];
   const double t = r.hd[CBEV_HD_T] + CB_DT;
-  asm volatile("" ::"v"(beh), "v"(nrt), "v"(tid0), "v"(ts), "v"(s[0]), "v"(s[1]), "v"(s[2]), "v"(s[3]), "v"(segmax));
+  asm volatile("" ::"v"(beh), "v"(nrt), "v"(tid0), "v"(ts), "v"(s[0]), "v"(s[1]), "v"(s[2]), "v"(s[3]));
   if (nact == 0) return;
   if (WIDE && nact > 64) {
     for (int k = lane; k < nact; k += 64) d_actor_step(r, k, t);
@@ -1228,13 +1181,13 @@ __global__ __launch_bounds__(256) void k_actors(KArgs K, uint8_t* __restrict__ r
   const int aw = nact <= 1 ? 64 : nact <= 2 ? 32 : nact <= 4 ? 16 : nact <= 8 ? 8 : nact <= 16 ? 4 : nact <= 32 ? 2 : 1;
   int best;
   switch (aw) {
-    case 64: best = actor_search<64>(r, nact, livem, fx, fy, nrt, segmax, lane); break;
-    case 32: best = actor_search<32>(r, nact, livem, fx, fy, nrt, segmax, lane); break;
-    case 16: best = actor_search<16>(r, nact, livem, fx, fy, nrt, segmax, lane); break;
-    case 8: best = actor_search<8>(r, nact, livem, fx, fy, nrt, segmax, lane); break;
-    case 4: best = actor_search<4>(r, nact, livem, fx, fy, nrt, segmax, lane); break;
-    case 2: best = actor_search<2>(r, nact, livem, fx, fy, nrt, segmax, lane); break;
-    default: best = actor_search<1>(r, nact, livem, fx, fy, nrt, segmax, lane); break;
+    case 64: best = actor_search<64>(r, nact, livem, fx, fy, nrt, lane); break;
+    case 32: best = actor_search<32>(r, nact, livem, fx, fy, nrt, lane); break;
+    case 16: best = actor_search<16>(r, nact, livem, fx, fy, nrt, lane); break;
+    case 8: best = actor_search<8>(r, nact, livem, fx, fy, nrt, lane); break;
+    case 4: best = actor_search<4>(r, nact, livem, fx, fy, nrt, lane); break;
+    case 2: best = actor_search<2>(r, nact, livem, fx, fy, nrt, lane); break;
+    default: best = actor_search<1>(r, nact, livem, fx, fy, nrt, lane); break;
   }
   CBEV_STAMPW(6, 2);
   // ---- 3: stanley_control (stanley_controller.py:64-89), pid_control, State.update

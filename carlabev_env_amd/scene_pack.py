@@ -142,8 +142,6 @@ def init_actor_slot(view: LY.RecordView, a: int, spec: ActorSpec, np_rng, map_si
     ad[LY.AD["STATE_ELAPSED"], a] = 0.0
     ad[LY.AD["P0"], a], ad[LY.AD["P1"], a] = p0, p1
     ad[LY.AD["GOAL_X"], a] = ad[LY.AD["GOAL_Y"], a] = 0.0
-    # the smoothed route's longest segment: the device target search's chunk pruning bound
-    ad[LY.AD["SEGMAX"], a] = float(np.max(np.hypot(np.diff(ci.cx), np.diff(ci.cy)))) if n > 1 else 0.0
     ai[LY.AI["KIND"], a] = 1 if spec.kind == "vehicle" else 2
     ai[LY.AI["SIZE"], a] = size
     ai[LY.AI["TIDX"], a] = ci.target_idx

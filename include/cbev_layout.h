@@ -79,9 +79,7 @@
   F_(TIME)           /* Controller.time */                                     \
   F_(ELAPSED) F_(STATE_ELAPSED) /* jaywalk.py:17-18 */                          \
   F_(P0) F_(P1)       /* behaviour parameters */                                \
-  F_(GOAL_X) F_(GOAL_Y) /* jaywalk _retreat_goal */                            \
-  F_(SEGMAX)         /* longest segment of the smoothed route (acx, acy): the   \
-                        actor target search's chunk pruning (device only) */
+  F_(GOAL_X) F_(GOAL_Y) /* jaywalk _retreat_goal */
 
 /* ---- actor scalars, int32, field-major [field][actor_cap] ------------- */
 #define CBEV_AI_FIELDS(F_)                                                     \

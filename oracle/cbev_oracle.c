@@ -720,13 +720,6 @@ static void actor_set_route_surface(orc_rec* r, int a, const double* rx, const d
   }
   free(tx);
   AI(r, CBEV_AI_NROUTE, a) = m;
-  /* the device's target-search pruning bound (AD SEGMAX): the longest segment */
-  double segmax = 0.0;
-  for (int i = 1; i < m; ++i) {
-    double d = hypot(cx[i] - cx[i - 1], cy[i] - cy[i - 1]);
-    if (d > segmax) segmax = d;
-  }
-  AD(r, CBEV_AD_SEGMAX, a) = segmax;
   AD(r, CBEV_AD_X, a) = cx[0];
   AD(r, CBEV_AD_Y, a) = cy[0];
   AD(r, CBEV_AD_V, a) = v0;

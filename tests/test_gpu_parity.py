@@ -82,10 +82,6 @@ def compare_records(a: np.ndarray, b: np.ndarray, layout, tag=""):
         # pass) follows every rebuild of the smoothed route
         assert np.array_equal(va.acf[a, :m, 0], va.acx[a, :m].astype(np.float32)), (tag, "acf x", a)
         assert np.array_equal(va.acf[a, :m, 1], va.acy[a, :m].astype(np.float32)), (tag, "acf y", a)
-        # and its longest segment (the search's chunk pruning bound, AD SEGMAX)
-        if m > 1:
-            seg = np.hypot(np.diff(va.acx[a, :m]), np.diff(va.acy[a, :m])).max()
-            assert np.isclose(va.ad[LY.AD["SEGMAX"], a], seg, rtol=1e-12, atol=1e-12), (tag, "segmax", a)
 
 
 def info_of(v, cause):
