@@ -2796,27 +2796,52 @@ __global__ __launch_bounds__(256) void k_ego(uint8_t* __restrict__ recs, int n, 
   }
   CBEV_STAMP(3, 1);
   // S2: Controller.calc_target_index (stanley_controller.py:51-62),
-  // np.argmin(np.hypot(dx, dy)): the first smallest hypot, in one pass
+  // np.argmin(np.hypot(dx, dy)): the first smallest hypot, in two passes as
+  // d_target_index_serial: the env's smallest squared distance (a square is
+  // within a few ulp of hypot^2, so every index whose hypot can reach the
+  // minimum has one within (1 + 1e-14) of it), then hypot over those candidates
+  // only (almost always one point of the env) with the reference's strict '<'
   if (s2) {
     double syaw, cyaw;
     d_sincos(s2yaw, &syaw, &cyaw);
     const double fx = s2hx + CB_WHEELBASE * cyaw;
     const double fy = s2hy + CB_WHEELBASE * syaw;
+    double d2v[S2_PF], m2 = INFINITY;
+#pragma unroll
+    for (int j = 0; j < S2_PF; ++j) {
+      const int i = s2sub + j * tpe2;
+      const double dx = fx - s2x[j], dy = fy - s2y[j];
+      d2v[j] = i < s2nr ? dx * dx + dy * dy : INFINITY;
+      m2 = d2v[j] < m2 ? d2v[j] : m2;  // NaN never wins
+    }
+    for (int i = s2sub + S2_PF * tpe2; i < s2nr; i += tpe2) {  // routes past the prefetched points
+      const double dx = fx - s2g.cx[i], dy = fy - s2g.cy[i];
+      const double d2 = dx * dx + dy * dy;
+      m2 = d2 < m2 ? d2 : m2;
+    }
+    butterfly(tpe2, [&](auto off) {
+      constexpr int O = decltype(off)::value;
+      const double q = peer_f64<O>(m2);
+      m2 = q < m2 ? q : m2;
+    });
+    const double lim = m2 * (1.0 + 1e-14);
     double bd = INFINITY;
     int bi = 0x7fffffff;
 #pragma unroll
     for (int j = 0; j < S2_PF; ++j) {
       const int i = s2sub + j * tpe2;
-      if (i < s2nr) {
+      if (d2v[j] <= lim) {
         const double h = hypot(fx - s2x[j], fy - s2y[j]);
-        if (h < bd) {  // first minimum within this thread's (increasing) indices; NaN never wins
+        if (h < bd) {  // first minimum within this thread's (increasing) indices
           bd = h;
           bi = i;
         }
       }
     }
-    for (int i = s2sub + S2_PF * tpe2; i < s2nr; i += tpe2) {  // routes past the prefetched points
-      const double h = hypot(fx - s2g.cx[i], fy - s2g.cy[i]);
+    for (int i = s2sub + S2_PF * tpe2; i < s2nr; i += tpe2) {
+      const double dx = fx - s2g.cx[i], dy = fy - s2g.cy[i];
+      if (!(dx * dx + dy * dy <= lim)) continue;
+      const double h = hypot(dx, dy);
       if (h < bd) {
         bd = h;
         bi = i;
