@@ -156,7 +156,12 @@ int cbev_bank_cursor(cbev_ctx* ctx, int64_t* cursor);
  * it first launches it on the stream it was recorded on, as does cbev_flush.
  * A caller that reads the records, the frame ring or writes the term buffer
  * itself calls cbev_flush first. Only records without actor slots (k_ego is the
- * step's first kernel) fold; otherwise cbev_reset_terminated launches at once. */
+ * step's first kernel) fold; otherwise cbev_reset_terminated launches at once.
+ * The deferral is host-side state, taken when cbev_step is called: a cbev_step
+ * captured into a graph while a reset is pending carries the folded reset, so
+ * every replay resets the envs its term buffer selects at replay time (the mask
+ * ranking and the cursor advance run on the device); cbev_flush before
+ * capturing a step that must not reset. */
 int cbev_set_deferred_reset(cbev_ctx* ctx, int on);
 /* 1 when a deferred reset is recorded and not yet applied. */
 int cbev_reset_pending(const cbev_ctx* ctx);
