@@ -162,6 +162,25 @@ __device__ int d_smooth_route(DRec& r, int a) {
   return n;
 }
 
+// The pruning circle (acb) of the float32 points p[0..m): the bounding box's
+// centre in 1/8 px fixed point and the largest distance from that quantised
+// centre, rounded up to 1/8 px plus 1/8 px (layout.acb_circles on the host)
+__device__ __forceinline__ uint2 d_acb_circle(const float* p, int m) {
+  double x0 = INFINITY, x1 = -INFINITY, y0 = INFINITY, y1 = -INFINITY;
+  for (int i = 0; i < m; ++i) {
+    x0 = fmin(x0, (double)p[2 * i]);
+    x1 = fmax(x1, (double)p[2 * i]);
+    y0 = fmin(y0, (double)p[2 * i + 1]);
+    y1 = fmax(y1, (double)p[2 * i + 1]);
+  }
+  const int qx = (int)fmin(fmax(rint((x0 + x1) * 0.5 * 8.0) + 32768.0, 0.0), 65535.0);
+  const int qy = (int)fmin(fmax(rint((y0 + y1) * 0.5 * 8.0) + 32768.0, 0.0), 65535.0);
+  const double cx = (qx - 32768) / 8.0, cy = (qy - 32768) / 8.0;
+  double rr = 0.0;
+  for (int i = 0; i < m; ++i) rr = fmax(rr, hypot((double)p[2 * i] - cx, (double)p[2 * i + 1] - cy));
+  return make_uint2((uint32_t)qx | ((uint32_t)qy << 16), (uint32_t)ceil(rr * 8.0) + 1u);
+}
+
 // BaseJaywalkBehavior._start_retreat (jaywalk.py:43-54) + Actor.set_route_surface
 // (actor.py:139-149) + Controller.set_route(jitter_start=False).
 __device__ __noinline__ void d_start_retreat(DRec& r, int a) {
@@ -196,6 +215,9 @@ __device__ __noinline__ void d_start_retreat(DRec& r, int a) {
     cf[2 * i] = (float)cx[i];
     cf[2 * i + 1] = (float)cy[i];
   }
+  uint2* cb = r.acb + (int64_t)a * ((RA + CBEV_ACB_PTS - 1) / CBEV_ACB_PTS);  // and its pruning circles
+  for (int b = 0; b * CBEV_ACB_PTS < m; ++b)
+    cb[b] = d_acb_circle(cf + 2 * CBEV_ACB_PTS * b, min(CBEV_ACB_PTS, m - CBEV_ACB_PTS * b));
   double v0 = RAD(r, CBEV_AD_V, a);
   RAD(r, CBEV_AD_X, a) = cx[0];
   RAD(r, CBEV_AD_Y, a) = cy[0];
@@ -243,8 +265,8 @@ __device__ __forceinline__ void wave_mem_fence() { __builtin_amdgcn_fence(__ATOM
 // ints: a DRec (or KArgs) reference makes every k_actors wave spill that struct
 // to scratch at launch (12 KB per wave), retreat or not.
 __device__ __noinline__ bool wave_start_retreat(uint8_t* base, int o_ad, int o_ai, int o_aix, int o_aiy, int o_arx,
-                                                int o_ary, int o_acx, int o_acy, int o_acyaw, int o_acf, int A, int RA,
-                                                int a, int lane) {
+                                                int o_ary, int o_acx, int o_acy, int o_acyaw, int o_acf, int o_acb, int A,
+                                                int RA, int a, int lane) {
   wave_mem_fence();  // the owner lane's behaviour stores come first
   DRec r{};
   r.ad = (double*)(base + o_ad);
@@ -381,6 +403,28 @@ __device__ __noinline__ bool wave_start_retreat(uint8_t* base, int o_ad, int o_a
     float* cf = (float*)(base + o_acf) + 2 * ((int64_t)a * RA + lane);  // the search's float32 copy
     cf[0] = (float)cxv;
     cf[1] = (float)cyv;
+  }
+  {  // its pruning circles: one per CBEV_ACB_PTS lanes (d_acb_circle's arithmetic, reduced over the block)
+    static_assert(CBEV_ACB_PTS == 16, "the block reductions below span 16 lanes");
+    const bool in = lane < nd;
+    const double px = (double)(float)cxv, py = (double)(float)cyv;
+    double x0 = in ? px : INFINITY, x1 = in ? px : -INFINITY, y0 = in ? py : INFINITY, y1 = in ? py : -INFINITY;
+#pragma unroll
+    for (int off = 1; off < 16; off <<= 1) {
+      x0 = fmin(x0, __shfl_xor(x0, off, 64));
+      x1 = fmax(x1, __shfl_xor(x1, off, 64));
+      y0 = fmin(y0, __shfl_xor(y0, off, 64));
+      y1 = fmax(y1, __shfl_xor(y1, off, 64));
+    }
+    const int qx = (int)fmin(fmax(rint((x0 + x1) * 0.5 * 8.0) + 32768.0, 0.0), 65535.0);
+    const int qy = (int)fmin(fmax(rint((y0 + y1) * 0.5 * 8.0) + 32768.0, 0.0), 65535.0);
+    double rr = in ? hypot(px - (qx - 32768) / 8.0, py - (qy - 32768) / 8.0) : 0.0;
+#pragma unroll
+    for (int off = 1; off < 16; off <<= 1) rr = fmax(rr, __shfl_xor(rr, off, 64));
+    if ((lane & 15) == 0 && lane < nd) {
+      uint2* cb = (uint2*)(base + o_acb) + (int64_t)a * ((RA + CBEV_ACB_PTS - 1) / CBEV_ACB_PTS) + (lane >> 4);
+      *cb = make_uint2((uint32_t)qx | ((uint32_t)qy << 16), (uint32_t)ceil(rr * 8.0) + 1u);
+    }
   }
   // ---- Actor.set_route_surface / Controller.set_route(jitter_start=False): pose at the
   // smoothed start, target index from there (calc_target_index), heading cyaw[idx]
@@ -1083,6 +1127,160 @@ __device__ __forceinline__ int actor_search(const DRec& r, int nact, uint64_t li
   return best;
 }
 
+// The windowed search (CBEV_ACTOR_WINDOW): in one round of loads, the two
+// CBEV_ACB_PTS-point blocks from the actor's previous target index (where the
+// arg-min almost always is: the target moves a point or two a step) and the
+// pruning circles of every block of the route (acb: a circle holding the
+// block's float32 points). The window's float32 minimum bounds pass 1's
+// candidates; a block outside the window is scanned (a second round) only if
+// its circle comes within that reach of the front axle -- by the triangle
+// inequality no point of a skipped block is within 3 eps of the float32
+// minimum, so it is never a pass-1 candidate. Then passes 1-2 as actor_search.
+#ifndef CBEV_ACTOR_WINDOW
+#define CBEV_ACTOR_WINDOW 1
+#endif
+constexpr int ACTOR_CQ = 10;  // circles per lane held at once (routes of more blocks: every block scanned)
+template <int AW>
+__device__ __forceinline__ int actor_search_win(const DRec& r, int nact, uint64_t livem, double fx, double fy,
+                                                int nrt, int tid0, int lane) {
+  constexpr int AG = 64 / AW;
+  constexpr int BP = CBEV_ACB_PTS;
+  constexpr int WPL = (2 * BP + AW - 1) / AW;  // window points per lane
+  constexpr int BPL = (BP + AW - 1) / AW;      // points per lane of a further block
+  const int RA = r.RA, NBC = (RA + BP - 1) / BP;
+  const int g = lane / AW, sub = lane - g * AW;
+  int best = 0;
+  for (int r0 = 0; r0 < nact; r0 += AG) {
+    const int aa = r0 + g;  // this group's actor
+    const double gfx = __shfl(fx, aa & 63), gfy = __shfl(fy, aa & 63);
+    const int gn = __shfl(nrt, aa & 63), gt0 = __shfl(tid0, aa & 63);
+    const bool glive = aa < nact && ((livem >> (aa & 63)) & 1ull);
+    const double* cx = r.acx + (int64_t)(aa & 63) * RA;
+    const double* cy = r.acy + (int64_t)(aa & 63) * RA;
+    const float2* cf = (const float2*)r.acf + (int64_t)(aa & 63) * RA;
+    const uint2* cb = r.acb + (int64_t)(aa & 63) * NBC;
+    const float ffx = (float)gfx, ffy = (float)gfy;
+    const int nb = (gn + BP - 1) / BP;
+    const int kb = min(max(gt0 - 2, 0) / BP, max(nb - 2, 0));  // the window: blocks kb, kb + 1
+    const int w0 = kb * BP, w1 = min(w0 + 2 * BP, gn);
+    float f1 = INFINITY, f2 = INFINITY, f3 = INFINITY;
+    int j1 = -1, j2 = -1;
+    auto track = [&](int i, float2 p) {
+      const float dx = ffx - p.x, dy = ffy - p.y;
+      const float d = dx * dx + dy * dy;
+      const bool l1 = d < f1, l2 = d < f2;
+      f3 = l2 ? f2 : (d < f3 ? d : f3);
+      f2 = l1 ? f1 : (l2 ? d : f2);
+      j2 = l1 ? j1 : (l2 ? i : j2);
+      f1 = l1 ? d : f1;
+      j1 = l1 ? i : j1;
+    };
+    uint32_t cand = 0;  // blocks outside the window to scan (group-uniform below)
+    if (glive) {
+      float2 pw[WPL];
+      uint2 cq[ACTOR_CQ];
+#pragma unroll
+      for (int u = 0; u < WPL; ++u) pw[u] = cf[min(w0 + sub + u * AW, gn - 1)];  // no branch around a load
+#pragma unroll
+      for (int q = 0; q < ACTOR_CQ; ++q) cq[q] = cb[min(sub + q * AW, nb - 1)];
+#pragma unroll
+      for (int u = 0; u < WPL; ++u) {
+        const int i = w0 + sub + u * AW;
+        if (i < w1) track(i, pw[u]);
+      }
+      float mw = f1;
+#pragma unroll
+      for (int off = AW / 2; off > 0; off >>= 1) {
+        const float o = __shfl_xor(mw, off, 64);
+        mw = o < mw ? o : mw;
+      }
+      const float reach = sqrtf(mw) + 0.15f + 0.05f;  // pass 1's 3 eps + float32 margins
+      if (nb > ACTOR_CQ * AW) {
+        cand = (nb >= 32 ? ~0u : ((1u << nb) - 1u)) & ~(3u << kb);
+      } else {
+#pragma unroll
+        for (int q = 0; q < ACTOR_CQ; ++q) {
+          const int k = sub + q * AW;
+          if (k >= nb || k == kb || k == kb + 1) continue;
+          const float bx = (float)((int)(cq[q].x & 0xffffu) - 32768) * 0.125f;
+          const float by = (float)((int)(cq[q].x >> 16) - 32768) * 0.125f;
+          const float dx = ffx - bx, dy = ffy - by;
+          if (sqrtf(dx * dx + dy * dy) - (float)cq[q].y * 0.125f <= reach) cand |= 1u << k;
+        }
+      }
+    }
+#pragma unroll
+    for (int off = AW / 2; off > 0; off >>= 1) cand |= (uint32_t)__shfl_xor((int)cand, off, 64);
+    // round 2 (rare): the blocks whose circle comes within reach
+    for (uint32_t c = cand; c; c &= c - 1) {
+      const int k0 = BP * __builtin_ctz(c);
+      float2 pb[BPL];
+#pragma unroll
+      for (int u = 0; u < BPL; ++u) pb[u] = cf[min(k0 + sub + u * AW, gn - 1)];
+#pragma unroll
+      for (int u = 0; u < BPL; ++u) {
+        const int i = k0 + sub + u * AW;
+        if (u * AW + sub < BP && i < gn) track(i, pb[u]);
+      }
+    }
+    float mf = f1;
+#pragma unroll
+    for (int off = AW / 2; off > 0; off >>= 1) {
+      const float o = __shfl_xor(mf, off, 64);
+      mf = o < mf ? o : mf;
+    }
+    const float tf = sqrtf(mf) + 0.15f, thr = tf * tf;  // 3 eps
+    double m2 = INFINITY, s2 = INFINITY;
+    int i2 = 0x7fffffff;
+    auto exact = [&](int i) {  // one point of the serial float64 scan, in index order
+      const double dx = gfx - cx[i], dy = gfy - cy[i];
+      const double d2 = dx * dx + dy * dy;
+      const bool lt = d2 < m2;
+      s2 = lt ? m2 : (d2 < s2 ? d2 : s2);
+      m2 = lt ? d2 : m2;
+      i2 = lt ? i : i2;
+    };
+    if (glive && f3 <= thr) {  // three or more candidates in this lane: its scanned points in float64, in index order
+      for (int kk = 0; kk < nb; ++kk) {
+        if (!(kk == kb || kk == kb + 1 || ((cand >> kk) & 1u))) continue;
+        for (int i = kk * BP + sub; i < min(kk * BP + BP, gn); i += AW) exact(i);
+      }
+    } else if (glive) {
+      int c1 = f1 <= thr ? j1 : -1, c2 = f2 <= thr ? j2 : -1;
+      if (c1 > c2) {  // index order (-1: none)
+        const int t = c1;
+        c1 = c2;
+        c2 = t;
+      }
+      if (c1 >= 0) exact(c1);
+      if (c2 >= 0) exact(c2);
+    }
+    group_min2<AW>(m2, i2, s2);
+    const double lim = m2 * (1.0 + 1e-14);
+    const bool need = !(s2 > lim);
+    double bd = INFINITY;
+    int bi = 0x7fffffff;
+    if (!need) {
+      bd = 0.0;
+      bi = i2;
+    } else if (glive) {
+      for (int i = sub; i < gn; i += AW) {
+        const double dx = gfx - cx[i], dy = gfy - cy[i];
+        if (!(dx * dx + dy * dy <= lim)) continue;
+        const double h = hypot(dx, dy);
+        if (bi == 0x7fffffff || h < bd) {  // the first candidate is taken as is (serial `first`)
+          bd = h;
+          bi = i;
+        }
+      }
+    }
+    group_argmin<AW>(bd, bi);
+    const int got = __shfl(bi, ((lane - r0) & (AG - 1)) * AW);
+    if (lane >= r0 && lane < r0 + AG) best = got == 0x7fffffff ? 0 : got;
+  }
+  return best;
+}
+
 // WIDE: the context's capacity allows more than 64 actors, which take the
 // serial per-lane path (d_actor_step). Contexts within 64 actor slots launch
 // k_actors<false>, which compiles without it: 134 instead of 246 VGPRs, 3 waves
@@ -1139,7 +1337,8 @@ __global__ __launch_bounds__(256) void k_actors(KArgs K, uint8_t* __restrict__ r
       rm &= rm - 1;
       uint8_t* base = recs + (int64_t)e * K.L.record_bytes;
       if (!wave_start_retreat(base, (int)K.L.ad, (int)K.L.ai, (int)K.L.aix, (int)K.L.aiy, (int)K.L.arx, (int)K.L.ary,
-                              (int)K.L.acx, (int)K.L.acy, (int)K.L.acyaw, (int)K.L.acf, r.A, RA, k, lane)) {
+                              (int)K.L.acx, (int)K.L.acy, (int)K.L.acyaw, (int)K.L.acf, (int)K.L.acb, r.A, RA, k,
+                              lane)) {
         // a rebuilt route of more than 64 points: scene_pack refuses such actors
         // (a StopReturn route of at most 63 points); a record written otherwise
         // is rebuilt serially by the wide kernel, flagged by the narrow one
@@ -1181,13 +1380,13 @@ __global__ __launch_bounds__(256) void k_actors(KArgs K, uint8_t* __restrict__ r
   const int aw = nact <= 1 ? 64 : nact <= 2 ? 32 : nact <= 4 ? 16 : nact <= 8 ? 8 : nact <= 16 ? 4 : nact <= 32 ? 2 : 1;
   int best;
   switch (aw) {
-    case 64: best = actor_search<64>(r, nact, livem, fx, fy, nrt, lane); break;
-    case 32: best = actor_search<32>(r, nact, livem, fx, fy, nrt, lane); break;
-    case 16: best = actor_search<16>(r, nact, livem, fx, fy, nrt, lane); break;
-    case 8: best = actor_search<8>(r, nact, livem, fx, fy, nrt, lane); break;
-    case 4: best = actor_search<4>(r, nact, livem, fx, fy, nrt, lane); break;
-    case 2: best = actor_search<2>(r, nact, livem, fx, fy, nrt, lane); break;
-    default: best = actor_search<1>(r, nact, livem, fx, fy, nrt, lane); break;
+    case 64: best = CBEV_ACTOR_WINDOW ? actor_search_win<64>(r, nact, livem, fx, fy, nrt, tid0, lane) : actor_search<64>(r, nact, livem, fx, fy, nrt, lane); break;
+    case 32: best = CBEV_ACTOR_WINDOW ? actor_search_win<32>(r, nact, livem, fx, fy, nrt, tid0, lane) : actor_search<32>(r, nact, livem, fx, fy, nrt, lane); break;
+    case 16: best = CBEV_ACTOR_WINDOW ? actor_search_win<16>(r, nact, livem, fx, fy, nrt, tid0, lane) : actor_search<16>(r, nact, livem, fx, fy, nrt, lane); break;
+    case 8: best = CBEV_ACTOR_WINDOW ? actor_search_win<8>(r, nact, livem, fx, fy, nrt, tid0, lane) : actor_search<8>(r, nact, livem, fx, fy, nrt, lane); break;
+    case 4: best = CBEV_ACTOR_WINDOW ? actor_search_win<4>(r, nact, livem, fx, fy, nrt, tid0, lane) : actor_search<4>(r, nact, livem, fx, fy, nrt, lane); break;
+    case 2: best = CBEV_ACTOR_WINDOW ? actor_search_win<2>(r, nact, livem, fx, fy, nrt, tid0, lane) : actor_search<2>(r, nact, livem, fx, fy, nrt, lane); break;
+    default: best = actor_search<1>(r, nact, livem, fx, fy, nrt, lane); break;  // one lane per actor: the 32-point window would not fit the registers
   }
   CBEV_STAMPW(6, 2);
   // ---- 3: stanley_control (stanley_controller.py:64-89), pid_control, State.update

@@ -81,6 +81,7 @@ struct DRec {
   int32_t* ai;
   double *acx, *acy, *acyaw, *aix, *aiy, *arx, *ary;
   float* acf;  // [A][RA][2]: acx / acy as float32
+  uint2* acb;  // [A][ceil(RA / CBEV_ACB_PTS)]: fixed-point circle of each block of acf's points
   int32_t* ti;
   int A, RA, T;
 };
@@ -103,6 +104,7 @@ __device__ __forceinline__ DRec bind_rec(uint8_t* base, const cbev_layout& L, co
   r.acy = (double*)(base + L.acy);
   r.acyaw = (double*)(base + L.acyaw);
   r.acf = (float*)(base + L.acf);
+  r.acb = (uint2*)(base + L.acb);
   r.aix = (double*)(base + L.aix);
   r.aiy = (double*)(base + L.aiy);
   r.arx = (double*)(base + L.arx);

@@ -47,6 +47,7 @@ AI = {n: i for i, n in enumerate(NAMES["AI"])}
 TI = {n: i for i, n in enumerate(NAMES["TI"])}
 EP = {n: i for i, n in enumerate(NAMES["EP"])}  # episode summary row columns (CBEV_EP_FIELDS)
 STATS_BYTES = 1856                              # sizeof(cbev_episode_stats)
+ACB_PTS = int(re.search(r"#define CBEV_ACB_PTS (\d+)", open(HEADER).read()).group(1))  # points per pruning circle
 
 # enums mirrored from the header (values are part of the C-ABI)
 BEH = {"none": 0, "timed_brake": 1, "cross": 2, "stop_mid": 3, "yield_return": 4}
@@ -67,7 +68,7 @@ class CbevCaps(ctypes.Structure):
 class CbevLayout(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int64) for n in (
         "hd", "hi", "cx", "cy", "cyaw", "raw_x", "raw_y", "raw_cum", "vis", "ad", "ai",
-        "acx", "acy", "acyaw", "aix", "aiy", "arx", "ary", "ti", "acf", "record_bytes")] + [
+        "acx", "acy", "acyaw", "aix", "aiy", "arx", "ary", "ti", "acf", "acb", "record_bytes")] + [
         ("vis_words", ctypes.c_int32), ("pad", ctypes.c_int32)]
 
 
@@ -120,6 +121,7 @@ class Layout:
             put(n, 8 * A * RA)
         put("ti", 4 * len(TI) * T)
         put("acf", 8 * A * RA)  # acx / acy as float32 pairs (the actor target search's first pass)
+        put("acb", 8 * A * ((RA + ACB_PTS - 1) // ACB_PTS))  # pruning circles of acf's point blocks
         return Layout(caps, off, _align(o, 256), vis_words)
 
 
@@ -170,6 +172,7 @@ class RecordView:
         self.ary = v("ary", np.float64, (A, RA))
         self.ti = v("ti", np.int32, (len(TI), T))
         self.acf = v("acf", np.float32, (A, RA, 2))
+        self.acb = v("acb", np.uint32, (A, (RA + ACB_PTS - 1) // ACB_PTS, 2))
 
     def h(self, name):
         return self.hd[HD[name]]
@@ -187,4 +190,22 @@ def batch_views(buf: np.ndarray, layout: Layout, n: int) -> dict:
     o = layout.off
     out["hd"] = base[:, o["hd"]:o["hd"] + 8 * len(HD)].view(np.float64)
     out["hi"] = base[:, o["hi"]:o["hi"] + 4 * len(HI)].view(np.int32)
+    return out
+
+
+def acb_circles(pts: np.ndarray) -> np.ndarray:
+    """The pruning circles (acb) of an actor's float32 route points pts[n][2]:
+    per block of ACB_PTS points, the bounding box's centre in 1/8 px fixed point
+    and the largest distance of a point from that (quantised) centre, rounded up
+    to 1/8 px plus 1/8 px. uint32[ceil(n / ACB_PTS)][2] (cbev_layout.h acb)."""
+    n = len(pts)
+    out = np.zeros(((n + ACB_PTS - 1) // ACB_PTS, 2), np.uint32)
+    p = pts.astype(np.float64)
+    for b in range(len(out)):
+        q = p[ACB_PTS * b: ACB_PTS * (b + 1)]
+        cq = np.clip(np.rint((q.min(0) + q.max(0)) * 0.5 * 8.0) + 32768, 0, 65535).astype(np.int64)
+        c = (cq - 32768) / 8.0
+        r = float(np.max(np.hypot(q[:, 0] - c[0], q[:, 1] - c[1])))
+        out[b, 0] = int(cq[0]) | (int(cq[1]) << 16)
+        out[b, 1] = int(np.ceil(r * 8.0)) + 1
     return out

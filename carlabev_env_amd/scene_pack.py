@@ -159,6 +159,7 @@ def init_actor_slot(view: LY.RecordView, a: int, spec: ActorSpec, np_rng, map_si
         ad[LY.AD["T_SPEED"], a] = 0.0
     view.acx[a, :n], view.acy[a, :n], view.acyaw[a, :n] = ci.cx, ci.cy, ci.cyaw
     view.acf[a, :n, 0], view.acf[a, :n, 1] = view.acx[a, :n], view.acy[a, :n]  # float32 rounding
+    view.acb[a, :(n + LY.ACB_PTS - 1) // LY.ACB_PTS] = LY.acb_circles(view.acf[a, :n])  # the search's pruning circles
     view.aix[a, :len(rx)], view.aiy[a, :len(rx)] = rx, ry
     view.arx[a, :len(rx)], view.ary[a, :len(rx)] = rx, ry
 

@@ -147,6 +147,9 @@ typedef struct cbev_caps {
   int32_t tl_cap;           /* traffic lights */
 } cbev_caps;
 
+/* route points per pruning circle of the actor target search (acb) */
+#define CBEV_ACB_PTS 16
+
 /* byte offsets of each group inside one record */
 typedef struct cbev_layout {
   int64_t hd, hi;                       /* double[HD_COUNT], int32[HI_COUNT] */
@@ -165,6 +168,12 @@ typedef struct cbev_layout {
   int64_t ti;                           /* int32[TI][T] */
   int64_t acf;                          /* float[A][RA][2]: acx / acy rounded to float32,
                                            the actor target search's first pass */
+  int64_t acb;                          /* uint32[A][ceil(RA / CBEV_ACB_PTS)][2]: per block of
+                                           CBEV_ACB_PTS consecutive points of acf, a circle
+                                           holding them in 1/8 px fixed point: word 0 =
+                                           (x * 8 + 32768) | (y * 8 + 32768) << 16, word 1 =
+                                           radius * 8 (rounded up): the actor target
+                                           search's pruning bound */
   int64_t record_bytes;                 /* multiple of 256 */
   int32_t vis_words;
   int32_t pad;
@@ -199,6 +208,7 @@ static inline cbev_layout cbev_make_layout(cbev_caps c) {
   L.ary = o;     o = cbev__align(o + 8 * A * RA, 64);
   L.ti = o;      o = cbev__align(o + 4 * (int64_t)CBEV_TI_COUNT * T, 64);
   L.acf = o;     o = cbev__align(o + 8 * A * RA, 64);
+  L.acb = o;     o = cbev__align(o + 8 * A * ((RA + CBEV_ACB_PTS - 1) / CBEV_ACB_PTS), 64);
   L.record_bytes = cbev__align(o, 256);
   L.pad = 0;
   return L;

@@ -190,3 +190,20 @@ def test_library_layout_check_refuses_a_mismatch():
             return rc
     with pytest.raises(RuntimeError, match="ai"):
         LY.check_library_layout(Shifted, CAPS_FULL)
+
+
+def test_acb_circles_hold_their_blocks():
+    """layout.acb_circles: per block of ACB_PTS route points, a fixed-point circle
+    holding every point (the actor target search skips a block by it), as
+    scene_pack writes it."""
+    rng = np.random.default_rng(5)
+    for n in (1, 15, 16, 17, 64, 276):
+        pts = (rng.uniform(0, 1200, 2) + np.cumsum(rng.normal(0, 9, (n, 2)), 0)).astype(np.float32)
+        acb = LY.acb_circles(pts)
+        assert acb.shape == ((n + LY.ACB_PTS - 1) // LY.ACB_PTS, 2)
+        for b in range(len(acb)):
+            w0, w1 = int(acb[b, 0]), int(acb[b, 1])
+            c = np.array([(w0 & 0xFFFF) - 32768, (w0 >> 16) - 32768]) / 8.0
+            q = pts[LY.ACB_PTS * b: LY.ACB_PTS * (b + 1)].astype(np.float64)
+            d = np.hypot(q[:, 0] - c[0], q[:, 1] - c[1])
+            assert d.max() <= w1 / 8.0 and w1 / 8.0 <= d.max() + 0.25 + 1e-9

@@ -82,6 +82,20 @@ def compare_records(a: np.ndarray, b: np.ndarray, layout, tag=""):
         # pass) follows every rebuild of the smoothed route
         assert np.array_equal(va.acf[a, :m, 0], va.acx[a, :m].astype(np.float32)), (tag, "acf x", a)
         assert np.array_equal(va.acf[a, :m, 1], va.acy[a, :m].astype(np.float32)), (tag, "acf y", a)
+        # and its pruning circles (acb) hold every block's float32 points
+        assert acb_holds(va.acb[a], va.acf[a, :m]), (tag, "acb", a)
+
+
+def acb_holds(acb, pts) -> bool:
+    """Every float32 route point lies inside its block's circle (cbev_layout.h acb)."""
+    P = LY.ACB_PTS
+    for b in range((len(pts) + P - 1) // P):
+        w0, w1 = int(acb[b, 0]), int(acb[b, 1])
+        c = np.array([(w0 & 0xFFFF) - 32768, (w0 >> 16) - 32768], np.float64) / 8.0
+        q = pts[P * b: P * (b + 1)].astype(np.float64)
+        if np.hypot(q[:, 0] - c[0], q[:, 1] - c[1]).max() > w1 / 8.0:
+            return False
+    return True
 
 
 def info_of(v, cause):
