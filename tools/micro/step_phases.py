@@ -73,6 +73,9 @@ def main():
         if k in (3, 5):  # cycles since the start of k_ego A (3) / B (5) in the same workgroup
             ref = buf[0, 0 if k == 3 else 1].astype(np.int64)[used][:, 0]
             print(f"{name}: cycles since the phase start: {[round(float((st[:, j] - ref).mean())) for j in range(4)]}")
+            print(f"   p50 {[round(float(np.percentile(st[:, j] - ref, 50))) for j in range(4)]} "
+                  f"p90 {[round(float(np.percentile(st[:, j] - ref, 90))) for j in range(4)]} "
+                  f"max {[round(float((st[:, j] - ref).max())) for j in range(4)]}")
             continue
         print(f"{name}: {used.sum()} WGs; cycles mean phase1 {d[:, 0].mean():.0f} (max {d[:, 0].max():.0f})  phase2 {d[:, 1].mean():.0f} "
               f"(max {d[:, 1].max():.0f})  phase3 {d[:, 2].mean():.0f}; WG total mean {(st[:, 3] - st[:, 0]).mean():.0f}; "
