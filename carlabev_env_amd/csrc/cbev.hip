@@ -2100,7 +2100,9 @@ __global__ __launch_bounds__(256) void k_bank_frames(KArgs K, const uint8_t* __r
 // XCD's env blocks and counts the selected envs' pieces in env order, taking
 // every WPX-th.
 #define RESET_PU 4                      // 16-byte loads per thread in flight (8: 12.1 vs 12.5 us at config 3, the step no faster)
+#ifndef RESET_MASK_WGS
 #define RESET_MASK_WGS 512              // k_reset_mask's grid cap (and its cursor copies)
+#endif
 #define CBEV_CURSOR_STRIDE 16           // 128 bytes between the cursor copies
 #define CBEV_RESET_MASK_MAX_N (1 << 20)  // k_reset_mask's unit masks: 2 B per 16 envs of LDS
 #define RESET_PIECE (4096 * RESET_PU)   // bytes per piece
