@@ -1142,7 +1142,8 @@ __device__ __forceinline__ int actor_search(const DRec& r, int nact, uint64_t li
 constexpr int ACTOR_CQ = 10;  // circles per lane held at once (routes of more blocks: every block scanned)
 template <int AW>
 __device__ __forceinline__ int actor_search_win(const DRec& r, int nact, uint64_t livem, double fx, double fy,
-                                                int nrt, int tid0, int lane) {
+                                                int nrt, int tid0, int lane, double p0x, double p0y, double p1x,
+                                                double p1y) {
   constexpr int AG = 64 / AW;
   constexpr int BP = CBEV_ACB_PTS;
   constexpr int WPL = (2 * BP + AW - 1) / AW;  // window points per lane
@@ -1232,8 +1233,24 @@ __device__ __forceinline__ int actor_search_win(const DRec& r, int nact, uint64_
     const float tf = sqrtf(mf) + 0.15f, thr = tf * tf;  // 3 eps
     double m2 = INFINITY, s2 = INFINITY;
     int i2 = 0x7fffffff;
+    // the arg-min is almost always the previous target or the next point, which
+    // the owner lane prefetched for the Stanley step: those two come from it
+    // (no memory round trip), any other candidate from the route
+    const double q0x = __shfl(p0x, aa & 63), q0y = __shfl(p0y, aa & 63);
+    const double q1x = __shfl(p1x, aa & 63), q1y = __shfl(p1y, aa & 63);
     auto exact = [&](int i) {  // one point of the serial float64 scan, in index order
-      const double dx = gfx - cx[i], dy = gfy - cy[i];
+      double px, py;
+      if (i == gt0) {
+        px = q0x;
+        py = q0y;
+      } else if (i == gt0 + 1) {
+        px = q1x;
+        py = q1y;
+      } else {
+        px = cx[i];
+        py = cy[i];
+      }
+      const double dx = gfx - px, dy = gfy - py;
       const double d2 = dx * dx + dy * dy;
       const bool lt = d2 < m2;
       s2 = lt ? m2 : (d2 < s2 ? d2 : s2);
@@ -1380,12 +1397,12 @@ __global__ __launch_bounds__(256) void k_actors(KArgs K, uint8_t* __restrict__ r
   const int aw = nact <= 1 ? 64 : nact <= 2 ? 32 : nact <= 4 ? 16 : nact <= 8 ? 8 : nact <= 16 ? 4 : nact <= 32 ? 2 : 1;
   int best;
   switch (aw) {
-    case 64: best = CBEV_ACTOR_WINDOW ? actor_search_win<64>(r, nact, livem, fx, fy, nrt, tid0, lane) : actor_search<64>(r, nact, livem, fx, fy, nrt, lane); break;
-    case 32: best = CBEV_ACTOR_WINDOW ? actor_search_win<32>(r, nact, livem, fx, fy, nrt, tid0, lane) : actor_search<32>(r, nact, livem, fx, fy, nrt, lane); break;
-    case 16: best = CBEV_ACTOR_WINDOW ? actor_search_win<16>(r, nact, livem, fx, fy, nrt, tid0, lane) : actor_search<16>(r, nact, livem, fx, fy, nrt, lane); break;
-    case 8: best = CBEV_ACTOR_WINDOW ? actor_search_win<8>(r, nact, livem, fx, fy, nrt, tid0, lane) : actor_search<8>(r, nact, livem, fx, fy, nrt, lane); break;
-    case 4: best = CBEV_ACTOR_WINDOW ? actor_search_win<4>(r, nact, livem, fx, fy, nrt, tid0, lane) : actor_search<4>(r, nact, livem, fx, fy, nrt, lane); break;
-    case 2: best = CBEV_ACTOR_WINDOW ? actor_search_win<2>(r, nact, livem, fx, fy, nrt, tid0, lane) : actor_search<2>(r, nact, livem, fx, fy, nrt, lane); break;
+    case 64: best = CBEV_ACTOR_WINDOW ? actor_search_win<64>(r, nact, livem, fx, fy, nrt, tid0, lane, pcx[0], pcy[0], pcx[1], pcy[1]) : actor_search<64>(r, nact, livem, fx, fy, nrt, lane); break;
+    case 32: best = CBEV_ACTOR_WINDOW ? actor_search_win<32>(r, nact, livem, fx, fy, nrt, tid0, lane, pcx[0], pcy[0], pcx[1], pcy[1]) : actor_search<32>(r, nact, livem, fx, fy, nrt, lane); break;
+    case 16: best = CBEV_ACTOR_WINDOW ? actor_search_win<16>(r, nact, livem, fx, fy, nrt, tid0, lane, pcx[0], pcy[0], pcx[1], pcy[1]) : actor_search<16>(r, nact, livem, fx, fy, nrt, lane); break;
+    case 8: best = CBEV_ACTOR_WINDOW ? actor_search_win<8>(r, nact, livem, fx, fy, nrt, tid0, lane, pcx[0], pcy[0], pcx[1], pcy[1]) : actor_search<8>(r, nact, livem, fx, fy, nrt, lane); break;
+    case 4: best = CBEV_ACTOR_WINDOW ? actor_search_win<4>(r, nact, livem, fx, fy, nrt, tid0, lane, pcx[0], pcy[0], pcx[1], pcy[1]) : actor_search<4>(r, nact, livem, fx, fy, nrt, lane); break;
+    case 2: best = CBEV_ACTOR_WINDOW ? actor_search_win<2>(r, nact, livem, fx, fy, nrt, tid0, lane, pcx[0], pcy[0], pcx[1], pcy[1]) : actor_search<2>(r, nact, livem, fx, fy, nrt, lane); break;
     default: best = actor_search<1>(r, nact, livem, fx, fy, nrt, lane); break;  // one lane per actor: the 32-point window would not fit the registers
   }
   CBEV_STAMPW(6, 2);
