@@ -1164,6 +1164,9 @@ __device__ __forceinline__ int actor_search_win(const DRec& r, int nact, uint64_
     const int nb = (gn + BP - 1) / BP;
     const int kb = min(max(gt0 - 2, 0) / BP, max(nb - 2, 0));  // the window: blocks kb, kb + 1
     const int w0 = kb * BP, w1 = min(w0 + 2 * BP, gn);
+    // group-uniform: more blocks than the circles a lane holds, or than the
+    // candidate bits: every block outside the window is scanned
+    const bool all = nb > ACTOR_CQ * AW || nb > 32;
     float f1 = INFINITY, f2 = INFINITY, f3 = INFINITY;
     int j1 = -1, j2 = -1;
     auto track = [&](int i, float2 p) {
@@ -1196,9 +1199,7 @@ __device__ __forceinline__ int actor_search_win(const DRec& r, int nact, uint64_
         mw = o < mw ? o : mw;
       }
       const float reach = sqrtf(mw) + 0.15f + 0.05f;  // pass 1's 3 eps + float32 margins
-      if (nb > ACTOR_CQ * AW) {
-        cand = (nb >= 32 ? ~0u : ((1u << nb) - 1u)) & ~(3u << kb);
-      } else {
+      if (!all) {
 #pragma unroll
         for (int q = 0; q < ACTOR_CQ; ++q) {
           const int k = sub + q * AW;
@@ -1213,8 +1214,8 @@ __device__ __forceinline__ int actor_search_win(const DRec& r, int nact, uint64_
 #pragma unroll
     for (int off = AW / 2; off > 0; off >>= 1) cand |= (uint32_t)__shfl_xor((int)cand, off, 64);
     // round 2 (rare): the blocks whose circle comes within reach
-    for (uint32_t c = cand; c; c &= c - 1) {
-      const int k0 = BP * __builtin_ctz(c);
+    auto scan_block = [&](int k) {
+      const int k0 = BP * k;
       float2 pb[BPL];
 #pragma unroll
       for (int u = 0; u < BPL; ++u) pb[u] = cf[min(k0 + sub + u * AW, gn - 1)];
@@ -1223,6 +1224,13 @@ __device__ __forceinline__ int actor_search_win(const DRec& r, int nact, uint64_
         const int i = k0 + sub + u * AW;
         if (u * AW + sub < BP && i < gn) track(i, pb[u]);
       }
+    };
+    if (all) {
+      if (glive)
+        for (int k = 0; k < nb; ++k)
+          if (k != kb && k != kb + 1) scan_block(k);
+    } else {
+      for (uint32_t c = cand; c; c &= c - 1) scan_block(__builtin_ctz(c));
     }
     float mf = f1;
 #pragma unroll
@@ -1259,7 +1267,7 @@ __device__ __forceinline__ int actor_search_win(const DRec& r, int nact, uint64_
     };
     if (glive && f3 <= thr) {  // three or more candidates in this lane: its scanned points in float64, in index order
       for (int kk = 0; kk < nb; ++kk) {
-        if (!(kk == kb || kk == kb + 1 || ((cand >> kk) & 1u))) continue;
+        if (!(all || kk == kb || kk == kb + 1 || ((cand >> (kk & 31)) & 1u))) continue;
         for (int i = kk * BP + sub; i < min(kk * BP + BP, gn); i += AW) exact(i);
       }
     } else if (glive) {

@@ -480,6 +480,35 @@ def test_parity_wide_actor_kernel():
     run_parity(["jaywalk"], 24, 80, seed0=30_000, caps=CAPS_WIDE)
 
 
+def _long_route_edit(recs, layout, P):
+    """Actor slots 0-3 of every record on 600-point out-and-back routes (300
+    points east along the start's row, then back beside it, half a point
+    shifted): 38 blocks of 16 points, more than the 10 circles a lane holds at 2
+    lanes per actor and than the 32 candidate bits. Slots 0-1 return 0.25 px
+    beside the outbound leg, so the first minimum is soon on the return leg's
+    last blocks (the reference's whole-route scan); slots 2-3 return 3 px away
+    and drive the outbound leg."""
+    from carlabev_env_amd.scene_pack import ActorSpec, init_actor_slot
+    for e in range(len(recs)):
+        v = LY.RecordView(recs[e], layout)
+        rng = np.random.default_rng(7000 + e)
+        for a in range(min(int(v.hi[LY.HI["NACT"]]), 4)):
+            x0, y0 = float(v.ad[LY.AD["X"], a]), float(v.ad[LY.AD["Y"], a])
+            n = 300
+            rx = [x0 + i for i in range(n)] + [x0 + n - 0.5 - i for i in range(n)]
+            ry = [y0] * n + [y0 + (0.25 if a < 2 else 3.0)] * n
+            init_actor_slot(v, a, ActorSpec("vehicle", rx, ry, 8.0), rng)
+
+
+def test_parity_long_actor_routes():
+    """k_actors' windowed search on routes with more blocks than its circles
+    (actor route capacity 640, 25 vehicles: 2 lanes per actor): every block
+    outside the window is scanned in the second round, blocks past the 32nd
+    included (stanley_controller.py:100-123 scans the whole route)."""
+    caps = LY.Caps(128, 25, 640, 4)
+    run_parity(["rt_hard_v1"], 8, 40, seed0=61_000, caps=caps, edit=_long_route_edit)
+
+
 def _sample_envs(n, k=160):
     """>= k env ids spread over the batch: a stride over all of it plus the
     workgroup / env-block / XCD-round boundaries (16-env staged workgroups, 64-env
