@@ -506,11 +506,13 @@ def main():
         passes = []
         term0 = env.termination_count()
         rows0 = env.bank_rows_used()
+        counts0 = env.reset_counts()
         for _ in range(max(1, args.repeats)):  # headline passes, no instrumentation
             reseed()
             passes.append(timed(False, False))
         pass_resets = env.termination_count() - term0
         pass_rows = env.bank_rows_used() - rows0
+        distinct_rows = int(np.unique(env.bank_rows_between(counts0, env.reset_counts(), env.bank.shape[0])).size)
         els = sorted(p[0] for p in passes)
         el = els[len(els) // 2]
         host_enq = sorted(p[2] for p in passes)[len(els) // 2]
@@ -596,9 +598,9 @@ def main():
             "bank_scenes": int(env.bank.shape[0]),
             "bank_scene_ids": (f"{BANK_GID0} + rank*{int(env.bank.shape[0])} + j: seeded scenes distinct from the "
                                f"{n} start scenes (ids rank*{n} + i)"),
-            # the device cursor's advance over the headline passes: every reset took the next bank row
+            # the resets of the headline passes (env e's j-th reset: bank row (e + j * stride) % B)
             "bank_rows_handed_out": pass_rows,
-            "distinct_bank_rows_handed_out": min(pass_rows, int(env.bank.shape[0])),
+            "distinct_bank_rows_handed_out": distinct_rows,
             "host_enqueue_ms_per_step": round(host_enq / args.steps * 1e3, 4),
             "ms_per_step_with_kernel_events": round(el_prof / args.steps * 1e3, 4),
             # per-step HIP-event spans; with no actor slots (config 2) k_actors is not launched and

@@ -58,6 +58,10 @@ def lib():
     L.cbev_reset_terminated.restype = _I
     L.cbev_bank_cursor.argtypes = [_P, _P]
     L.cbev_bank_cursor.restype = _I
+    L.cbev_reset_counts.argtypes = [_P, _P, _I]
+    L.cbev_reset_counts.restype = _I
+    L.cbev_bank_stride.argtypes = [_I]
+    L.cbev_bank_stride.restype = _I
     L.cbev_set_deferred_reset.argtypes = [_P, _I]
     L.cbev_set_deferred_reset.restype = _I
     L.cbev_reset_pending.argtypes = [_P]
@@ -107,6 +111,7 @@ def check(rc: int, what: str = "cbev call"):
 EXPORTED_SYMBOLS = ("cbev_abi_version", "cbev_params_size", "cbev_layout_of", "cbev_field_names", "cbev_last_error",
                     "cbev_create", "cbev_destroy", "cbev_set_map", "cbev_step", "cbev_reset", "cbev_bank_frames",
                     "cbev_reset_frames", "cbev_reset_masked", "cbev_reset_terminated", "cbev_bank_cursor",
+                    "cbev_reset_counts", "cbev_bank_stride",
                     "cbev_set_deferred_reset", "cbev_reset_pending", "cbev_flush",
                     "cbev_expand_obs", "cbev_vector_obs", "cbev_set_fov_mask", "cbev_set_obs_size", "cbev_resize_obs", "cbev_profile", "cbev_profile_read",
                     "cbev_profile_raster", "cbev_error_flags", "cbev_set_episode_stats", "cbev_episode_slot",

@@ -1127,7 +1127,7 @@ __device__ __forceinline__ int actor_search(const DRec& r, int nact, uint64_t li
   return best;
 }
 
-// The windowed search (CBEV_ACTOR_WINDOW): in one round of loads, the two
+// The windowed search: in one round of loads, the two
 // CBEV_ACB_PTS-point blocks from the actor's previous target index (where the
 // arg-min almost always is: the target moves a point or two a step) and the
 // pruning circles of every block of the route (acb: a circle holding the
@@ -1136,9 +1136,6 @@ __device__ __forceinline__ int actor_search(const DRec& r, int nact, uint64_t li
 // its circle comes within that reach of the front axle -- by the triangle
 // inequality no point of a skipped block is within 3 eps of the float32
 // minimum, so it is never a pass-1 candidate. Then passes 1-2 as actor_search.
-#ifndef CBEV_ACTOR_WINDOW
-#define CBEV_ACTOR_WINDOW 1
-#endif
 constexpr int ACTOR_CQ = 10;  // circles per lane held at once (routes of more blocks: every block scanned)
 template <int AW>
 __device__ __forceinline__ int actor_search_win(const DRec& r, int nact, uint64_t livem, double fx, double fy,
@@ -1405,12 +1402,12 @@ __global__ __launch_bounds__(256) void k_actors(KArgs K, uint8_t* __restrict__ r
   const int aw = nact <= 1 ? 64 : nact <= 2 ? 32 : nact <= 4 ? 16 : nact <= 8 ? 8 : nact <= 16 ? 4 : nact <= 32 ? 2 : 1;
   int best;
   switch (aw) {
-    case 64: best = CBEV_ACTOR_WINDOW ? actor_search_win<64>(r, nact, livem, fx, fy, nrt, tid0, lane, pcx[0], pcy[0], pcx[1], pcy[1]) : actor_search<64>(r, nact, livem, fx, fy, nrt, lane); break;
-    case 32: best = CBEV_ACTOR_WINDOW ? actor_search_win<32>(r, nact, livem, fx, fy, nrt, tid0, lane, pcx[0], pcy[0], pcx[1], pcy[1]) : actor_search<32>(r, nact, livem, fx, fy, nrt, lane); break;
-    case 16: best = CBEV_ACTOR_WINDOW ? actor_search_win<16>(r, nact, livem, fx, fy, nrt, tid0, lane, pcx[0], pcy[0], pcx[1], pcy[1]) : actor_search<16>(r, nact, livem, fx, fy, nrt, lane); break;
-    case 8: best = CBEV_ACTOR_WINDOW ? actor_search_win<8>(r, nact, livem, fx, fy, nrt, tid0, lane, pcx[0], pcy[0], pcx[1], pcy[1]) : actor_search<8>(r, nact, livem, fx, fy, nrt, lane); break;
-    case 4: best = CBEV_ACTOR_WINDOW ? actor_search_win<4>(r, nact, livem, fx, fy, nrt, tid0, lane, pcx[0], pcy[0], pcx[1], pcy[1]) : actor_search<4>(r, nact, livem, fx, fy, nrt, lane); break;
-    case 2: best = CBEV_ACTOR_WINDOW ? actor_search_win<2>(r, nact, livem, fx, fy, nrt, tid0, lane, pcx[0], pcy[0], pcx[1], pcy[1]) : actor_search<2>(r, nact, livem, fx, fy, nrt, lane); break;
+    case 64: best = actor_search_win<64>(r, nact, livem, fx, fy, nrt, tid0, lane, pcx[0], pcy[0], pcx[1], pcy[1]); break;
+    case 32: best = actor_search_win<32>(r, nact, livem, fx, fy, nrt, tid0, lane, pcx[0], pcy[0], pcx[1], pcy[1]); break;
+    case 16: best = actor_search_win<16>(r, nact, livem, fx, fy, nrt, tid0, lane, pcx[0], pcy[0], pcx[1], pcy[1]); break;
+    case 8: best = actor_search_win<8>(r, nact, livem, fx, fy, nrt, tid0, lane, pcx[0], pcy[0], pcx[1], pcy[1]); break;
+    case 4: best = actor_search_win<4>(r, nact, livem, fx, fy, nrt, tid0, lane, pcx[0], pcy[0], pcx[1], pcy[1]); break;
+    case 2: best = actor_search_win<2>(r, nact, livem, fx, fy, nrt, tid0, lane, pcx[0], pcy[0], pcx[1], pcy[1]); break;
     default: best = actor_search<1>(r, nact, livem, fx, fy, nrt, lane); break;  // one lane per actor: the 32-point window would not fit the registers
   }
   CBEV_STAMPW(6, 2);
@@ -2125,10 +2122,7 @@ __global__ __launch_bounds__(256) void k_bank_frames(KArgs K, const uint8_t* __r
 // XCD's env blocks and counts the selected envs' pieces in env order, taking
 // every WPX-th.
 #define RESET_PU 4                      // 16-byte loads per thread in flight (8: 12.1 vs 12.5 us at config 3, the step no faster)
-#ifndef RESET_MASK_WGS
-#define RESET_MASK_WGS 512              // k_reset_mask's grid cap (and its cursor copies)
-#endif
-#define CBEV_CURSOR_STRIDE 16           // 128 bytes between the cursor copies
+#define RESET_MASK_WGS 512              // k_reset_mask's grid cap
 #define CBEV_RESET_MASK_MAX_N (1 << 20)  // k_reset_mask's unit masks: 2 B per 16 envs of LDS
 #define RESET_PIECE (4096 * RESET_PU)   // bytes per piece
 __host__ __device__ __forceinline__ int reset_pieces(int64_t bytes) {
@@ -2201,13 +2195,16 @@ __global__ __launch_bounds__(256) void k_reset_copy(KArgs K, uint8_t* __restrict
 }
 
 // Canonical-loop reset (reset(reset_mask=terminated), tools/debug_env.py:56-132)
-// from a bank with cached reset frames: every env with mask[e] != 0 takes the
-// next bank row in env-id order, bank[(cursor + k) % n_bank] for the k-th
-// selected env, so consecutive resets walk the whole bank (every reset a
-// distinct scene until it wraps) whatever order the kernels ran in. The mask is
+// from a bank with cached reset frames: every env with mask[e] != 0 takes its
+// next bank row, bank_row_of(e, j) = (e + j * stride) % n_bank for its j-th
+// reset (j = seq[e].x, the env's resets so far; stride coprime with n_bank, so
+// each env walks the whole bank before a scene repeats for it). The row of an
+// env depends on nothing outside that env (round 6: no global cursor, so the
+// reset folded into k_ego needs no other workgroup's mask bytes). The mask is
 // read when the reset runs (cbev_reset_terminated passes the last step's term
 // buffer, so in-place edits of it between the step and the reset count).
-// Ranking, once per workgroup and independent of how many envs are selected:
+// Ranking (which envs are selected, to deal their copies over the grid), once
+// per workgroup and independent of how many envs are selected:
 // the mask is cut into 16-byte units, each thread takes `upt` consecutive
 // units (16-byte loads, all in flight), keeps each unit's nonzero bits in LDS
 // and its count; one workgroup exclusive scan gives every thread's first slot.
@@ -2215,15 +2212,13 @@ __global__ __launch_bounds__(256) void k_reset_copy(KArgs K, uint8_t* __restrict
 // 256 thread prefixes, the unit within the thread and the set bit within the
 // unit: O(n / 4096 + log) per workgroup, no pass over the selected envs per
 // piece. Pieces as in k_reset_copy (16 KB, RESET_PU loads per thread in
-// flight), dealt over the grid. The cursor lives on the device only, one copy
-// per possible workgroup (RESET_MASK_WGS slots, a 128-byte line each): workgroup
-// w reads slot w at its start and, since every workgroup counts the same
-// selected total, writes cursor + total back to its own slots (w, w + grid, ...)
-// at its end. No workgroup touches another's slot, so there is no ordering
-// between workgroups to arrange and no atomic (a ticket counter taken by all 512
-// workgroups cost 4.5 us per call); graph replays hand out fresh rows, and rows
-// advance only when a reset runs. The leading scalar arguments are preloaded
-// into SGPRs.
+// flight), dealt over the grid. An env's pieces are copied by different
+// workgroups, which all read seq[e].x before any of them moves it: each piece
+// ends with one acquire-release increment of seq[e].y (pieces done), and the
+// piece that completes the env advances seq[e].x and clears seq[e].y, after every
+// other piece's read. The sequence lives on the device only: graph replays hand
+// out fresh rows, and rows advance only when a reset runs. The leading scalar
+// arguments are preloaded into SGPRs.
 __device__ __forceinline__ uint32_t nonzero_bytes16(const uint4 v) {  // bit b: byte b of the 16 is nonzero
   uint32_t m = 0;
   const uint32_t w[4] = {v.x, v.y, v.z, v.w};
@@ -2235,9 +2230,12 @@ __device__ __forceinline__ uint32_t nonzero_bytes16(const uint4 v) {  // bit b: 
   return m;
 }
 
-__global__ __launch_bounds__(256) void k_reset_mask(int n, int n_bank, int rb, int SS, int n_frames, int upt,
-                                                    const uint8_t* __restrict__ mask,
-                                                    unsigned long long* __restrict__ cursor,
+__device__ __forceinline__ int bank_row_of(int e, uint32_t j, uint32_t stride, int n_bank) {
+  return (int)(((uint64_t)e + (uint64_t)j * stride) % (uint64_t)n_bank);
+}
+__global__ __launch_bounds__(256) void k_reset_mask(int n, int n_bank, uint32_t stride, int rb, int SS, int n_frames,
+                                                    int upt, const uint8_t* __restrict__ mask,
+                                                    uint32_t* __restrict__ seq,
                                                     uint8_t* __restrict__ recs, const uint8_t* __restrict__ bank,
                                                     const uint8_t* __restrict__ bank_frames,
                                                     uint8_t* __restrict__ ring, KArgs K) {
@@ -2246,7 +2244,6 @@ __global__ __launch_bounds__(256) void k_reset_mask(int n, int n_bank, int rb, i
   int* wsum = pre + 257;                     // [4] wave totals
   uint16_t* um = (uint16_t*)(lds + 1056);    // [256 * upt] unit masks
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const unsigned long long cur = cursor[CBEV_CURSOR_STRIDE * blockIdx.x];  // this workgroup's copy, beside the mask
   const int nu = (n + 15) >> 4;               // 16-byte units
   const bool vec = ((uintptr_t)mask & 15u) == 0;
   int cnt = 0;
@@ -2296,7 +2293,8 @@ __global__ __launch_bounds__(256) void k_reset_mask(int n, int n_bank, int rb, i
       m = um[++u];
     }
     const int e = 16 * u + nth_set_bit(m, j);
-    const int b = (int)((cur + (unsigned long long)slot) % (unsigned long long)n_bank);
+    const uint32_t js = seq[2 * (int64_t)e];  // the env's resets so far (moved only once all its pieces read it)
+    const int b = bank_row_of(e, js, stride, n_bank);
     const bool fr = c < pf;  // uniform
     const uint8_t* src = fr ? bank_frames + (int64_t)b * SS : bank + (int64_t)b * rb;
     uint8_t* dst = fr ? ring + (int64_t)e * SS : recs + (int64_t)e * rb;
@@ -2321,11 +2319,15 @@ __global__ __launch_bounds__(256) void k_reset_mask(int n, int n_bank, int rb, i
       }
     }
     if (c == pf && threadIdx.x == 0 && K.stats != nullptr) K.stats[e].t0 = (double)wall_clock64();
+    __syncthreads();  // every wave's read of seq[e] has returned (its value addressed this piece's loads)
+    if (threadIdx.x == 0) {
+      const uint32_t d = __hip_atomic_fetch_add(seq + 2 * (int64_t)e + 1, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+      if (d == (uint32_t)ppe - 1) {  // the env's last piece: every other piece has read seq[e].x
+        seq[2 * (int64_t)e + 1] = 0u;
+        __hip_atomic_store(seq + 2 * (int64_t)e, js + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
   }
-  // this workgroup's cursor copies for the next call (total > 0: unchanged otherwise)
-  if (total > 0)
-    for (int w = blockIdx.x + gridDim.x * tid; w < RESET_MASK_WGS; w += gridDim.x * 256)
-      cursor[CBEV_CURSOR_STRIDE * w] = cur + (unsigned long long)total;
 }
 // k_reset_mask's dynamic LDS: prefixes + wave totals (1056 B) + the unit masks
 __host__ __forceinline__ int reset_mask_upt(int n) { return ((n + 15) / 16 + 255) / 256; }
@@ -2494,9 +2496,14 @@ __device__ __forceinline__ void d_episode_summary(const KArgs& K, const DRec& r,
   row[CBEV_EP_SECONDS] = (double)(wall_clock64() - (uint64_t)st->t0) * K.tick_s;
   row[CBEV_EP_CTX_ID] = (double)hi[CBEV_HI_CTX_ID];
   const int slot = atomicAdd(K.ep_count, 1);
-  double* o = K.ep_rows + (int64_t)slot * CBEV_EP_COUNT;
+  // a slot holds at most ep_cap rows: a step replayed from a graph (whose next-slot
+  // zeroing is the same slot every replay) keeps counting past them but never
+  // writes past its table
+  if (slot < K.ep_cap) {
+    double* o = K.ep_rows + (int64_t)slot * CBEV_EP_COUNT;
 #pragma unroll
-  for (int k = 0; k < CBEV_EP_COUNT; ++k) o[k] = row[k];
+    for (int k = 0; k < CBEV_EP_COUNT; ++k) o[k] = row[k];
+  }
   // history.append(current), deque(maxlen=200)
   const int h = st->head;
   if (wn == CBEV_STATS_HIST) {
@@ -2781,54 +2788,31 @@ __device__ __forceinline__ void butterfly(int tpe, F&& f) {
 
 // ---- the canonical reset folded into k_ego (KArgs::rmask; cbev_set_deferred_reset)
 // reset(reset_mask=terminated) between two steps (carlabev.py:96-148,
-// tools/debug_env.py:56-132) without a launch of its own: the next k_ego ranks
-// the mask (the previous step's term buffer, read when this step runs, so
-// in-place edits of it count) exactly as k_reset_mask does, the k-th selected
-// env in id order takes bank row (cursor + k) % n_bank, and each workgroup
-// stages its reset envs from their bank rows instead of their records. Every
-// workgroup loads the whole mask (n bytes) and counts the selected envs before
-// its first env and in total; the cursor copies are k_reset_mask's (slot w of
-// workgroup w, all advanced by the total).
+// tools/debug_env.py:56-132) without a launch of its own: the next k_ego reads
+// its own envs' mask bytes (the previous step's term buffer, read when this
+// step runs, so in-place edits of it count), each selected env takes
+// bank_row_of(e, seq[e]) exactly as k_reset_mask gives it and advances its
+// sequence (the workgroup owns its envs' entries), and the workgroup stages its
+// reset envs from their bank rows instead of their records. Nothing is read
+// from another workgroup's envs: the mask bytes of a workgroup's envs were
+// published by the previous step's k_raster items of the same XCD.
 __device__ __forceinline__ int P_size_sq(const KArgs& K) { return K.P.size * K.P.size; }
 struct EgoReset {
-  uint64_t bits;            // the workgroup's envs to reset (bit k: env e0 + k)
-  int base, total;          // bank row of the workgroup's first selected env; selected envs in the whole mask
+  uint64_t bits;  // the workgroup's envs to reset (bit k: env e0 + k); their bank rows in rrow[k]
 };
-// bank row of env k of the workgroup (bit k of R.bits set)
-__device__ __forceinline__ int ego_reset_row(const EgoReset& R, int k, int n_bank) {
-  return (int)((unsigned)(R.base + __popcll(R.bits & ((1ull << k) - 1ull))) % (unsigned)n_bank);
-}
-__device__ __forceinline__ EgoReset ego_reset_scan(const KArgs& K, int n, int e0, int ne_eff, int* red) {
-  // waves 0 and 1 load and count the mask (waves 2 and 3 keep their staging
-  // LDS-DMA in flight: raw barriers, no vmcnt drain)
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const unsigned long long cur = K.rcursor[CBEV_CURSOR_STRIDE * blockIdx.x];
-  if (wave < 2) {
-    const int nu = (n + 15) >> 4, u0 = e0 >> 4;
-    const bool vec = ((uintptr_t)K.rmask & 15u) == 0;
-    int cb = 0, ct = 0;
-    for (int u = tid; u < nu; u += 128) {
-      uint32_t m = 0;
-      if (vec && 16 * u + 16 <= n) {
-        m = nonzero_bytes16(*(const uint4*)(K.rmask + 16 * (int64_t)u));
-      } else {
-        for (int b = 0; b < 16; ++b)
-          if (16 * u + b < n && K.rmask[16 * (int64_t)u + b] != 0) m |= 1u << b;
-      }
-      const int c = __popc(m);
-      ct += c;
-      cb += u < u0 ? c : (u == u0 ? __popc(m & ((1u << (e0 & 15)) - 1u)) : 0);
-    }
-    const bool mine = wave == 0 && tid < ne_eff && K.rmask[e0 + tid] != 0;  // the workgroup's own envs (ne <= 64)
-    const uint64_t bits = __ballot(mine);
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      cb += __shfl_xor(cb, o, 64);
-      ct += __shfl_xor(ct, o, 64);
-    }
-    if (lane == 0) {
-      red[2 * wave] = cb;
-      red[2 * wave + 1] = ct;
+__device__ __forceinline__ EgoReset ego_reset_take(const KArgs& K, int e0, int ne_eff, int* red, int* rrow) {
+  // wave 0 (lane k: env e0 + k, ne <= 64); waves 2 and 3 keep their staging
+  // LDS-DMA in flight (a raw barrier, no vmcnt drain)
+  const int tid = threadIdx.x;
+  if (tid < 64) {
+    const bool sel = tid < ne_eff && K.rmask[e0 + tid] != 0;
+    const uint64_t bits = __ballot(sel);
+    if (sel) {
+      const int e = e0 + tid;
+      const uint32_t j = K.rseq[2 * (int64_t)e];
+      rrow[tid] = bank_row_of(e, j, K.rstride, K.rn_bank);
+      K.rseq[2 * (int64_t)e] = j + 1u;
+      if (K.stats != nullptr) K.stats[e].t0 = (double)wall_clock64();  // the episode's start
     }
     if (tid == 0) {
       red[8] = (int)(uint32_t)bits;
@@ -2837,16 +2821,7 @@ __device__ __forceinline__ EgoReset ego_reset_scan(const KArgs& K, int n, int e0
   }
   lds_barrier();
   EgoReset R;
-  const int before = red[0] + red[2];
-  R.total = red[1] + red[3];
   R.bits = (uint64_t)(uint32_t)red[8] | ((uint64_t)(uint32_t)red[9] << 32);
-  R.base = (int)((cur + (unsigned long long)before) % (unsigned long long)K.rn_bank);
-  // the reset envs' episode start
-  if (tid < ne_eff && ((R.bits >> tid) & 1u) && K.stats != nullptr) K.stats[e0 + tid].t0 = (double)wall_clock64();
-  // this workgroup's cursor copies, advanced for the next reset
-  if (R.total > 0)
-    for (int w = blockIdx.x + gridDim.x * tid; w < K.rncur; w += gridDim.x * 256)
-      K.rcursor[CBEV_CURSOR_STRIDE * w] = cur + (unsigned long long)R.total;
   lds_barrier();  // red is the collision scratch from S4 on
   return R;
 }
@@ -2902,7 +2877,11 @@ __global__ __launch_bounds__(256) void k_ego(uint8_t* __restrict__ recs, int n, 
   const int e0 = staged_env0(blockIdx.x, ne, n);
   const int ne_eff = min(ne, n - e0);
   const EgoPack pk = ego_pack(K.L);
-  uint8_t* scr = lds + ne * pk.bytes;  // [ne] collision scratch (from S4; the folded reset's scan before)
+  uint8_t* scr = lds + ne * pk.bytes;  // [ne] collision scratch (from S4; the folded reset's mask bits before)
+  const CollScratchLayout SL = coll_scratch_layout(K.C, K.L.vis_words);
+  HeroPre* pre = (HeroPre*)(scr + ne * SL.bytes);  // [ne]
+  int* best = (int*)(pre + ne);                   // [ne] target search result
+  int* rrow = best + ne;                          // [ne] a folded reset's bank row per env
   // S0: the staging first (it depends on nothing loaded, and its scalars are
   // preloaded), then the action loads and the actor prefetch, whose latency
   // overlaps the staging's. With a folded reset the records are staged
@@ -2910,11 +2889,11 @@ __global__ __launch_bounds__(256) void k_ego(uint8_t* __restrict__ recs, int n, 
   // rows once the mask is ranked.
   auto src_rec = [&](int k) -> uint8_t* { return recs + (int64_t)(e0 + k) * st_rb; };
   ego_stage_in(lds, src_rec, ne_eff > 0 ? ne_eff : 0, st_n0, st_n, st_raw_x);
-  EgoReset R{0ull, 0, 0};
-  if (K.rmask != nullptr) R = ego_reset_scan(K, n, e0, ne_eff, (int*)scr);
+  EgoReset R{0ull};
+  if (K.rmask != nullptr) R = ego_reset_take(K, e0, ne_eff, (int*)scr, rrow);
   auto src = [&](int k) -> uint8_t* {
     if (R.bits != 0ull && ((R.bits >> k) & 1ull))
-      return (uint8_t*)K.rbank + (int64_t)ego_reset_row(R, k, K.rn_bank) * st_rb;
+      return (uint8_t*)K.rbank + (int64_t)rrow[k] * st_rb;
     return recs + (int64_t)(e0 + k) * st_rb;
   };
   if (R.bits != 0ull) ego_restage(lds, src, R.bits, ne_eff, st_n0, st_n, st_raw_x);
@@ -2922,7 +2901,6 @@ __global__ __launch_bounds__(256) void k_ego(uint8_t* __restrict__ recs, int n, 
   const cbev_params& P = K.P;
   const int64_t rb = K.L.record_bytes;
   if (ne_eff <= 0) return;
-  const CollScratchLayout SL = coll_scratch_layout(K.C, K.L.vis_words);
   // the folded reset's record ranges k_ego does not write back ([cx, vis) and
   // past the vis group), bank row -> record: one 16-byte piece per thread
   // loaded now and stored at S7 (more pieces than threads: copied at S7)
@@ -2941,8 +2919,6 @@ __global__ __launch_bounds__(256) void k_ego(uint8_t* __restrict__ recs, int n, 
     rest_v = *(const uint4*)(src(rest_k) + rest_o);
     asm volatile("" ::"v"(rest_v.x), "v"(rest_v.y), "v"(rest_v.z), "v"(rest_v.w));  // issued here, not sunk to S7
   }
-  HeroPre* pre = (HeroPre*)(scr + ne * SL.bytes);  // [ne]
-  int* best = (int*)(pre + ne);                   // [ne] target search result
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   auto rec = [&](int k) { return bind_ego(lds + k * pk.bytes, src(k), K, pk); };
@@ -3105,7 +3081,7 @@ __global__ __launch_bounds__(256) void k_ego(uint8_t* __restrict__ recs, int n, 
       hero_env_render_setup(K, rr);
       // a folded reset's bank row for k_raster (the reset frame into the other ring
       // slots), beside the fast bit it reads anyway: RS_FAST bits 1.. = row + 1
-      if ((R.bits >> lane) & 1ull) rr.hi[CBEV_HI_RS_FAST] |= (ego_reset_row(R, lane, K.rn_bank) + 1) << 1;
+      if ((R.bits >> lane) & 1ull) rr.hi[CBEV_HI_RS_FAST] |= (rrow[lane] + 1) << 1;
     } else if (wave == 3) {  // the updated yaw's cos / sin for the actors' TTCs (S5)
       const double yaw = ((const double*)(lds + lane * pk.bytes + K.L.hd))[CBEV_HD_YAW];
       d_sincos(yaw, &pre[lane].syaw, &pre[lane].cyaw);
@@ -3637,9 +3613,10 @@ struct cbev_ctx {
   int ep_ring, ep_n;
   int64_t step_count;         // cbev_step calls since cbev_set_episode_stats
   double tick_s;
-  // bank cursor of cbev_reset_masked (rows taken so far): one copy per
-  // k_reset_mask workgroup, all equal between calls
-  unsigned long long* cur_dev;  // [RESET_MASK_WGS * CBEV_CURSOR_STRIDE]
+  // per-env reset sequence of cbev_reset_masked (resets so far, pieces done):
+  // env e's j-th reset takes bank row (e + j * bank_stride(n_bank)) % n_bank
+  uint32_t* seq_dev;  // [CBEV_RESET_MASK_MAX_N][2]
+  int seq_n;          // the largest n a masked reset has run on
   // cbev_set_deferred_reset: a cbev_reset_terminated recorded here and folded
   // into the next cbev_step's k_ego (KArgs::rmask), or launched as k_reset_mask
   // by the next call that would observe it (flush_pending)
@@ -3768,12 +3745,14 @@ static KArgs kargs(const cbev_ctx* c) {
   K.stats = c->stats;
   K.ep_rows = nullptr;
   K.ep_count = K.ep_count_next = nullptr;
+  K.ep_cap = 0;
   K.tick_s = c->tick_s;
   K.rmask = K.rbank = K.rbank_frames = K.term_scr = nullptr;
   K.rring = K.term_pub = nullptr;
-  K.rcursor = nullptr;
+  K.rseq = nullptr;
   K.rring_stride = 0;
-  K.rn_bank = K.rn_frames = K.rslot = K.rncur = 0;
+  K.rn_bank = K.rn_frames = K.rslot = 0;
+  K.rstride = 0;
   return K;
 }
 
@@ -3820,9 +3799,45 @@ static int flush_pending(cbev_ctx* c) {
     const int rc_ = flush_pending(c);     \
     if (rc_ != CBEV_OK) return rc_;       \
   } while (0)
-// can k_ego take the reset (no k_actors before it; its workgroups within the cursor copies)?
-static bool fold_ok(const cbev_ctx* c, int n) {
-  return c->C.actor_cap == 0 && (n + c->ego_ne - 1) / c->ego_ne <= RESET_MASK_WGS && n <= CBEV_RESET_MASK_MAX_N;
+// The folded reset's termination scratch (k_ego -> k_raster) for n envs: *ok = 1
+// once it exists; allocated only when `s` is not being captured (hipMalloc /
+// hipFree invalidate a global-mode stream capture), *ok = 0 otherwise.
+static hipError_t ensure_term_scr(cbev_ctx* c, int n, hipStream_t s, int* ok) {
+  *ok = c->scr_n >= n;
+  if (*ok) return hipSuccess;
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  hipError_t e = hipStreamIsCapturing(s, &st);
+  if (e != hipSuccess || st != hipStreamCaptureStatusNone) return e;
+  if (c->term_scr) {
+    e = hipFree(c->term_scr);
+    if (e != hipSuccess) return e;
+  }
+  c->term_scr = nullptr;
+  c->scr_n = 0;
+  e = hipMalloc(&c->term_scr, n);
+  if (e != hipSuccess) return e;
+  c->scr_n = n;
+  *ok = 1;
+  return hipSuccess;
+}
+// can k_ego take the reset (no k_actors before it)?
+static bool fold_ok(const cbev_ctx* c, int n) { return c->C.actor_cap == 0 && n <= CBEV_RESET_MASK_MAX_N; }
+static uint32_t gcd_u32(uint32_t a, uint32_t b) {
+  while (b) {
+    const uint32_t t = a % b;
+    a = b;
+    b = t;
+  }
+  return a;
+}
+// The bank stride of the masked reset (bank_row_of): the odd integer nearest
+// 0.618 n_bank that is coprime with n_bank (so env e's resets e, e + stride, ...
+// walk all n_bank rows before one repeats, and neighbouring envs start far apart)
+static uint32_t bank_stride(int n_bank) {
+  if (n_bank <= 1) return 0u;
+  uint32_t p = (uint32_t)(0.6180339887498949 * (double)n_bank) | 1u;
+  while (gcd_u32(p, (uint32_t)n_bank) != 1u) p += 2u;
+  return p % (uint32_t)n_bank;
 }
 
 
@@ -3868,9 +3883,9 @@ int cbev_create(const cbev_params* params, const cbev_caps* caps, int device, cb
   if (caps->actor_cap > 0 && caps->actor_route_cap < 2) return set_err(CBEV_EINVAL, "actor_route_cap < 2");
   if (raster_lds_bytes(P) > 160 * 1024) return set_err(CBEV_EINVAL, "crop %d needs more LDS than a CU has", P.crop);
   const cbev_layout lay = cbev_make_layout(*caps);
-  // k_ego LDS per env: packed record ranges + collision scratch + HeroPre + target index
+  // k_ego LDS per env: packed record ranges + collision scratch + HeroPre + target index + folded reset's bank row
   const int per_env = ego_pack(lay).bytes + coll_scratch_layout(*caps, lay.vis_words).bytes + (int)sizeof(HeroPre) +
-                      (int)sizeof(int);
+                      2 * (int)sizeof(int);
   const int ego_ne = ego_ne_for(per_env, caps->actor_cap);
   // k_ego stages the record prefix HD .. vis_draw as one range (EgoPack)
   if (!(lay.hd < lay.hi && lay.hi < lay.cx && lay.cx < lay.cy && lay.cy < lay.cyaw && lay.cyaw < lay.raw_x &&
@@ -3896,9 +3911,9 @@ int cbev_create(const cbev_params* params, const cbev_caps* caps, int device, cb
   if (e == hipSuccess) e = hipMemset(c->err_dev, 0, sizeof(int32_t));
   if (e == hipSuccess) e = hipMalloc(&c->nterm_dev, sizeof(unsigned long long));
   if (e == hipSuccess) e = hipMemset(c->nterm_dev, 0, sizeof(unsigned long long));
-  const size_t cur_bytes = (size_t)RESET_MASK_WGS * CBEV_CURSOR_STRIDE * sizeof(unsigned long long);
-  if (e == hipSuccess) e = hipMalloc(&c->cur_dev, cur_bytes);
-  if (e == hipSuccess) e = hipMemset(c->cur_dev, 0, cur_bytes);
+  const size_t seq_bytes = (size_t)CBEV_RESET_MASK_MAX_N * 2 * sizeof(uint32_t);
+  if (e == hipSuccess) e = hipMalloc(&c->seq_dev, seq_bytes);
+  if (e == hipSuccess) e = hipMemset(c->seq_dev, 0, seq_bytes);
   if (e == hipSuccess) {
     int khz = 0;  // wall_clock64() rate
     e = hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device);
@@ -4052,7 +4067,7 @@ void cbev_destroy(cbev_ctx* c) {
   if (c->lut_dev) (void)hipFree(c->lut_dev);
   if (c->err_dev) (void)hipFree(c->err_dev);
   if (c->nterm_dev) (void)hipFree(c->nterm_dev);
-  if (c->cur_dev) (void)hipFree(c->cur_dev);
+  if (c->seq_dev) (void)hipFree(c->seq_dev);
   if (c->area_dev) (void)hipFree(c->area_dev);
   if (c->fov_dev) (void)hipFree(c->fov_dev);
   free(c);
@@ -4125,12 +4140,13 @@ int cbev_step(cbev_ctx* c, void* records, int n, const void* actions, uint8_t* f
     const int64_t off = frames - c->pend.frames;
     fold = records == c->pend.records && n == c->pend.n && off >= 0 && off % stride == 0 &&
            off / stride < c->pend.n_frames && fold_ok(c, n);
+    // the fold's scratch: allocated when the reset was recorded, or here -- but
+    // never while the stream is being captured (a hipMalloc / hipFree there
+    // invalidates a global-mode capture): such a step launches the reset instead
     if (fold && c->scr_n < n) {
-      if (c->term_scr) HIP_TRY(hipFree(c->term_scr));
-      c->term_scr = nullptr;
-      c->scr_n = 0;
-      HIP_TRY(hipMalloc(&c->term_scr, n));
-      c->scr_n = n;
+      int ok = 0;
+      HIP_TRY(ensure_term_scr(c, n, s, &ok));
+      fold = ok != 0;
     }
     if (fold) {
       K.rmask = c->pend.mask;
@@ -4141,8 +4157,9 @@ int cbev_step(cbev_ctx* c, void* records, int n, const void* actions, uint8_t* f
       K.rn_bank = c->pend.n_bank;
       K.rn_frames = c->pend.n_frames;
       K.rslot = (int)(off / stride);
-      K.rcursor = c->cur_dev;
-      K.rncur = RESET_MASK_WGS;
+      K.rseq = c->seq_dev;
+      K.rstride = bank_stride(c->pend.n_bank);
+      if (n > c->seq_n) c->seq_n = n;
       K.term_scr = c->term_scr;
       K.term_pub = term;
       ego_term = c->term_scr;
@@ -4164,6 +4181,7 @@ int cbev_step(cbev_ctx* c, void* records, int n, const void* actions, uint8_t* f
     K.ep_rows = c->ep_rows + (int64_t)slot * c->ep_n * CBEV_EP_COUNT;
     K.ep_count = c->ep_counts + slot;
     K.ep_count_next = c->ep_counts + next;
+    K.ep_cap = c->ep_n;
     c->step_count += 1;
   }
   hipLaunchKernelGGL(k_ego, dim3((n + c->ego_ne - 1) / c->ego_ne), dim3(256), (size_t)c->ego_lb, s,
@@ -4259,8 +4277,10 @@ static int launch_reset_mask(cbev_ctx* c, void* records, int n, const uint8_t* m
   const int64_t pieces = (int64_t)n * ppe;
   const int grid = pieces >= RESET_MASK_WGS ? RESET_MASK_WGS : (int)pieces;
   const int upt = reset_mask_upt(n);
+  if (n > c->seq_n) c->seq_n = n;
   hipLaunchKernelGGL(k_reset_mask, dim3(grid), dim3(256), reset_mask_lds(n), (hipStream_t)stream, n, n_bank,
-                     (int)c->L.record_bytes, SS, n_frames, upt, mask, c->cur_dev, (uint8_t*)records, (const uint8_t*)bank, bank_frames, frames, K);
+                     bank_stride(n_bank), (int)c->L.record_bytes, SS, n_frames, upt, mask, c->seq_dev,
+                     (uint8_t*)records, (const uint8_t*)bank, bank_frames, frames, K);
   HIP_TRY(hipGetLastError());
   return CBEV_OK;
 }
@@ -4275,6 +4295,8 @@ int cbev_reset_terminated(cbev_ctx* c, void* records, int n, const void* bank, i
     if (n_bank <= 0) return set_err(CBEV_EINVAL, "empty bank");
     if (n_frames < 1) return set_err(CBEV_EINVAL, "n_frames < 1");
     CBEV_FLUSH(c);  // an earlier one no step took
+    int ok = 0;  // the folding step's scratch, allocated here outside any capture (cbev_step never allocates under one)
+    HIP_TRY(ensure_term_scr(c, n, (hipStream_t)stream, &ok));
     c->pend.on = 1;
     c->pend.records = records;
     c->pend.n = n;
@@ -4309,11 +4331,27 @@ int cbev_bank_cursor(cbev_ctx* c, int64_t* cursor) {
   CBEV_FLUSH(c);  // a deferred reset is applied before anything observes the state
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(hipDeviceSynchronize());  // the resets are queued on the caller's (non-blocking) stream
-  unsigned long long v = 0;
-  HIP_TRY(hipMemcpy(&v, c->cur_dev, sizeof v, hipMemcpyDeviceToHost));
-  *cursor = (int64_t)v;
+  std::vector<uint32_t> v((size_t)2 * c->seq_n);
+  if (c->seq_n > 0) HIP_TRY(hipMemcpy(v.data(), c->seq_dev, v.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  int64_t t = 0;
+  for (int e = 0; e < c->seq_n; ++e) t += v[2 * (size_t)e];
+  *cursor = t;
   return CBEV_OK;
 }
+
+int cbev_reset_counts(cbev_ctx* c, uint32_t* counts_host, int n) {
+  if (!c || !counts_host) return set_err(CBEV_EINVAL, "null argument");
+  if (n < 0 || n > CBEV_RESET_MASK_MAX_N) return set_err(CBEV_EINVAL, "n %d out of range", n);
+  CBEV_FLUSH(c);  // a deferred reset is applied before anything observes the state
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipDeviceSynchronize());
+  std::vector<uint32_t> v((size_t)2 * n);
+  if (n > 0) HIP_TRY(hipMemcpy(v.data(), c->seq_dev, v.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  for (int e = 0; e < n; ++e) counts_host[e] = v[2 * (size_t)e];
+  return CBEV_OK;
+}
+
+int cbev_bank_stride(int n_bank) { return n_bank > 0 ? (int)bank_stride(n_bank) : -1; }
 
 int cbev_expand_obs(cbev_ctx* c, const uint8_t* ring, int n, int n_frames, int head, int kind, int n_channels,
                     const uint32_t* lut_host, void* out, void* stream) {

@@ -37,22 +37,25 @@ struct KArgs {
   double* ep_rows;            // this step's summary rows [n][CBEV_EP_COUNT], first *ep_count used
   int32_t* ep_count;          // this step's row count (zeroed by the step before)
   int32_t* ep_count_next;     // the next step's row count, zeroed by this step
+  int ep_cap;                 // rows a slot holds (the n of cbev_set_episode_stats)
   double tick_s;              // seconds per wall_clock64() tick
   // The canonical reset folded into this step (cbev_set_deferred_reset: a
   // cbev_reset_terminated recorded, applied by k_ego; rmask null: none). k_ego
-  // ranks the mask, takes each reset env's record from bank row
-  // (cursor + rank) % rn_bank, copies the bank frame into the ring slots other
-  // than rslot and writes the step's termination flags to term_scr (the mask is
-  // the previous step's flags); k_raster publishes term_pub[e] = term_scr[e].
+  // reads its envs' mask bytes, takes each reset env's record from bank row
+  // (e + seq[e] * rstride) % rn_bank (and advances seq[e]), copies the bank frame
+  // into the ring slots other than rslot and writes the step's termination flags
+  // to term_scr (the mask is the previous step's flags); k_raster publishes
+  // term_pub[e] = term_scr[e].
   const uint8_t* rmask;
   const uint8_t* rbank;
   const uint8_t* rbank_frames;
   uint8_t* rring;
-  unsigned long long* rcursor;  // the cursor copies (k_reset_mask's): slot w of workgroup w
+  uint32_t* rseq;  // [n][2] per env: resets so far, pieces done (k_reset_mask's)
   const uint8_t* term_scr;
   uint8_t* term_pub;
   int64_t rring_stride;  // bytes between ring slots (n * S * S)
-  int rn_bank, rn_frames, rslot, rncur;
+  int rn_bank, rn_frames, rslot;
+  uint32_t rstride;  // bank_stride(rn_bank)
 };
 
 // class id of padded-map texel (x, y)

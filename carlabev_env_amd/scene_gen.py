@@ -5,6 +5,8 @@ What is restated from the reference, same RNG streams and draw order:
   lead_brake scenario sampler          src/scenes/scenarios/lead_brake.py:18-129
   jaywalk scenario sampler             src/scenes/scenarios/jaywalk.py:28-117
   scenario level draw                  src/managers/scene_generator.py:170-182
+      (pinned since round 6: 96 scenes of every level, the seeded level draw and
+      kwarg overrides, tests/test_lane_graph.py)
 
   random traffic (ego route, vehicles)  src/managers/scene_generator.py:196-344,
                                        src/scenes/utils.py:74-211
@@ -368,7 +370,9 @@ class SceneGenerator:
             vehicles.append(ActorSpec("vehicle", [x_center] * 6, [ry0 - i * rear_step for i in range(6)], rear_speed,
                                       {"type": "timed_brake",
                                        "params": {"start_brake_t": rbd, "decel_mps2": brake_strength}}))
-        return SceneSpec(ego_rx, ego_ry, ego_speed, ego_speed, vehicles=vehicles)
+        spec = SceneSpec(ego_rx, ego_ry, ego_speed, ego_speed, vehicles=vehicles)
+        spec.len_route_m = route_length_meters(ego_rx, ego_ry)  # compute_total_dist_m (lead_brake.py:50)
+        return spec
 
     # ------------------------------------------------------------ jaywalk
     def jaywalk(self, level: int, g: np.random.Generator, kw: dict) -> SceneSpec:
@@ -401,7 +405,9 @@ class SceneGenerator:
             rear_speed = kw.get("rear_speed", max(ego_speed - float(g.uniform(1.0, 3.0)), 4.0))
             vehicles.append(ActorSpec("vehicle", [ped_x_base] * 6, [ry0 - i * rear_step for i in range(6)],
                                       rear_speed, None))
-        return SceneSpec(ego_rx, ego_ry, ego_speed, ego_speed, vehicles=vehicles, pedestrians=peds)
+        spec = SceneSpec(ego_rx, ego_ry, ego_speed, ego_speed, vehicles=vehicles, pedestrians=peds)
+        spec.len_route_m = route_length_meters(ego_rx, ego_ry)  # compute_total_dist_m (jaywalk.py:55)
+        return spec
 
     # ------------------------------------------------------------ red light runner
     @staticmethod
@@ -554,9 +560,12 @@ class SceneGenerator:
                 ego_route_graph=options.get("ego_route_graph", "full_vehicle"),
             )
         if scene in ("lead_brake", "jaywalk", "red_light_runner"):
+            # scenario_options.setdefault("level", scenario_rng.choice([1, 2, 3, 4]))
+            # (scene_generator.py:180-183): the draw is made even when a level is given
+            drawn = bundle.scenario_rng.choice([1, 2, 3, 4])
             level = options.get("level")
             if level is None:
-                level = bundle.scenario_rng.choice([1, 2, 3, 4])
+                level = drawn
             g = bundle.scenario_np_rng
             kw = {k: v for k, v in options.items() if k not in ("scene", "level", "reset_mask")}
             if self._anchors is not None:

@@ -420,10 +420,11 @@ class CarlaBEVVectorEnv:
     def reset_terminated(self):
         """The canonical loop's reset(reset_mask=terminated) on the device: every env
         whose `term` flag is set when the launch runs (the last step's, including any
-        in-place edit of env.term since) <- the next bank rows in env-id order
-        (bank[(cursor + k) % B] for the k-th of them; the cursor walks the whole bank,
-        so every reset is a distinct scene until it wraps), reset frame into every
-        frame-stack slot. One launch, no host sync."""
+        in-place edit of env.term since) <- its next bank row (env e's j-th reset
+        takes bank[(e + j * stride) % B], stride = cbev_bank_stride(B) coprime with B,
+        so each env walks the whole bank before a scene repeats for it), reset frame
+        into every frame-stack slot. One launch (or none: folded into the next
+        step), no host sync."""
         if self.bank is None:
             raise RuntimeError("no scene bank attached")
         if not self._stepped:
@@ -457,19 +458,35 @@ class CarlaBEVVectorEnv:
         return obs.clone() if self.copy_obs else obs
 
     def bank_rows_used(self) -> int:
-        """Bank rows the cursor resets (reset_terminated, reset_from_bank without
-        bank_idx) have handed out since the env was created (synchronises); with B
-        rows, resets k .. k + B - 1 all got distinct scenes."""
+        """Bank rows the masked resets (reset_terminated, reset_from_bank without
+        bank_idx) have handed out since the env was created (synchronises)."""
         n = ctypes.c_int64()
         check(lib().cbev_bank_cursor(self._ctx, ctypes.byref(n)), "cbev_bank_cursor")
         return int(n.value)
+
+    def reset_counts(self) -> np.ndarray:
+        """Per-env counts j of those resets (uint32[N], synchronises): env e's j-th
+        took bank row (e + j * cbev_bank_stride(B)) % B."""
+        out = np.zeros(self.num_envs, np.uint32)
+        check(lib().cbev_reset_counts(self._ctx, out.ctypes.data_as(ctypes.c_void_p), self.num_envs),
+              "cbev_reset_counts")
+        return out
+
+    @staticmethod
+    def bank_rows_between(c0: np.ndarray, c1: np.ndarray, n_bank: int) -> np.ndarray:
+        """The bank rows the masked resets took between two reset_counts() readings."""
+        c0, c1 = c0.astype(np.int64), c1.astype(np.int64)
+        d = c1 - c0
+        e = np.repeat(np.arange(len(c0), dtype=np.int64), d)
+        j = np.repeat(c0, d) + (np.arange(int(d.sum()), dtype=np.int64) - np.repeat(np.cumsum(d) - d, d))
+        return (e + j * int(lib().cbev_bank_stride(n_bank))) % n_bank
 
     def reset_from_bank(self, mask: torch.Tensor | None = None, bank_idx: torch.Tensor | None = None):
         """Device-only partial reset from the scene bank, reset frame into every
         frame-stack slot. One launch, no host sync.
         Without bank_idx: the envs selected by mask (all when None; its contents as
-        the launch reads them) take the next bank rows of the device cursor in env-id
-        order (reset_terminated is this with mask = env.term).
+        the launch reads them) take their next bank rows (reset_terminated's per-env
+        rule; reset_terminated is this with mask = env.term).
         With bank_idx: env i (mask[i]) <- bank[bank_idx[i]]; the cursor is untouched."""
         if self.bank is None:
             raise RuntimeError("no scene bank attached")
@@ -689,7 +706,7 @@ class CarlaBEVVectorEnv:
         else:
             torch.cuda.default_stream(self.device).synchronize()
         slot = step % EP_RING
-        cnt = int(self._ep_counts[slot].item())
+        cnt = min(int(self._ep_counts[slot].item()), self.num_envs)  # a slot holds at most N rows
         if cnt == 0:
             return {}
         rows = self._ep_rows[slot, :cnt].cpu().numpy()

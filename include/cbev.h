@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define CBEV_ABI_VERSION 6
+#define CBEV_ABI_VERSION 7
 
 typedef struct cbev_ctx cbev_ctx;
 
@@ -74,7 +74,9 @@ int cbev_step(cbev_ctx* ctx, void* records, int n, const void* actions, uint8_t*
  * of them) and zeroes counts[(s + 1) % ring], so a slot stays readable until
  * step s + ring - 1 is queued (ring >= 3). cbev_reset / cbev_reset_frames stamp
  * each reset env's episode start on the device clock (CBEV_EP_SECONDS).
- * stats = NULL turns it off. Not stream-ordered: call it between steps. */
+ * stats = NULL turns it off. Not stream-ordered: call it between steps. A slot
+ * holds at most n rows: a step replayed from a graph (which zeroes the same next
+ * slot every replay) keeps counting in counts[] but writes no row past them. */
 int cbev_set_episode_stats(cbev_ctx* ctx, void* stats, int n, double* rows, int32_t* counts, int ring);
 /* Slot of the latest step's rows (-1 when off) and the step count. */
 int cbev_episode_slot(const cbev_ctx* ctx, int64_t* step_count);
@@ -129,10 +131,13 @@ int cbev_reset_frames(cbev_ctx* ctx, void* records, int n, const void* bank, int
 
 /* `reset(options={"reset_mask": mask})` (SyncVectorEnv.reset -> CarlaBEV.reset,
  * carlabev.py:96-148) from a bank with cached reset frames, each reset a fresh
- * bank row: the envs with mask[e] != 0 (uint8[n], read when the launch runs)
- * take the next rows of a device cursor in env-id order, the k-th selected env
- * bank[(cursor + k) % n_bank], and the cursor moves past them, so consecutive
- * resets walk the whole bank. Records and ring contents as cbev_reset_frames
+ * bank row: every env with mask[e] != 0 (uint8[n], read when the launch runs)
+ * takes bank row (e + j * cbev_bank_stride(n_bank)) % n_bank for its j-th such
+ * reset (j counted per env on the device from 0 at cbev_create; the stride is
+ * coprime with n_bank, so each env walks the whole bank before a scene repeats
+ * for it). The row of an env depends on that env alone (ABI 7; before, a global
+ * cursor dealt rows in env-id order, which made every workgroup of the folded
+ * reset read the whole mask). Records and ring contents as cbev_reset_frames
  * with those bank rows. One launch, no host sync; n <= 2^20. */
 int cbev_reset_masked(cbev_ctx* ctx, void* records, int n, const uint8_t* mask, const void* bank, int n_bank,
                       const uint8_t* bank_frames, uint8_t* frames, int n_frames, void* stream);
@@ -142,13 +147,18 @@ int cbev_reset_masked(cbev_ctx* ctx, void* records, int n, const uint8_t* mask, 
 int cbev_reset_terminated(cbev_ctx* ctx, void* records, int n, const void* bank, int n_bank,
                           const uint8_t* bank_frames, uint8_t* frames, int n_frames, void* stream);
 /* Bank rows cbev_reset_masked / cbev_reset_terminated have handed out since
- * cbev_create (synchronises the device). */
+ * cbev_create: the sum of the per-env counts (synchronises the device). */
 int cbev_bank_cursor(cbev_ctx* ctx, int64_t* cursor);
+/* The per-env counts j of those resets for envs 0 .. n-1 (synchronises). */
+int cbev_reset_counts(cbev_ctx* ctx, uint32_t* counts_host, int n);
+/* The stride of the masked reset's bank rows for a bank of n_bank rows (-1 if n_bank < 1). */
+int cbev_bank_stride(int n_bank);
 /* Deferred canonical reset (off by default). With it on, cbev_reset_terminated
  * records the reset instead of launching it, and the next cbev_step of the same
  * records and frame ring folds it into its first kernel (k_ego; the envs take
- * the same bank rows, records and ring slots end up as cbev_reset_masked leaves
- * them, the mask is read when that step runs): the canonical loop's
+ * the same bank rows and advance the same per-env counts, records and ring
+ * slots end up as cbev_reset_masked leaves them, the mask is read when that
+ * step runs): the canonical loop's
  * step -> reset(reset_mask=terminated) -> step costs no reset launch. Any other
  * call on the context that reads or writes its state (every cbev_reset* call,
  * cbev_expand_obs, cbev_vector_obs, cbev_resize_obs, cbev_pack_frames,
@@ -160,8 +170,10 @@ int cbev_bank_cursor(cbev_ctx* ctx, int64_t* cursor);
  * The deferral is host-side state, taken when cbev_step is called: a cbev_step
  * captured into a graph while a reset is pending carries the folded reset, so
  * every replay resets the envs its term buffer selects at replay time (the mask
- * ranking and the cursor advance run on the device); cbev_flush before
- * capturing a step that must not reset. */
+ * reads and the count advance run on the device); cbev_flush before capturing a
+ * step that must not reset. The fold needs a scratch buffer, allocated by
+ * cbev_reset_terminated outside any capture; a captured cbev_step never
+ * allocates: if the buffer does not exist yet it launches the reset instead. */
 int cbev_set_deferred_reset(cbev_ctx* ctx, int on);
 /* 1 when a deferred reset is recorded and not yet applied. */
 int cbev_reset_pending(const cbev_ctx* ctx);

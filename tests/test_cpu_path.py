@@ -22,7 +22,8 @@ def test_library_loads_and_exports_every_symbol():
     L = _lib.lib()
     for name in _lib.EXPORTED_SYMBOLS:
         assert hasattr(L, name), name
-    assert L.cbev_abi_version() == 6
+    assert L.cbev_abi_version() == 7
+    assert L.cbev_bank_stride(8192) % 2 == 1 and L.cbev_bank_stride(1) == 0 and L.cbev_bank_stride(0) == -1
     assert L.cbev_params_size() == ctypes.sizeof(CbevParams)
 
 

@@ -613,6 +613,145 @@ def test_full_size_config2_stats_on():
                          push=300) >= 128
 
 
+def run_full_size_folded(n_envs, steps, caps, seed0, bank_seed0, act_seed=1, distinct=96, bank_distinct=48,
+                         n_bank=1021, F=2):
+    """The headline's exact kernel variant against the oracle: bench config 2's
+    step with the device episode statistics on AND the canonical reset folded into
+    the next step (cbev_set_deferred_reset: bench.py's loop of step() +
+    reset_terminated(), carlabev.py:96-148,177-185 and deeprl/stats.py:30-148).
+    Every step the terminated envs are reset from a bank (cbev_reset_terminated,
+    then folded into the next k_ego); every third bank row starts off the road, so
+    an env reset from it terminates in the very step that takes the reset (reset
+    and terminated in consecutive steps). Every third step the caller edits the
+    records (pushes envs off the road), which flushes the pending reset first
+    (k_reset_mask): both reset paths, interleaved. The oracle copies each reset
+    env's bank row (reset_rows: the same per-env rule) and its reset frame into
+    every ring slot; frames (all ring slots), records, reward / term / trunc /
+    cause / info and each terminated env's summary row are compared per step on
+    a sampled subset, and the per-env reset counts at the end."""
+    cfg, P, padded, layout, builder = world(128, "discrete9_v1", "carl_base_v1", 0.5, caps=caps)
+    base, _ = build_records(builder, distinct, ["rt_no_traffic_v1"], seed0=seed0)
+    recs = base[np.arange(n_envs) % distinct].copy()
+    bdist, _ = build_records(builder, bank_distinct, ["rt_no_traffic_v1"], seed0=bank_seed0)
+    bank = bdist[np.arange(n_bank) % bank_distinct].copy()
+    for b in range(0, n_bank, 3):
+        LY.RecordView(bank[b], layout).hd[LY.HD["X"]] += 60.0
+    dw = DevWorld(P, padded, caps)
+    L = lib()
+    S = P.size
+    check(L.cbev_set_deferred_reset(dw.ctx, 1), "deferred")
+    d_bank = torch.from_numpy(bank).cuda()
+    bf = torch.zeros((n_bank, S, S), dtype=torch.uint8, device="cuda")
+    check(L.cbev_bank_frames(dw.ctx, ptr(d_bank), n_bank, ptr(bf), None), "bank_frames")
+    d_recs = torch.from_numpy(recs).cuda()
+    ring = torch.zeros((F, n_envs, S, S), dtype=torch.uint8, device="cuda")
+    check(L.cbev_reset(dw.ctx, ptr(d_recs), n_envs, None, 0, None, None, 0, ptr(ring), F, None), "reset")
+    orc = O.Oracle(P, padded, caps.c(), layout.record_bytes)
+    sample = _sample_envs(n_envs)
+    pos = {int(e): j for j, e in enumerate(sample)}
+    h_recs = recs[sample].copy()
+    h_ring = np.zeros((F, len(sample), S, S), np.uint8)
+    for j in range(len(sample)):
+        orc.reset_obs(h_recs[j], h_ring[0, j])
+        h_ring[1:, j] = h_ring[0, j]
+    bank_frame = {}
+
+    def frame_of(b):
+        if b not in bank_frame:
+            f = np.zeros((S, S), np.uint8)
+            orc.reset_obs(bank[b].copy(), f)
+            bank_frame[b] = f
+        return bank_frame[b]
+
+    rng = np.random.default_rng(act_seed)
+    p = np.ones(P.n_discrete)
+    p[1] += 4.0
+    acts = rng.choice(P.n_discrete, size=(steps, n_envs), p=p / p.sum()).astype(np.int32)
+    prng = np.random.default_rng(act_seed + 1)
+    rew = torch.zeros(n_envs, dtype=torch.float64, device="cuda")
+    term = torch.zeros(n_envs, dtype=torch.uint8, device="cuda")
+    trunc = torch.zeros_like(term)
+    cause = torch.zeros(n_envs, dtype=torch.int32, device="cuda")
+    info = torch.zeros((n_envs, 16), dtype=torch.float32, device="cuda")
+    st = EpisodeStatsOn(dw.ctx, n_envs)
+    seq = np.zeros(n_envs, np.int64)
+    pending = None
+    folded = flushed = reset_then_term = resets_seen = 0
+    was_reset = np.zeros(len(sample), bool)
+    for t in range(steps):
+        slot = t % F
+        edit = t % 3 == 2
+        if pending is not None:
+            if edit:  # the caller writes the records: it flushes the pending reset first (cbev.h)
+                check(L.cbev_flush(dw.ctx), "flush")
+                flushed += 1
+            else:
+                folded += L.cbev_reset_pending(dw.ctx)
+            ids, rows = reset_rows(pending, seq, n_bank)  # the oracle side of either path
+            was_reset[:] = False
+            for e, b in zip(ids.tolist(), rows.tolist()):
+                if e in pos:
+                    j = pos[e]
+                    h_recs[j] = bank[b]
+                    h_ring[:, j] = frame_of(b)
+                    was_reset[j] = True
+                    resets_seen += 1
+            pending = None
+        if edit:
+            ids = np.unique(np.concatenate([prng.choice(n_envs, size=300, replace=False), sample[t::7][:4]]))
+            sel_p = torch.from_numpy(ids).cuda()
+            h = d_recs[sel_p].cpu().numpy()
+            for k, e in enumerate(ids):
+                LY.RecordView(h[k], layout).hd[LY.HD["X"]] += 60.0
+                if int(e) in pos:
+                    LY.RecordView(h_recs[pos[int(e)]], layout).hd[LY.HD["X"]] += 60.0
+            d_recs[sel_p] = torch.from_numpy(h).cuda()
+        a = torch.from_numpy(np.ascontiguousarray(acts[t])).cuda()
+        check(L.cbev_step(dw.ctx, ptr(d_recs), n_envs, ptr(a), ptr(ring[slot]), ptr(rew), ptr(term), ptr(trunc),
+                          ptr(cause), ptr(info), None), "step")
+        h_cause = np.array([orc.step_one(h_recs[j], np.ascontiguousarray(acts[t, e]), h_ring[slot, j])
+                            for j, e in enumerate(sample)], np.int32)
+        torch.cuda.synchronize()
+        assert L.cbev_reset_pending(dw.ctx) == 0
+        sel = torch.from_numpy(sample).cuda()
+        dg = ring[:, sel].cpu().numpy()
+        bad = np.argwhere(dg != h_ring)
+        assert bad.size == 0, (t, "ring", bad[:4])
+        dr = d_recs[sel].cpu().numpy()
+        for j, e in enumerate(sample):
+            compare_records(dr[j], h_recs[j], layout, tag=(t, int(e)))
+        views = [LY.RecordView(h_recs[j], layout) for j in range(len(sample))]
+        tn = term.cpu().numpy()
+        assert np.array_equal(tn[sample], [v.i("TERM") for v in views]), t
+        assert np.array_equal(trunc[sel].cpu().numpy(), [v.i("TRUNC") for v in views]), t
+        assert np.array_equal(cause[sel].cpu().numpy(), h_cause), t
+        assert np.allclose(rew[sel].cpu().numpy(), [v.h("REWARD") for v in views], rtol=1e-9, atol=1e-12), t
+        got, want = info[sel].cpu().numpy(), np.stack([info_of(v, 0) for v in views])
+        assert np.array_equal(got[:, 13:], want[:, 13:]) and np.allclose(got, want, rtol=1e-6, atol=1e-6), t
+        st.check(t, tn, sample, views, h_cause)
+        reset_then_term += int(np.sum(was_reset & (tn[sample] != 0)))
+        pending = tn.astype(bool)
+        check(L.cbev_reset_terminated(dw.ctx, ptr(d_recs), n_envs, ptr(d_bank), n_bank, ptr(bf), ptr(ring), F, None),
+              "reset_terminated")
+    check(L.cbev_flush(dw.ctx), "flush")
+    reset_rows(pending, seq, n_bank)
+    assert np.array_equal(_counts(L, dw, n_envs), seq)
+    assert error_flags(dw.ctx) == 0
+    assert folded >= steps // 2 and flushed >= 2, (folded, flushed)
+    assert st.rows_seen > 0 and resets_seen > 0 and reset_then_term > 0, (st.rows_seen, resets_seen, reset_then_term)
+
+
+def test_full_size_config2_stats_folded_reset():
+    """The bench's headline variant (statistics on + the folded reset) at config
+    2's batch and capacities, against the oracle (run_full_size_folded)."""
+    run_full_size_folded(4096, 15, bench_caps(2), 10_000, 14_000)
+
+
+def test_stats_folded_reset_small():
+    """The same at an odd batch (partial k_ego workgroups) and a 3-slot ring."""
+    run_full_size_folded(45, 24, bench_caps(2), 10_200, 14_200, distinct=45, bank_distinct=17, n_bank=53, F=3)
+
+
 def test_parity_stats_on_small():
     """Every env, every step, with the episode statistics on (odd batch: partial
     k_ego workgroups), at config 2's and config 5's capacities."""
@@ -708,13 +847,23 @@ def _bank_world(n, B, F, caps, kinds, seed0, bank_seed0):
     return P, layout, dw, d_bank, bf, d_recs, ring
 
 
-def _want_reset(L, dw, d_recs, ring, d_bank, bf, mask_np, cursor, F):
-    """cbev_reset_frames with the bank rows the cursor reset hands out: the k-th
-    selected env in id order gets bank[(cursor + k) % B]."""
-    n, B = d_recs.shape[0], d_bank.shape[0]
+def reset_rows(mask_np, seq, B):
+    """The bank rows a masked reset hands out (include/cbev.h, ABI 7): env e's
+    j-th reset takes (e + j * cbev_bank_stride(B)) % B, j = seq[e]; advances seq."""
     ids = np.flatnonzero(mask_np)
+    stride = lib().cbev_bank_stride(B)
+    rows = (ids.astype(np.int64) + seq[ids].astype(np.int64) * stride) % B
+    seq[ids] += 1
+    return ids, rows
+
+
+def _want_reset(L, dw, d_recs, ring, d_bank, bf, mask_np, seq, F):
+    """cbev_reset_frames with the bank rows the masked reset hands out
+    (reset_rows); seq (the per-env reset counts) is advanced in place."""
+    n, B = d_recs.shape[0], d_bank.shape[0]
+    ids, rows = reset_rows(mask_np, seq, B)
     bidx = np.zeros(n, np.int32)
-    bidx[ids] = (cursor + np.arange(len(ids))) % B
+    bidx[ids] = rows
     want_r, want_f = d_recs.clone(), ring.clone()
     m = torch.from_numpy(mask_np.astype(np.uint8)).cuda()
     check(L.cbev_reset_frames(dw.ctx, ptr(want_r), n, ptr(d_bank), B, ptr(m), ptr(torch.from_numpy(bidx).cuda()),
@@ -728,11 +877,17 @@ def _cursor(L, dw):
     return c.value
 
 
+def _counts(L, dw, n):
+    out = np.zeros(n, np.uint32)
+    check(L.cbev_reset_counts(dw.ctx, out.ctypes.data_as(P_), n), "reset_counts")
+    return out
+
+
 def test_reset_terminated_matches_masked_reset():
     """cbev_reset_terminated (the canonical loop's reset from the last step's term
-    buffer) = cbev_reset_frames with mask = that step's terminations and bank rows
-    handed out in env-id order from the cursor: the k-th terminated env gets
-    bank[(cursor + k) % B], and the cursor moves past them."""
+    buffer) = cbev_reset_frames with mask = that step's terminations and the bank
+    rows of the per-env rule (reset_rows: env e's j-th reset takes
+    (e + j * stride) % B), and each terminated env's count moves by one."""
     n, B, F = 45, 11, 4
     P, layout, dw, d_bank, bf, d_recs, ring = _bank_world(n, B, F, bench_caps(3), ["rt_hard_v1", "rt_medium_v1"],
                                                            2100, 2900)
@@ -742,7 +897,7 @@ def test_reset_terminated_matches_masked_reset():
     trunc = torch.zeros_like(term)
     cause = torch.zeros(n, dtype=torch.int32, device="cuda")
     acts = action_stream(P, n, 12, seed=7)
-    cursor = 0
+    seq = np.zeros(n, np.int64)
     rng = np.random.default_rng(5)
     total = 0
     for t in range(12):
@@ -755,15 +910,15 @@ def test_reset_terminated_matches_masked_reset():
         check(L.cbev_step(dw.ctx, ptr(d_recs), n, ptr(a), ptr(ring[t % F]), ptr(rew), ptr(term), ptr(trunc),
                           ptr(cause), None, None), "step")
         torch.cuda.synchronize()
-        want_r, want_f, k = _want_reset(L, dw, d_recs, ring, d_bank, bf, term.cpu().numpy().astype(bool), cursor, F)
+        want_r, want_f, k = _want_reset(L, dw, d_recs, ring, d_bank, bf, term.cpu().numpy().astype(bool), seq, F)
         total += k
         check(L.cbev_reset_terminated(dw.ctx, ptr(d_recs), n, ptr(d_bank), B, ptr(bf), ptr(ring), F, None), "reset_term")
         torch.cuda.synchronize()
         assert torch.equal(d_recs, want_r), t
         assert torch.equal(ring, want_f), t
-        cursor += k
-        assert _cursor(L, dw) == cursor, t
-    assert total > 20
+        assert np.array_equal(_counts(L, dw, n), seq), t
+        assert _cursor(L, dw) == total, t
+    assert total > 20 and seq.max() > B // n + 1  # some env walked past its first bank rows
     # n must match the last step's
     assert L.cbev_reset_terminated(dw.ctx, ptr(d_recs), n - 1, ptr(d_bank), B, ptr(bf), ptr(ring), F, None) != 0
 
@@ -783,7 +938,7 @@ def test_reset_masked_mass_termination_and_edits():
     cause = torch.zeros(n, dtype=torch.int32, device="cuda")
     acts = action_stream(P, n, 6, seed=3)
     rng = np.random.default_rng(11)
-    cursor = 0
+    seq = np.zeros(n, np.int64)
 
     def step(t, push):
         h = d_recs.cpu().numpy()
@@ -799,46 +954,49 @@ def test_reset_masked_mass_termination_and_edits():
     step(0, range(n))
     m = term.cpu().numpy().astype(bool)
     assert m.sum() > n // 2
-    want_r, want_f, k = _want_reset(L, dw, d_recs, ring, d_bank, bf, m, cursor, F)
+    want_r, want_f, k = _want_reset(L, dw, d_recs, ring, d_bank, bf, m, seq, F)
     check(L.cbev_reset_terminated(dw.ctx, ptr(d_recs), n, ptr(d_bank), B, ptr(bf), ptr(ring), F, None), "reset_term")
     torch.cuda.synchronize()
     assert torch.equal(d_recs, want_r) and torch.equal(ring, want_f)
-    cursor += k
-    assert _cursor(L, dw) == cursor
-    # 2: a step whose terminations are not reset: the cursor stays
+    assert _cursor(L, dw) == seq.sum()
+    # 2: a step whose terminations are not reset: the counts stay
     step(1, rng.choice(n, size=300, replace=False))
-    assert term.cpu().numpy().sum() > 0 and _cursor(L, dw) == cursor
+    assert term.cpu().numpy().sum() > 0 and np.array_equal(_counts(L, dw, n), seq)
     # 3: in-place edits of the term buffer before the reset
     step(2, rng.choice(n, size=700, replace=False))
     extra = torch.from_numpy((rng.random(n) < 0.05).astype(np.uint8)).cuda()
     term |= extra
     term[:17] = 0
     m = term.cpu().numpy().astype(bool)
-    want_r, want_f, k = _want_reset(L, dw, d_recs, ring, d_bank, bf, m, cursor, F)
+    want_r, want_f, k = _want_reset(L, dw, d_recs, ring, d_bank, bf, m, seq, F)
     check(L.cbev_reset_terminated(dw.ctx, ptr(d_recs), n, ptr(d_bank), B, ptr(bf), ptr(ring), F, None), "reset_term")
     torch.cuda.synchronize()
     assert torch.equal(d_recs, want_r) and torch.equal(ring, want_f)
-    cursor += k
-    assert _cursor(L, dw) == cursor
+    assert np.array_equal(_counts(L, dw, n), seq)
     # 4: cbev_reset_masked with an arbitrary mask at an odd byte offset (byte-wise mask loads)
     buf = torch.zeros(n + 3, dtype=torch.uint8, device="cuda")
     mview = buf[3:]
     mh = rng.random(n) < 0.4
     mview.copy_(torch.from_numpy(mh.astype(np.uint8) * 7))  # any nonzero byte selects
-    want_r, want_f, k = _want_reset(L, dw, d_recs, ring, d_bank, bf, mh, cursor, F)
+    want_r, want_f, k = _want_reset(L, dw, d_recs, ring, d_bank, bf, mh, seq, F)
     check(L.cbev_reset_masked(dw.ctx, ptr(d_recs), n, ptr(mview), ptr(d_bank), B, ptr(bf), ptr(ring), F, None),
           "reset_masked")
     torch.cuda.synchronize()
     assert torch.equal(d_recs, want_r) and torch.equal(ring, want_f)
-    cursor += k
-    assert _cursor(L, dw) == cursor and cursor > B  # wrapped around the bank
+    # 5: the same mask again straight away (no step between): every selected env takes its next row
+    want_r, want_f, k = _want_reset(L, dw, d_recs, ring, d_bank, bf, mh, seq, F)
+    check(L.cbev_reset_masked(dw.ctx, ptr(d_recs), n, ptr(mview), ptr(d_bank), B, ptr(bf), ptr(ring), F, None),
+          "reset_masked again")
+    torch.cuda.synchronize()
+    assert torch.equal(d_recs, want_r) and torch.equal(ring, want_f)
+    assert np.array_equal(_counts(L, dw, n), seq) and _cursor(L, dw) == seq.sum() > B  # more rows than the bank
 
 
 def test_reset_cursor_advances_under_graph_replay():
-    """The bank cursor lives on the device: a cbev_reset_terminated
-    captured once in a HIP graph and replayed hands out the next rows on every
-    replay (each replay = the eager call: the k-th selected env gets bank[(cursor +
-    k) % B]) and the cursor moves by the selected count each time."""
+    """The per-env reset counts live on the device: a
+    cbev_reset_terminated captured once in a HIP graph and replayed hands out the
+    next rows on every replay (each replay = the eager call, reset_rows) and the
+    selected envs' counts move by one each time."""
     n, B, F = 45, 17, 2
     P, layout, dw, d_bank, bf, d_recs, ring = _bank_world(n, B, F, bench_caps(2), ["rt_no_traffic_v1"], 3100, 3900)
     L = lib()
@@ -860,16 +1018,15 @@ def test_reset_cursor_advances_under_graph_replay():
             check(L.cbev_reset_terminated(dw.ctx, ptr(d_recs), n, ptr(d_bank), B, ptr(bf), ptr(ring), F,
                                           P_(torch.cuda.current_stream().cuda_stream)), "reset_term (capture)")
     torch.cuda.synchronize()
-    cursor = _cursor(L, dw)  # capture runs nothing
-    assert cursor == 0
+    assert _cursor(L, dw) == 0  # capture runs nothing
+    seq = np.zeros(n, np.int64)
     for rep in range(3):
-        want_r, want_f, k = _want_reset(L, dw, d_recs, ring, d_bank, bf, sel, cursor, F)
+        want_r, want_f, k = _want_reset(L, dw, d_recs, ring, d_bank, bf, sel, seq, F)
         g.replay()
         torch.cuda.synchronize()
         assert torch.equal(d_recs, want_r) and torch.equal(ring, want_f), rep
-        cursor += k
-        assert _cursor(L, dw) == cursor, rep
-    assert cursor > B  # wrapped: every replay took fresh rows
+        assert np.array_equal(_counts(L, dw, n), seq), rep
+    assert _cursor(L, dw) == 3 * int(sel.sum())
 
 
 def _same_records(a, b, layout):
@@ -883,9 +1040,10 @@ def _same_records(a, b, layout):
     return torch.equal(a, b)
 
 
-def _deferred_pair(n, B, F, caps, seed0, bank_seed0):
+def _deferred_pair(n, B, F, caps, seed0, bank_seed0, stats=True):
     """Two contexts on the same scenes and bank: reset_terminated launched at once
-    (A) and deferred into the next step (B, cbev_set_deferred_reset)."""
+    (A) and deferred into the next step (B, cbev_set_deferred_reset); with the
+    device episode statistics on in both (stats: the headline's k_ego variant)."""
     cfg, P, padded, layout, builder = world(caps=caps)
     recs, _ = build_records(builder, n, ["rt_no_traffic_v1"], seed0=seed0)
     bank, _ = build_records(builder, B, ["rt_no_traffic_v1"], seed0=bank_seed0)
@@ -906,14 +1064,39 @@ def _deferred_pair(n, B, F, caps, seed0, bank_seed0):
                     trunc=torch.zeros(n, dtype=torch.uint8, device="cuda"),
                     cause=torch.zeros(n, dtype=torch.int32, device="cuda"),
                     info=torch.zeros((n, 16), dtype=torch.float32, device="cuda"))
+        if stats:
+            bufs["stats"] = EpisodeStatsOn(dw.ctx, n)
         out.append((dw, d_bank, bf, d_recs, ring, bufs))
     return P, layout, out
+
+
+_T0 = slice(8 * 200 + 16, 8 * 200 + 24)  # cbev_episode_stats.t0 (the device clock at the episode's reset)
+
+
+def _same_stats(a, b, step, n):
+    """The two contexts' episode statistics after `step`: per-env accumulators
+    (all but the reset clock stamp t0), this step's summary rows (by env; all
+    columns but the elapsed SECONDS) and their count."""
+    sa, sb = a.stats.cpu().numpy(), b.stats.cpu().numpy()
+    keep = np.ones(sa.shape[1], bool)
+    keep[_T0] = False
+    if not np.array_equal(sa[:, keep], sb[:, keep]):
+        return False
+    slot = step % a.RING
+    ca, cb = min(int(a.counts[slot].item()), n), min(int(b.counts[slot].item()), n)
+    if ca != cb:
+        return False
+    ra, rb_ = a.rows[slot, :ca].cpu().numpy(), b.rows[slot, :cb].cpu().numpy()
+    ra, rb_ = ra[np.argsort(ra[:, LY.EP["ENV"]])], rb_[np.argsort(rb_[:, LY.EP["ENV"]])]
+    cols = [c for c in range(ra.shape[1]) if c != LY.EP["SECONDS"]]
+    return bool(np.array_equal(ra[:, cols], rb_[:, cols]))
 
 
 def test_deferred_reset_matches_immediate():
     """The canonical reset folded into the next step's k_ego (cbev_set_deferred_reset)
     leaves exactly the state the immediate k_reset_mask + step leave: records, every
-    frame-stack slot, reward / term / trunc / cause / info and the bank cursor, step
+    frame-stack slot, reward / term / trunc / cause / info, the episode statistics
+    (accumulators, summary rows) and the per-env reset counts, step
     after step. Covered: envs pushed off the road (resets in most steps), in-place
     edits of the term buffer between the step and the reset (the folded reset reads
     the buffer when the next step runs), a reset read straight away (cbev_flush, and
@@ -925,7 +1108,7 @@ def test_deferred_reset_matches_immediate():
         S = P.size
         acts = action_stream(P, n, 16, seed=21)
         rng = np.random.default_rng(3)
-        folded = 0
+        folded = rows_seen = 0
         for t in range(16):
             push = rng.choice(n, size=min(n, int(rng.integers(1, 9)) * max(1, n // 40)), replace=False)
             extra = torch.from_numpy((rng.random(n) < 0.03).astype(np.uint8)).cuda()
@@ -945,6 +1128,8 @@ def test_deferred_reset_matches_immediate():
             assert L.cbev_reset_pending(dB.ctx) == 0
             for k in ("rew", "term", "trunc", "cause", "info"):
                 assert torch.equal(bA[k], bB[k]), (n, t, k)
+            assert _same_stats(bA["stats"], bB["stats"], t, n), (n, t, "episode stats")
+            rows_seen += int(bA["stats"].counts[t % bA["stats"].RING].item())
             assert _same_records(rA, rB, layout), (n, t, "records")
             assert torch.equal(gA, gB), (n, t, "ring")
             if t % 5 == 4:  # no reset before the next step
@@ -973,7 +1158,83 @@ def test_deferred_reset_matches_immediate():
         (dA, _, _, rA, gA, bA), (dB, _, _, rB, gB, bB) = ctxs
         assert _same_records(rA, rB, layout) and torch.equal(gA, gB)
         assert _cursor(L, dA) == _cursor(L, dB) and _cursor(L, dA) > 0
+        assert np.array_equal(_counts(L, dA, n), _counts(L, dB, n))
         assert folded >= 3, folded  # steps that took a pending reset
+        assert rows_seen > 0
+
+
+def _graph_pair(n, B, F, seed0, bank_seed0, capture_reset):
+    """Deferred context B, one step + reset captured into a graph (capture_reset:
+    the reset_terminated inside the capture too, on a context that never
+    allocated the fold's scratch), against an eager context A with the deferral
+    off; both on the same scenes, bank and statistics."""
+    caps = bench_caps(2)
+    P, layout, ctxs = _deferred_pair(n, B, F, caps, seed0, bank_seed0)
+    L = lib()
+    (dA, bankA, bfA, rA, gA, bA), (dB, bankB, bfB, rB, gB, bB) = ctxs
+    check(L.cbev_set_deferred_reset(dA.ctx, 0), "deferred off")
+    a0 = torch.zeros(n, dtype=torch.int32, device="cuda")
+
+    def push(d_recs, every):
+        h = d_recs.cpu().numpy()
+        for e in range(0, n, every):
+            LY.RecordView(h[e], layout).hd[LY.HD["X"]] += 60.0
+        d_recs.copy_(torch.from_numpy(h))
+
+    def step(dw, d_recs, ring, b, a):
+        check(L.cbev_step(dw.ctx, ptr(d_recs), n, ptr(a), ptr(ring[0]), ptr(b["rew"]), ptr(b["term"]), ptr(b["trunc"]),
+                          ptr(b["cause"]), ptr(b["info"]), P_(torch.cuda.current_stream().cuda_stream)), "step")
+
+    def reset(dw, d_recs, ring, d_bank, bf):
+        check(L.cbev_reset_terminated(dw.ctx, ptr(d_recs), n, ptr(d_bank), B, ptr(bf), ptr(ring), F,
+                                      P_(torch.cuda.current_stream().cuda_stream)), "reset_terminated")
+
+    for ctx_ in ((dA, rA, gA, bA), (dB, rB, gB, bB)):
+        push(ctx_[1], 3)
+        step(ctx_[0], ctx_[1], ctx_[2], ctx_[3], a0)
+    torch.cuda.synchronize()
+    assert int(bA["term"].sum()) > 0
+    if not capture_reset:
+        reset(dB, rB, gB, bankB, bfB)  # recorded (and the fold's scratch allocated) before the capture
+        assert L.cbev_reset_pending(dB.ctx) == 1
+    side = torch.cuda.Stream()
+    g = torch.cuda.CUDAGraph()
+    side.wait_stream(torch.cuda.current_stream())
+    acts = torch.ones(n, dtype=torch.int32, device="cuda")
+    with torch.cuda.stream(side):
+        with torch.cuda.graph(g, stream=side):
+            if capture_reset:
+                reset(dB, rB, gB, bankB, bfB)
+            step(dB, rB, gB, bB, acts)
+    torch.cuda.synchronize()
+    for rep in range(4):
+        if rep == 2:  # more terminations between replays (flushed: nothing is pending outside the graph)
+            assert L.cbev_reset_pending(dB.ctx) == (1 if capture_reset else 0)
+            check(L.cbev_flush(dB.ctx), "flush")
+            torch.cuda.synchronize()
+            for d_recs in (rA, rB):
+                push(d_recs, 5)
+        reset(dA, rA, gA, bankA, bfA)
+        step(dA, rA, gA, bA, acts)
+        g.replay()
+        torch.cuda.synchronize()
+        for k in ("rew", "term", "trunc", "cause", "info"):
+            assert torch.equal(bA[k], bB[k]), (rep, k)
+        assert _same_records(rA, rB, layout), (rep, "records")
+        assert torch.equal(gA, gB), (rep, "ring")
+    check(L.cbev_flush(dB.ctx), "flush")
+    torch.cuda.synchronize()
+    assert np.array_equal(_counts(L, dA, n), _counts(L, dB, n)) and _cursor(L, dA) > 0
+
+
+def test_folded_step_under_graph_capture():
+    """a cbev_step captured while a reset is pending carries the
+    folded reset (each replay resets the envs the term buffer selects, then
+    steps), and a capture that records the reset itself on a fresh context (no
+    fold scratch yet) allocates nothing under the capture: its step launches the
+    reset instead. Each replay equals the eager reset_terminated + step."""
+    _graph_pair(45, 13, 2, 7100, 17100, capture_reset=False)
+    _graph_pair(45, 13, 2, 7200, 17200, capture_reset=True)
 
 
 def test_vector_env_reads_after_deferred_reset():

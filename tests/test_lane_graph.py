@@ -9,6 +9,9 @@ graphs tools/convert_graphs.py extracted from assets/Town01/*.pkl:
   - 52 seeded random-traffic scenes          scene_generator.py:95-327 (all rt_* presets,
     right/left-lane ego graphs, a route profile and an intersection/turn filter)
   - 5 red-light-runner scenes                red_light_running.py:74-245
+  - 96 lead_brake / jaywalk scenes           lead_brake.py:18-129, jaywalk.py:29-117, every level
+    (8 seeds each), the seeded level draw of build_scene (scene_generator.py:165-191)
+    and kwarg overrides (anchors, speeds, gaps, delays)
 Everything is compared exactly (the planner's arithmetic is raw/8 and the
 same float sums in the same order), including how far each RNG stream was
 advanced.
@@ -90,6 +93,50 @@ def test_red_light_runner_matches_reference(gen):
         got = [{"x": t.x, "y": t.y, "orientation": t.orientation, "state": state[t.state], "width": t.width,
                 "length": t.length} for t in spec.traffic_lights]
         assert got == case["traffic_light"]
+
+
+# our behaviour dicts (scene_pack / behavior/registry.py names) <-> the reference's objects
+_JAYWALK = {"cross": "CrossBehavior", "stop_mid": "StopMidBehavior", "yield_return": "StopReturnBehavior"}
+
+
+def _same_behavior(ours, ref):
+    if ours is None or ref is None:
+        return ours is None and ref is None
+    p = ours["params"]
+    if ours["type"] == "timed_brake":  # LeadBrakeBehavior(start_brake_t, dec_rate), behavior/lead_brake.py:1-15
+        return ref["class"] == "LeadBrakeBehavior" and p["start_brake_t"] == ref["start_brake_t"] and \
+            p["decel_mps2"] == ref["dec_rate"]
+    if ref["class"] != _JAYWALK.get(ours["type"]) or p["start_delay"] != ref["start_delay"]:
+        return False
+    return ours["type"] != "yield_return" or p["yield_duration"] == ref["stop_duration"]
+
+
+def test_lead_brake_and_jaywalk_samplers_match_reference(gen):
+    """LeadBrakeScenario.sample / JaywalkScenario.sample through build_scene: the
+    level the sampler got (drawn from scenario_rng when not given), ego route and
+    speeds, len_route, every actor's route, cruise speed and behaviour, and how
+    far scenario_np_rng (the samplers' draws; the actors' spawn jitter is drawn
+    from it later, at Actor.reset) and scenario_rng advanced."""
+    n = {"lead_brake": 0, "jaywalk": 0}
+    for case in GOLD["scenarios"]:
+        tag = (case["scene"], case["seed"], case["options"])
+        bundle = build_rng_bundle(scene_seed=case["seed"])
+        spec = gen.build_scene(dict(case["options"]), bundle)
+        assert spec.context["level"] == case["level"], tag
+        ag = case["agent"]
+        assert [float(v) for v in spec.agent_rx] == ag["rx"] and [float(v) for v in spec.agent_ry] == ag["ry"], tag
+        assert spec.initial_speed_mps == ag["speed"] and spec.target_speed_mps == ag["target_speed"], tag
+        assert spec.len_route_m == case["len_route"], tag
+        for mine, refs in ((spec.vehicles, case["vehicles"]), (spec.pedestrians, case["pedestrians"])):
+            assert len(mine) == len(refs), tag
+            for a, ref in zip(mine, refs):
+                assert [float(v) for v in a.rx] == ref["rx"] and [float(v) for v in a.ry] == ref["ry"], tag
+                assert a.speed_mps == ref["cruise_mps"], tag
+                assert _same_behavior(a.behavior, ref["behavior"]), (tag, a.behavior, ref["behavior"])
+        assert float(bundle.scenario_np_rng.random()) == case["scenario_np_next"], tag
+        assert bundle.scenario_rng.random() == case["scenario_rng_next"], tag
+        n[case["scene"]] += 1
+    assert n["lead_brake"] >= 40 and n["jaywalk"] >= 40
 
 
 def test_shortest_path_edge_cases():
