@@ -354,6 +354,63 @@ def fresh_pass(env, pool, one_step, args, world, n, device, seconds=2.0):
             "note": "per rank; resets beyond the fresh scenes reuse bank scenes (recycled)"}
 
 
+def surface_loop(cfgd, n, device, acts, pool, steps, warmup, fresh):
+    """INTEGRATION.md §1's loop verbatim on the reference surface (make_env,
+    step, reset(options={"reset_mask": done, **opts}); tools/debug_env.py:56-132):
+    obs is the fresh float32 wire observation of every step, `done` goes to the
+    host each step, the masked envs are rebuilt by the host (CarlaBEV.reset,
+    carlabev.py:96-148). fresh=False: no seeds, as the reference's loop resets, so
+    every reset is the scene of the config's seed (carlabev.py:84) and is served
+    from the builder's memo after its first build; fresh=True: each reset call
+    passes a new seed per env (reset(seed=[...], options)), so every reset
+    builds a scene nobody built before (on the BuildPool's workers)."""
+    import torch
+    from carlabev_env_amd.vector_env import make_env
+    opts = scene_options(cfgd, 0)
+    env = make_env({"env": env_config(cfgd), "num_envs": n}, device=device, caps=cfgd["caps"], reset_pool=pool)
+    t0 = time.perf_counter()
+    obs, _ = env.reset(seed=0, options=opts)
+    torch.cuda.synchronize()
+    init_s = time.perf_counter() - t0
+    calls = [0]
+
+    def run(k, t_off):
+        resets = 0
+        for t in range(k):
+            obs, rew, term, trunc, infos = env.step(acts[(t_off + t) % acts.shape[0]])
+            done = term | trunc
+            if done.any():
+                m = done.cpu().numpy()
+                resets += int(m.sum())
+                if fresh:
+                    calls[0] += 1
+                    seeds = [10_000_000 + calls[0] * n + i for i in range(n)]
+                    obs, _ = env.reset(seed=seeds, options={"reset_mask": m, **opts})
+                else:
+                    obs, _ = env.reset(options={"reset_mask": m, **opts})
+        return resets
+
+    run(warmup, 0)
+    torch.cuda.synchronize()
+    b0, h0, p0 = env.builder.builds, env.builder.memo_hits, env.pool_builds
+    t0 = time.perf_counter()
+    resets = run(steps, warmup)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    built = env.builder.builds - b0 + env.pool_builds - p0
+    out = {"value": round(n * steps / el, 1), "unit": "env-steps/s", "steps": steps, "warmup": warmup,
+           "ms_per_step": round(el / steps * 1e3, 3), "resets_per_step": round(resets / steps, 2),
+           "scenes_built": built, "memo_copies": env.builder.memo_hits - h0 - (env.pool_builds - p0),
+           "fresh_reset_frac": round(built / resets, 4) if resets else None,
+           "pool_workers": 0 if pool is None else pool.workers, "initial_reset_s": round(init_s, 2),
+           "loop": ("step(a) -> done = term | trunc -> reset(seed=[fresh per env], options={'reset_mask': done, **opts})"
+                    if fresh else "step(a) -> done = term | trunc -> reset(options={'reset_mask': done, **opts})")}
+    env.close()
+    del env, obs
+    torch.cuda.empty_cache()
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -375,6 +432,9 @@ def main():
                     help="timed passes of exactly --steps steps each (re-seeded between); value = their median")
     ap.add_argument("--no-defer-reset", action="store_true",
                     help="launch every canonical reset at once (k_reset_mask) instead of folding it into the next step")
+    ap.add_argument("--surface-steps", type=int, default=40,
+                    help="steps of the reference-surface loop legs (surface_loop, surface_loop_fresh; 0: off)")
+    ap.add_argument("--surface-workers", type=int, default=16, help="BuildPool workers for the surface-loop resets")
     ap.add_argument("--info-mode", default="full", choices=("none", "full"),
                     help="full (default, as the reference's step() always runs Stats.step, carlabev.py:226-227): "
                          "device episode statistics + a StepInfos per step (not read); none: statistics off")
@@ -396,6 +456,10 @@ def main():
     pool = None
     if args.fresh_workers > 0:  # spawned before this process touches the GPU
         pool = start_scene_pool(cfgd, args.fresh_workers, rank, world)
+    bpool = None
+    if args.surface_steps > 0 and args.surface_workers > 0:  # likewise
+        from carlabev_env_amd.scene_pool import BuildPool
+        bpool = BuildPool(env_config(cfgd).model_dump(), cfgd["caps"], workers=args.surface_workers, chunk=1)
 
     import torch
     import torch.distributed as dist
@@ -539,6 +603,10 @@ def main():
         if pool is not None:
             reseed()
             fresh = fresh_pass(env, pool, one_step, args, world, n, device)
+    surf = surf_fresh = None
+    if args.surface_steps > 0:
+        surf = surface_loop(cfgd, n, device, acts_all, bpool, args.surface_steps, 10, fresh=False)
+        surf_fresh = surface_loop(cfgd, n, device, acts_all, bpool, args.surface_steps, 10, fresh=True)
 
     S = P.size
     # per env: S^2 texels sampled + S^2 frame bytes + ego state
@@ -618,6 +686,9 @@ def main():
                          "achieved_step_events": round(n * algo_bytes / (ms3[2] * 1e-3) / 1e9, 1)},
             "with_wire_obs": None if wire_value is None else round(wire_value, 1),
             "fresh_resets": fresh,
+            # the reference surface's own loop, host scene builds included
+            "surface_loop": surf,
+            "surface_loop_fresh": surf_fresh,
             "gather_bytes_per_step": None if gatherer is None else gatherer.bytes_per_step,
             "cpu_baseline": cpu,
         }
@@ -625,6 +696,8 @@ def main():
     env.close()
     if pool is not None:
         pool.close()
+    if bpool is not None:
+        bpool.close()
     if world > 1:
         dist.destroy_process_group()
 

@@ -23,11 +23,33 @@ FLAGS = ["--offload-arch=gfx950", "-O3", "-fPIC", "-shared", "-std=c++17", "-ffp
          f"-I{os.path.join(REPO, 'include')}"]
 
 
-def needs_build() -> bool:
-    if not os.path.exists(OUT):
+# the host-only helpers of scene generation (libcbev_host.so: g++, no HIP, so
+# spawned scene-pool workers load it without touching a GPU)
+HOST_SRC = os.path.join(HERE, "csrc", "cbev_host.cpp")
+HOST_OUT = os.path.join(HERE, "libcbev_host.so")
+HOST_DEPS = [HOST_SRC, os.path.join(REPO, "include", "cbev_host.h")]
+HOST_FLAGS = ["-O2", "-fPIC", "-shared", "-std=c++17", "-ffp-contract=off", "-fno-fast-math", "-Wall",
+              f"-I{os.path.join(REPO, 'include')}"]
+
+
+def _stale(out, deps) -> bool:
+    if not os.path.exists(out):
         return True
-    t = os.path.getmtime(OUT)
-    return any(os.path.getmtime(d) > t for d in DEPS)
+    t = os.path.getmtime(out)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def needs_build() -> bool:
+    return _stale(OUT, DEPS)
+
+
+def build_host(force: bool = False, verbose: bool = False) -> str:
+    if force or _stale(HOST_OUT, HOST_DEPS):
+        cmd = [os.environ.get("CXX", "g++"), *HOST_FLAGS, "-o", HOST_OUT, HOST_SRC]
+        if verbose:
+            print(" ".join(cmd))
+        subprocess.run(cmd, check=True)
+    return HOST_OUT
 
 
 def build(force: bool = False, verbose: bool = False) -> str:
@@ -36,6 +58,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
         if verbose:
             print(" ".join(cmd))
         subprocess.run(cmd, check=True)
+    build_host(force, verbose)
     return OUT
 
 

@@ -12,6 +12,8 @@ arithmetic here, with the same libraries the reference uses:
 """
 from __future__ import annotations
 
+from collections import OrderedDict
+
 import numpy as np
 from scipy.signal import savgol_filter
 
@@ -20,9 +22,28 @@ K_GAIN = 2.0
 MAX_STEER = np.radians(30.0)
 
 
+_SMOOTH_MEMO: "OrderedDict[tuple, tuple]" = OrderedDict()
+_SMOOTH_MEMO_CAP = 64  # recent routes: a scene smooths its ego route for the profile check and again at packing
+
+
 def smooth_and_compute(ax, ay, window: int = 9, poly: int = 3):
+    """utils.py:200-269, memoised on the exact input bytes (a pure function:
+    a repeated route returns copies of the same arrays)."""
     ax = np.asarray(ax, dtype=float)
     ay = np.asarray(ay, dtype=float)
+    key = (ax.tobytes(), ay.tobytes(), int(window), int(poly))
+    hit = _SMOOTH_MEMO.get(key)
+    if hit is None:
+        hit = _smooth_and_compute(ax, ay, window, poly)
+        _SMOOTH_MEMO[key] = hit
+        if len(_SMOOTH_MEMO) > _SMOOTH_MEMO_CAP:
+            _SMOOTH_MEMO.popitem(last=False)
+    else:
+        _SMOOTH_MEMO.move_to_end(key)
+    return tuple(a.copy() for a in hit)
+
+
+def _smooth_and_compute(ax, ay, window: int, poly: int):
     if ax.size != ay.size:
         raise ValueError("ax and ay must have same length")
     d = np.hypot(np.diff(ax), np.diff(ay))

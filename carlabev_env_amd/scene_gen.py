@@ -30,6 +30,7 @@ is also what the GPU and the oracle are compared on.
 """
 from __future__ import annotations
 
+import ctypes
 import os
 
 import hashlib
@@ -123,7 +124,22 @@ def _m2s(m: float) -> float:
 
 
 def route_length_meters(rx, ry) -> float:
-    """envs/geometry.py:61-69 (segment lengths summed in order, then scaled)."""
+    """envs/geometry.py:61-69 (segment lengths hypot(dx, dy) summed in order, then
+    scaled), the sum natively (cbevh_route_length: libm hypot as np.hypot,
+    float64 additions in the same order)."""
+    if len(rx) != len(ry):
+        raise ValueError("Route coordinates mismatch.")
+    if len(rx) < 2:
+        return 0.0
+    x = np.asarray(rx, dtype=np.float64)
+    y = np.asarray(ry, dtype=np.float64)
+    p = ctypes.c_void_p
+    total = lane_graph.host_lib().cbevh_route_length(x.ctypes.data_as(p), y.ctypes.data_as(p), len(x))
+    return float(total) * MPP
+
+
+def route_length_meters_py(rx, ry) -> float:
+    """route_length_meters as the reference writes it (the tests' cross-check)."""
     if len(rx) != len(ry):
         raise ValueError("Route coordinates mismatch.")
     total = 0.0

@@ -135,6 +135,84 @@ class ScenePool:
                 p.terminate()
 
 
+def _build_worker(cfg_dict, caps, tasks, results):
+    builder, layout = make_builder(cfg_dict, caps)
+    rb = layout.record_bytes
+    while True:
+        task = tasks.get()
+        if task is None:
+            return
+        tag, items = task
+        out = np.zeros((len(items), rb), np.uint8)
+        meta = []
+        try:
+            for k, (seed, options) in enumerate(items):
+                info, _spec, ctx = builder.build(out[k], seed, options)
+                meta.append((info, ctx))
+        except Exception as exc:  # noqa: BLE001 - reported to the caller by build()
+            results.put((tag, None, f"{type(exc).__name__}: {exc}"))
+            continue
+        results.put((tag, out.tobytes(), meta))
+
+
+class BuildPool:
+    """Worker processes building the records of explicit (seed, options) resets,
+    for `CarlaBEVVectorEnv.reset` when a reset needs many distinct scenes
+    (make_env(cfg, reset_pool=BuildPool(...))). The workers are spawned, so
+    create the pool before the calling process touches the GPU (a process that
+    has initialised HIP must not start programs: the pool's workers are started
+    here, once). Each worker runs the HostResetBuilder the env runs (same config,
+    same capacities), so the records are the bytes an in-process build writes
+    (tests/test_scene_pool.py)."""
+
+    def __init__(self, cfg_dict: dict, caps: dict, workers: int = 4, chunk: int = 4):
+        from . import layout as LY
+        ctx = mp.get_context("spawn")
+        self.rb = LY.Layout.make(LY.Caps(**caps)).record_bytes
+        self.cfg_dict, self.caps, self.chunk, self.workers = dict(cfg_dict), dict(caps), max(1, chunk), workers
+        self._tasks, self._results = ctx.Queue(), ctx.Queue()
+        self._procs = [ctx.Process(target=_build_worker, args=(self.cfg_dict, self.caps, self._tasks, self._results),
+                                   daemon=True) for _ in range(workers)]
+        for p in self._procs:
+            p.start()
+        self._tag = 0
+
+    def build(self, items, timeout: float = 600.0):
+        """items: [(seed, options)] -> (uint8[k][record_bytes], [(spawn_validation, scenario_context)]),
+        in the order given; blocks until every scene is built."""
+        items = list(items)
+        out = np.zeros((len(items), self.rb), np.uint8)
+        meta = [None] * len(items)
+        pending = {}
+        for i in range(0, len(items), self.chunk):
+            self._tag += 1
+            pending[self._tag] = i
+            self._tasks.put((self._tag, items[i:i + self.chunk]))
+        deadline = time.perf_counter() + timeout
+        while pending:
+            try:
+                tag, data, m = self._results.get(timeout=max(0.1, deadline - time.perf_counter()))
+            except queue.Empty:
+                raise TimeoutError(f"BuildPool: {len(pending)} chunks not built in {timeout:.0f} s") from None
+            if tag not in pending:
+                continue  # a chunk of an earlier, failed call
+            i = pending.pop(tag)
+            if data is None:
+                raise RuntimeError(f"scene build worker failed: {m}")
+            k = len(m)
+            out[i:i + k] = np.frombuffer(data, np.uint8).reshape(k, self.rb)
+            meta[i:i + k] = m
+        return out, meta
+
+    def close(self):
+        for _ in self._procs:
+            self._tasks.put(None)
+        for p in self._procs:
+            p.join(timeout=10)
+            if p.is_alive():
+                p.terminate()
+
+
 def build_scenes(cfg_dict: dict, caps: dict, difficulty: str, seed0: int, record_bytes: int, gids,
                  workers: int = 8, timeout: float = 1800.0) -> np.ndarray:
     """Packed records of the scenes of `gids` (uint8[len(gids)][record_bytes], in

@@ -91,7 +91,9 @@ class StepInfos(Mapping):
 
     __slots__ = ("_env", "_step", "_stream", "_d", "__weakref__")
 
-    def __init__(self, env, step: int, stream: int):
+    def __init__(self, env, step: int, stream):
+        # stream: the torch Stream the step was queued on, held (not its raw
+        # handle) so reading the infos never synchronises a destroyed stream
         self._env, self._step, self._stream, self._d = env, step, stream, None
 
     def _get(self) -> dict:
@@ -118,7 +120,7 @@ class CarlaBEVVectorEnv:
 
     def __init__(self, cfg, *, num_envs: int | None = None, device=None, caps: dict | None = None,
                  info_mode: str = "full", scene_generator=None, wrappers: bool = True, copy_obs: bool = True,
-                 defer_reset: bool = True):
+                 defer_reset: bool = True, reset_pool=None):
         """wrappers=False gives the base `CarlaBEV` observation of every env, as a
         `SyncVectorEnv` of unwrapped `CarlaBEV(cfg)` would: (S, S, 3) uint8 RGB for the
         BEV modes, float32[7] for obs_mode="vector" (carlabev.py:233-244, spaces.py:54-61).
@@ -132,7 +134,18 @@ class CarlaBEVVectorEnv:
         defer_reset=True (default) lets reset_terminated() fold into the next step's
         first kernel (cbev_set_deferred_reset): every accessor of the env's state
         (records, ring, term, frames(), observations, render, the bank calls) applies a
-        recorded reset first, so what the caller observes is unchanged."""
+        recorded reset first, so what the caller observes is unchanged. It takes
+        effect only when the records have no actor slots (caps actor_cap == 0:
+        k_ego is the step's first kernel) and no resize is configured; otherwise
+        reset_terminated() launches at once. A tensor taken from records / ring /
+        term before reset_terminated() shows the pre-reset state until the next
+        step or accessor applies it.
+
+        reset_pool: a scene_pool.BuildPool (created before this process touched the
+        GPU) that builds the distinct scenes a reset(options) needs in worker
+        processes; records are byte-identical to the in-process build. Built scenes
+        are memoised either way (HostResetBuilder), so a repeated (seed, options)
+        reset, such as the reference's canonical loop without seeds, is a copy."""
         if isinstance(cfg, RunConfig):
             raw = cfg
         elif isinstance(cfg, dict) and "env" in cfg:
@@ -241,6 +254,8 @@ class CarlaBEVVectorEnv:
         self.single_action_space.seed(seed)
         self.generator = scene_generator or SceneGenerator(self.cfg, self.cfg.map_name)
         self.builder = HostResetBuilder(self.cfg, self.classes, self.params, self.layout, self.generator)
+        self.reset_pool = reset_pool
+        self.pool_builds = 0  # scenes reset() had the pool build
         self.scene_context = [dict() for _ in range(N)]
         # scenario contexts by id (records carry CTX_ID): bank rows' ids stay, an env's
         # host-reset id is released at its next host reset
@@ -558,6 +573,19 @@ class CarlaBEVVectorEnv:
         host = self._new_record_buffer(max(len(idx), 1))
         spawn_infos = []
         self._flush_pending(all_=True)  # contexts released below may still be read
+        if self.reset_pool is not None and len(idx) > 1:
+            # the distinct scenes not memoised yet, built by the pool's workers and
+            # memoised here; the loop below then copies them
+            todo = {}
+            for i in idx.tolist():
+                key = self.builder.memo_key(seeds[i], options)
+                if key is not None and key not in todo and self.builder.memo_get(key) is None:
+                    todo[key] = i
+            if len(todo) > 1:
+                recs, meta = self.reset_pool.build([(seeds[i], options) for i in todo.values()])
+                for key, rec, (info, ctx) in zip(todo, recs, meta):
+                    self.builder.memo_put(key, rec, info, None, ctx)
+                self.pool_builds += len(todo)
         for k, i in enumerate(idx):
             info, spec, ctx = self.builder.build(host[k], seeds[i], options)
             spawn_infos.append(info)
@@ -677,9 +705,18 @@ class CarlaBEVVectorEnv:
         from the device only when accessed; {} otherwise."""
         if self.info_mode != "full":
             return {}
-        infos = StepInfos(self, self._ep_step - 1, self._step_stream)
+        infos = StepInfos(self, self._ep_step - 1, self._step_stream_obj())
         self._pending.append((self._ep_step - 1, weakref.ref(infos)))
         return infos
+
+    def _step_stream_obj(self):
+        """The torch Stream of the last step (its raw handle kept by step_async_only)."""
+        if not self._step_stream:
+            return None
+        cur = torch.cuda.current_stream(self.device)
+        if cur.cuda_stream == self._step_stream:
+            return cur
+        return torch.cuda.ExternalStream(self._step_stream, device=self.device)
 
     def _flush_pending(self, all_: bool = False):
         """Read the StepInfos whose device rows the next step would recycle (or all,
@@ -691,18 +728,18 @@ class CarlaBEVVectorEnv:
             if obj is not None:
                 obj._get()
 
-    def _materialize_infos(self, step: int, stream: int = 0) -> dict:
+    def _materialize_infos(self, step: int, stream=None) -> dict:
         """Vector-env infos of `step` from its device rows (SyncVectorEnv._add_info
         layout: {"episode_info": {key: array, "_key": mask}, "_episode_info": mask,
         "episode": {"r", "l", "t"} + masks, "_episode": mask}; {} when no env
         terminated). The scenario context is merged as carlabev.py:181-182 does.
-        Waits for the stream the step was launched on (`stream`, its raw handle;
-        0: the legacy default stream), not the whole device: RCCL gathers and the
+        Waits for the stream the step was launched on (`stream`, a torch Stream
+        the StepInfos holds; None: the legacy default stream), not the whole device: RCCL gathers and the
         caller's other streams keep running. A step's rows stay valid until
         EP_RING - 1 newer steps are queued, and _flush_pending reads them before
         that, so a step enqueues no event or other marker for its infos."""
-        if stream:
-            torch.cuda.ExternalStream(stream, device=self.device).synchronize()
+        if stream is not None:
+            stream.synchronize()
         else:
             torch.cuda.default_stream(self.device).synchronize()
         slot = step % EP_RING

@@ -139,6 +139,31 @@ def test_lead_brake_and_jaywalk_samplers_match_reference(gen):
     assert n["lead_brake"] >= 40 and n["jaywalk"] >= 40
 
 
+def test_native_search_equals_python_statement():
+    """cbevh_shortest_path (libcbev_host.so) = LaneGraph.shortest_path_py on the
+    fixture pairs and 400 more seeded pairs per graph (no-path cases included),
+    and cbevh_route_length = the reference's loop of np.hypot."""
+    from carlabev_env_amd.scene_gen import route_length_meters, route_length_meters_py
+    rng = np.random.default_rng(7)
+    nopath = 0
+    for key, g in lane_graph.planners("Town01").items():
+        pairs = [(c["source"], c["target"]) for c in GOLD["paths"] if c["graph"] == lane_graph.PLANNER_FILES[key]]
+        pairs += [(g.ids[int(a)], g.ids[int(b)]) for a, b in rng.integers(0, len(g.ids), (400, 2))]
+        for s_, t_ in pairs:
+            try:
+                want = g.shortest_path_py(s_, t_)
+            except lane_graph.NoPath:
+                nopath += 1
+                with pytest.raises(lane_graph.NoPath):
+                    g.shortest_path(s_, t_)
+                continue
+            assert g.shortest_path(s_, t_) == want, (key, s_, t_)
+            xs = [g.node_xy_surface(n)[0] for n in want]
+            ys = [g.node_xy_surface(n)[1] for n in want]
+            assert route_length_meters(xs, ys) == route_length_meters_py(xs, ys)
+    assert nopath > 0
+
+
 def test_shortest_path_edge_cases():
     g = lane_graph.planners("Town01")["vehicle-R"]
     n0 = g.ids[5]

@@ -65,3 +65,48 @@ def test_build_scenes_rejects_repeated_ids():
     _, layout = make_builder(cfg, CAPS)
     with pytest.raises(ValueError, match="repeated scene ids"):
         build_scenes(cfg, CAPS, "rt_easy_v1", 0, layout.record_bytes, [3, 5, 3], workers=1)
+
+
+def test_build_pool_matches_serial_reset_build():
+    """BuildPool (the parallel half of CarlaBEVVectorEnv.reset(options)) writes the
+    bytes, spawn validation and scenario context a serial in-process build writes
+    for the same (seed, options), in the order asked, over scene kinds with and
+    without traffic and scenario samplers."""
+    from carlabev_env_amd.scene_pool import BuildPool
+    cfg = EnvConfig(size=128, obs_size=(128, 128), render_mode="rgb_array").model_dump()
+    builder, layout = make_builder(cfg, CAPS)
+    items = [(7_000 + k, dict(scene_options(d, k))) for k, d in
+             enumerate(["rt_no_traffic_v1", "rt_medium_v1", "mix3", "rt_easy_v1", "mix3", "mix3", "rt_medium_v1"])]
+    items.append((None, dict(scene_options("rt_no_traffic_v1", 0))))  # seed None: the config's seed (carlabev.py:84)
+    pool = BuildPool(cfg, CAPS, workers=3, chunk=2)
+    try:
+        recs, meta = pool.build(items)
+    finally:
+        pool.close()
+    for k, (seed, opts) in enumerate(items):
+        want = np.zeros(layout.record_bytes, np.uint8)
+        info, _spec, ctx = builder.build(want, seed, opts)
+        assert np.array_equal(recs[k], want), k
+        assert meta[k] == (info, ctx), k
+
+
+def test_reset_build_memo_is_exact():
+    """HostResetBuilder memoises by (scene seed, options): a repeated reset copies
+    the bytes of the first build (which a fresh builder reproduces), and the
+    returned dicts are independent copies."""
+    cfg = EnvConfig(size=128, obs_size=(128, 128), render_mode="rgb_array").model_dump()
+    b1, layout = make_builder(cfg, CAPS)
+    b2, _ = make_builder(cfg, CAPS)
+    opts = dict(scene_options("rt_medium_v1", 3))
+    r1, r2, r3 = (np.zeros(layout.record_bytes, np.uint8) for _ in range(3))
+    i1, _, c1 = b1.build(r1, 5, dict(opts, reset_mask=np.ones(4, bool)))
+    i2, _, c2 = b1.build(r2, 5, opts)  # the reset mask is not part of the scene
+    b2.build(r3, 5, opts)
+    assert b1.builds == 1 and b1.memo_hits == 1
+    assert np.array_equal(r1, r2) and np.array_equal(r1, r3)
+    assert i1 == i2 and c1 == c2 and c1 is not c2
+    c2["scene"] = "edited"
+    _, _, c4 = b1.build(r2, 5, opts)
+    assert c4["scene"] != "edited"
+    b1.build(r2, 6, opts)  # another seed: built
+    assert b1.builds == 2 and not np.array_equal(r1, r2)
