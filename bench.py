@@ -432,8 +432,10 @@ def main():
                     help="timed passes of exactly --steps steps each (re-seeded between); value = their median")
     ap.add_argument("--no-defer-reset", action="store_true",
                     help="launch every canonical reset at once (k_reset_mask) instead of folding it into the next step")
-    ap.add_argument("--surface-steps", type=int, default=40,
-                    help="steps of the reference-surface loop legs (surface_loop, surface_loop_fresh; 0: off)")
+    ap.add_argument("--surface-steps", type=int, default=100,
+                    help="timed steps of the reference-surface loop legs (surface_loop, surface_loop_fresh; 0: off)")
+    ap.add_argument("--surface-warmup", type=int, default=300,
+                    help="untimed steps before them (from the initial reset to a steady reset rate)")
     ap.add_argument("--surface-workers", type=int, default=16, help="BuildPool workers for the surface-loop resets")
     ap.add_argument("--info-mode", default="full", choices=("none", "full"),
                     help="full (default, as the reference's step() always runs Stats.step, carlabev.py:226-227): "
@@ -605,8 +607,9 @@ def main():
             fresh = fresh_pass(env, pool, one_step, args, world, n, device)
     surf = surf_fresh = None
     if args.surface_steps > 0:
-        surf = surface_loop(cfgd, n, device, acts_all, bpool, args.surface_steps, 10, fresh=False)
-        surf_fresh = surface_loop(cfgd, n, device, acts_all, bpool, args.surface_steps, 10, fresh=True)
+        surf = surface_loop(cfgd, n, device, acts_all, bpool, args.surface_steps, args.surface_warmup, fresh=False)
+        surf_fresh = surface_loop(cfgd, n, device, acts_all, bpool, args.surface_steps, args.surface_warmup,
+                                  fresh=True)
 
     S = P.size
     # per env: S^2 texels sampled + S^2 frame bytes + ego state

@@ -786,15 +786,17 @@ __device__ __forceinline__ void ego_stage_in(uint8_t* lds, Src src, int ne, int 
   }
 }
 
-// the changed ranges back: HD + HI (the first pieces) and the vis group
-__device__ __forceinline__ void ego_stage_out(const uint8_t* lds, uint8_t* __restrict__ recs, int e0, int ne,
-                                              const KArgs& K, const EgoPack& p) {
+// the changed ranges back: HD + HI (the first pieces) and the vis group, from
+// each env's LDS slot (slot(k): its record's, or its bank row's after a folded reset)
+template <class Slot>
+__device__ __forceinline__ void ego_stage_out(Slot slot, uint8_t* __restrict__ recs, int e0, int ne, const KArgs& K,
+                                              const EgoPack& p) {
   const int nhh = (int)(K.L.cx / 16), nout = nhh + p.nvis;
   const int64_t rb = K.L.record_bytes;
   for (int q = threadIdx.x; q < ne * nout; q += 256) {
     const int k = q / nout, j = q - k * nout;
     const int c = j < nhh ? j : p.vis_c + (j - nhh);
-    *(uint4*)(recs + (int64_t)(e0 + k) * rb + ego_src(p.n0, p.raw_x, c)) = *(const uint4*)(lds + k * p.bytes + 16 * c);
+    *(uint4*)(recs + (int64_t)(e0 + k) * rb + ego_src(p.n0, p.raw_x, c)) = *(const uint4*)(slot(k) + 16 * c);
   }
 }
 
@@ -2805,11 +2807,11 @@ __device__ __forceinline__ EgoReset ego_reset_take(const KArgs& K, int e0, int n
   // LDS-DMA in flight (a raw barrier, no vmcnt drain)
   const int tid = threadIdx.x;
   if (tid < 64) {
-    const bool sel = tid < ne_eff && K.rmask[e0 + tid] != 0;
+    const int e = e0 + (tid < ne_eff ? tid : 0);
+    const uint32_t j = K.rseq[2 * (int64_t)e];  // loaded beside the mask byte (one round trip)
+    const bool sel = tid < ne_eff && K.rmask[e] != 0;
     const uint64_t bits = __ballot(sel);
     if (sel) {
-      const int e = e0 + tid;
-      const uint32_t j = K.rseq[2 * (int64_t)e];
       rrow[tid] = bank_row_of(e, j, K.rstride, K.rn_bank);
       K.rseq[2 * (int64_t)e] = j + 1u;
       if (K.stats != nullptr) K.stats[e].t0 = (double)wall_clock64();  // the episode's start
@@ -2826,16 +2828,15 @@ __device__ __forceinline__ EgoReset ego_reset_take(const KArgs& K, int e0, int n
   return R;
 }
 
-// the reset envs' staged ranges again, from their bank rows (waves 2 and 3,
-// the same pieces and LDS bytes as ego_stage_in): each wave waits for its own
-// first DMA, so the bank bytes land after the record's
+// the reset envs' staged ranges from their bank rows (waves 2 and 3, the pieces
+// of ego_stage_in) into the bank slots (lds = the slot region after the ne
+// record slots): no wait for the records' DMA, whose slots they do not touch
 template <class Src>
 __device__ __forceinline__ void ego_restage(uint8_t* lds, Src src, uint64_t bits, int ne, int n0, int n, int raw_x) {
   const int total = ne * n;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (wave < 2) return;
-  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's record DMA has landed
   for (int b = (wave - 2) * 64; b < total; b += 128) {
     const int q = b + lane;
     const int k = q / n, c = q - k * n;
@@ -2877,7 +2878,10 @@ __global__ __launch_bounds__(256) void k_ego(uint8_t* __restrict__ recs, int n, 
   const int e0 = staged_env0(blockIdx.x, ne, n);
   const int ne_eff = min(ne, n - e0);
   const EgoPack pk = ego_pack(K.L);
-  uint8_t* scr = lds + ne * pk.bytes;  // [ne] collision scratch (from S4; the folded reset's mask bits before)
+  // LDS: [ne] record slots, then (contexts the reset can fold into: no actor
+  // slots) [ne] bank-row slots, then the collision scratch
+  const int nslot = K.C.actor_cap == 0 ? 2 : 1;
+  uint8_t* scr = lds + nslot * ne * pk.bytes;  // [ne] collision scratch (from S4; the folded reset's mask bits before)
   const CollScratchLayout SL = coll_scratch_layout(K.C, K.L.vis_words);
   HeroPre* pre = (HeroPre*)(scr + ne * SL.bytes);  // [ne]
   int* best = (int*)(pre + ne);                   // [ne] target search result
@@ -2896,7 +2900,9 @@ __global__ __launch_bounds__(256) void k_ego(uint8_t* __restrict__ recs, int n, 
       return (uint8_t*)K.rbank + (int64_t)rrow[k] * st_rb;
     return recs + (int64_t)(e0 + k) * st_rb;
   };
-  if (R.bits != 0ull) ego_restage(lds, src, R.bits, ne_eff, st_n0, st_n, st_raw_x);
+  if (R.bits != 0ull) ego_restage(lds + ne * pk.bytes, src, R.bits, ne_eff, st_n0, st_n, st_raw_x);
+  // env k's staged ranges: its record slot, or its bank-row slot when the folded reset takes it
+  auto slot = [&](int k) -> uint8_t* { return lds + ((R.bits >> k) & 1ull ? ne + k : k) * pk.bytes; };
   CBEV_STAMP(3, 0);
   const cbev_params& P = K.P;
   const int64_t rb = K.L.record_bytes;
@@ -2921,7 +2927,7 @@ __global__ __launch_bounds__(256) void k_ego(uint8_t* __restrict__ recs, int n, 
   }
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  auto rec = [&](int k) { return bind_ego(lds + k * pk.bytes, src(k), K, pk); };
+  auto rec = [&](int k) { return bind_ego(slot(k), src(k), K, pk); };
   if (blockIdx.x == 0 && tid == 0 && K.ep_count_next != nullptr) *K.ep_count_next = 0;
   // S2 + S1 under the staging (waves 0 and 1 issue none of it, so their loads
   // are waited for precisely while the LDS-DMA of waves 2 and 3 stays in
@@ -3083,7 +3089,7 @@ __global__ __launch_bounds__(256) void k_ego(uint8_t* __restrict__ recs, int n, 
       // slots), beside the fast bit it reads anyway: RS_FAST bits 1.. = row + 1
       if ((R.bits >> lane) & 1ull) rr.hi[CBEV_HI_RS_FAST] |= (rrow[lane] + 1) << 1;
     } else if (wave == 3) {  // the updated yaw's cos / sin for the actors' TTCs (S5)
-      const double yaw = ((const double*)(lds + lane * pk.bytes + K.L.hd))[CBEV_HD_YAW];
+      const double yaw = ((const double*)(slot(lane) + K.L.hd))[CBEV_HD_YAW];
       d_sincos(yaw, &pre[lane].syaw, &pre[lane].cyaw);
     } else if (wave == 0) {
       const DRec r = rec(lane);
@@ -3259,7 +3265,7 @@ __global__ __launch_bounds__(256) void k_ego(uint8_t* __restrict__ recs, int n, 
   __syncthreads();
   CBEV_STAMP(1, 2);
   // S7
-  ego_stage_out(lds, recs, e0, ne_eff, K, pk);
+  ego_stage_out(slot, recs, e0, ne_eff, K, pk);
   if (rest_k >= 0) *(uint4*)(recs + (int64_t)(e0 + rest_k) * rb + rest_o) = rest_v;
   for (int q = threadIdx.x + 256; q < nres * rpp; q += 256) {
     int k, o;
@@ -3883,9 +3889,11 @@ int cbev_create(const cbev_params* params, const cbev_caps* caps, int device, cb
   if (caps->actor_cap > 0 && caps->actor_route_cap < 2) return set_err(CBEV_EINVAL, "actor_route_cap < 2");
   if (raster_lds_bytes(P) > 160 * 1024) return set_err(CBEV_EINVAL, "crop %d needs more LDS than a CU has", P.crop);
   const cbev_layout lay = cbev_make_layout(*caps);
-  // k_ego LDS per env: packed record ranges + collision scratch + HeroPre + target index + folded reset's bank row
-  const int per_env = ego_pack(lay).bytes + coll_scratch_layout(*caps, lay.vis_words).bytes + (int)sizeof(HeroPre) +
-                      2 * (int)sizeof(int);
+  // k_ego LDS per env: packed record ranges (twice without actor slots: the
+  // folded reset's bank-row slot) + collision scratch + HeroPre + target index +
+  // folded reset's bank row
+  const int per_env = (caps->actor_cap == 0 ? 2 : 1) * ego_pack(lay).bytes +
+                      coll_scratch_layout(*caps, lay.vis_words).bytes + (int)sizeof(HeroPre) + 2 * (int)sizeof(int);
   const int ego_ne = ego_ne_for(per_env, caps->actor_cap);
   // k_ego stages the record prefix HD .. vis_draw as one range (EgoPack)
   if (!(lay.hd < lay.hi && lay.hi < lay.cx && lay.cx < lay.cy && lay.cy < lay.cyaw && lay.cyaw < lay.raw_x &&
