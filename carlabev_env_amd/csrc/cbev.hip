@@ -2030,13 +2030,8 @@ void k_raster(KArgs K, uint8_t* __restrict__ recs, int n, uint8_t* __restrict__ 
   // items only, after the render (loads and stores there: no register is held
   // across the render for it)
   const int row = K.rbank_frames != nullptr && K.rn_frames > 1 ? (r.hi[CBEV_HI_RS_FAST] >> 1) - 1 : -1;
-  // the step's termination flags, published once k_ego's reset no longer reads
-  // the previous ones (loaded now, stored after the render)
-  const bool pub = K.term_pub != nullptr && t == 0 && threadIdx.x == 0;
-  const uint8_t tflag = pub ? K.term_scr[e] : 0;
   raster_tile<G, true, kRasterNT>(K, r, J, t, frames + e * SS, 1, 0, lds);
   if (row >= 0) raster_reset_frame<G>(K, row, e, t);
-  if (pub) K.term_pub[e] = tflag;
   CBEV_STAMP(2, 3);
 }
 
@@ -2807,11 +2802,13 @@ __device__ __forceinline__ EgoReset ego_reset_take(const KArgs& K, int e0, int n
   // LDS-DMA in flight (a raw barrier, no vmcnt drain)
   const int tid = threadIdx.x;
   if (tid < 64) {
-    const int e = e0 + (tid < ne_eff ? tid : 0);
-    const uint32_t j = K.rseq[2 * (int64_t)e];  // loaded beside the mask byte (one round trip)
+    const int e = e0 + tid;
+    // the mask bytes were written by this workgroup's envs' previous k_ego (this
+    // XCD's L2); the reset counts are read for the selected envs only (a cold line)
     const bool sel = tid < ne_eff && K.rmask[e] != 0;
     const uint64_t bits = __ballot(sel);
     if (sel) {
+      const uint32_t j = K.rseq[2 * (int64_t)e];
       rrow[tid] = bank_row_of(e, j, K.rstride, K.rn_bank);
       K.rseq[2 * (int64_t)e] = j + 1u;
       if (K.stats != nullptr) K.stats[e].t0 = (double)wall_clock64();  // the episode's start
@@ -3639,8 +3636,6 @@ struct cbev_ctx {
     int n_frames;
     void* stream;
   } pend;
-  uint8_t* term_scr;          // [scr_n] the folding step's termination flags (k_ego -> k_raster)
-  int scr_n;
   const uint8_t* last_term;   // term buffer of the last cbev_step (cbev_reset_terminated's mask)
   int last_n;                 // n of the last cbev_step (0: none yet)
 };
@@ -3753,8 +3748,8 @@ static KArgs kargs(const cbev_ctx* c) {
   K.ep_count = K.ep_count_next = nullptr;
   K.ep_cap = 0;
   K.tick_s = c->tick_s;
-  K.rmask = K.rbank = K.rbank_frames = K.term_scr = nullptr;
-  K.rring = K.term_pub = nullptr;
+  K.rmask = K.rbank = K.rbank_frames = nullptr;
+  K.rring = nullptr;
   K.rseq = nullptr;
   K.rring_stride = 0;
   K.rn_bank = K.rn_frames = K.rslot = 0;
@@ -3805,27 +3800,6 @@ static int flush_pending(cbev_ctx* c) {
     const int rc_ = flush_pending(c);     \
     if (rc_ != CBEV_OK) return rc_;       \
   } while (0)
-// The folded reset's termination scratch (k_ego -> k_raster) for n envs: *ok = 1
-// once it exists; allocated only when `s` is not being captured (hipMalloc /
-// hipFree invalidate a global-mode stream capture), *ok = 0 otherwise.
-static hipError_t ensure_term_scr(cbev_ctx* c, int n, hipStream_t s, int* ok) {
-  *ok = c->scr_n >= n;
-  if (*ok) return hipSuccess;
-  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
-  hipError_t e = hipStreamIsCapturing(s, &st);
-  if (e != hipSuccess || st != hipStreamCaptureStatusNone) return e;
-  if (c->term_scr) {
-    e = hipFree(c->term_scr);
-    if (e != hipSuccess) return e;
-  }
-  c->term_scr = nullptr;
-  c->scr_n = 0;
-  e = hipMalloc(&c->term_scr, n);
-  if (e != hipSuccess) return e;
-  c->scr_n = n;
-  *ok = 1;
-  return hipSuccess;
-}
 // can k_ego take the reset (no k_actors before it)?
 static bool fold_ok(const cbev_ctx* c, int n) { return c->C.actor_cap == 0 && n <= CBEV_RESET_MASK_MAX_N; }
 static uint32_t gcd_u32(uint32_t a, uint32_t b) {
@@ -4063,7 +4037,6 @@ int cbev_profile_raster(cbev_ctx* c, void* records, int n, uint8_t* frames, int 
 void cbev_destroy(cbev_ctx* c) {
   if (!c) return;
   c->pend.on = 0;  // a deferred reset nothing observed is dropped with the context
-  if (c->term_scr) (void)hipFree(c->term_scr);
   (void)hipSetDevice(c->device);
   if (c->prof_ev) {
     for (int i = 0; i < 4 * CBEV_PROF_MAX; ++i) (void)hipEventDestroy(c->prof_ev[i]);
@@ -4148,14 +4121,6 @@ int cbev_step(cbev_ctx* c, void* records, int n, const void* actions, uint8_t* f
     const int64_t off = frames - c->pend.frames;
     fold = records == c->pend.records && n == c->pend.n && off >= 0 && off % stride == 0 &&
            off / stride < c->pend.n_frames && fold_ok(c, n);
-    // the fold's scratch: allocated when the reset was recorded, or here -- but
-    // never while the stream is being captured (a hipMalloc / hipFree there
-    // invalidates a global-mode capture): such a step launches the reset instead
-    if (fold && c->scr_n < n) {
-      int ok = 0;
-      HIP_TRY(ensure_term_scr(c, n, s, &ok));
-      fold = ok != 0;
-    }
     if (fold) {
       K.rmask = c->pend.mask;
       K.rbank = (const uint8_t*)c->pend.bank;
@@ -4168,9 +4133,6 @@ int cbev_step(cbev_ctx* c, void* records, int n, const void* actions, uint8_t* f
       K.rseq = c->seq_dev;
       K.rstride = bank_stride(c->pend.n_bank);
       if (n > c->seq_n) c->seq_n = n;
-      K.term_scr = c->term_scr;
-      K.term_pub = term;
-      ego_term = c->term_scr;
       c->pend.on = 0;
     } else {
       CBEV_FLUSH(c);
@@ -4303,8 +4265,6 @@ int cbev_reset_terminated(cbev_ctx* c, void* records, int n, const void* bank, i
     if (n_bank <= 0) return set_err(CBEV_EINVAL, "empty bank");
     if (n_frames < 1) return set_err(CBEV_EINVAL, "n_frames < 1");
     CBEV_FLUSH(c);  // an earlier one no step took
-    int ok = 0;  // the folding step's scratch, allocated here outside any capture (cbev_step never allocates under one)
-    HIP_TRY(ensure_term_scr(c, n, (hipStream_t)stream, &ok));
     c->pend.on = 1;
     c->pend.records = records;
     c->pend.n = n;

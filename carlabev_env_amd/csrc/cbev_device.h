@@ -42,17 +42,15 @@ struct KArgs {
   // The canonical reset folded into this step (cbev_set_deferred_reset: a
   // cbev_reset_terminated recorded, applied by k_ego; rmask null: none). k_ego
   // reads its envs' mask bytes, takes each reset env's record from bank row
-  // (e + seq[e] * rstride) % rn_bank (and advances seq[e]), copies the bank frame
-  // into the ring slots other than rslot and writes the step's termination flags
-  // to term_scr (the mask is the previous step's flags); k_raster publishes
-  // term_pub[e] = term_scr[e].
+  // (e + seq[e] * rstride) % rn_bank (and advances seq[e]) and k_raster copies the
+  // bank frame into the ring slots other than rslot. A workgroup reads only its
+  // own envs' mask bytes, before it writes their termination flags, so the mask
+  // may be the term buffer this step writes.
   const uint8_t* rmask;
   const uint8_t* rbank;
   const uint8_t* rbank_frames;
   uint8_t* rring;
   uint32_t* rseq;  // [n][2] per env: resets so far, pieces done (k_reset_mask's)
-  const uint8_t* term_scr;
-  uint8_t* term_pub;
   int64_t rring_stride;  // bytes between ring slots (n * S * S)
   int rn_bank, rn_frames, rslot;
   uint32_t rstride;  // bank_stride(rn_bank)

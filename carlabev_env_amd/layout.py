@@ -193,6 +193,21 @@ def batch_views(buf: np.ndarray, layout: Layout, n: int) -> dict:
     return out
 
 
+def retreat_route_violations(hi: np.ndarray, ai: np.ndarray, caps: Caps) -> np.ndarray:
+    """Records whose StopReturn (yield_return) actor would rebuild a retreat
+    route longer than the narrow k_actors rebuilds (64 points, one per lane;
+    contexts of at most 64 actor slots): hi = int32[n][HI_COUNT], ai =
+    int32[n][AI_COUNT][A] of n records. scene_pack refuses such actors when it
+    packs a scene; this check covers records written any other way (the kernel
+    would only flag CBEV_ERR_RETREAT_ROUTE and keep the actor's old route)."""
+    if caps.actor_cap == 0 or caps.actor_cap > 64:
+        return np.zeros(hi.shape[0], bool)
+    nact = hi[:, HI["NACT"]]
+    live = np.arange(caps.actor_cap)[None, :] < nact[:, None]
+    bad = (ai[:, AI["BEH"], :] == BEH["yield_return"]) & (ai[:, AI["NRX"], :] + 1 > min(caps.actor_route_cap, 64))
+    return (bad & live).any(axis=1)
+
+
 def acb_circles(pts: np.ndarray) -> np.ndarray:
     """The pruning circles (acb) of an actor's float32 route points pts[n][2]:
     per block of ACB_PTS points, the bounding box's centre in 1/8 px fixed point

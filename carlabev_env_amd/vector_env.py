@@ -141,6 +141,14 @@ class CarlaBEVVectorEnv:
         term before reset_terminated() shows the pre-reset state until the next
         step or accessor applies it.
 
+        caps: the record capacities (layout.Caps fields). The default, DEFAULT_CAPS with
+        actor_cap >= max_vehicles + 4, holds any scene the generator makes: actor
+        routes up to 288 points (the longest lane-graph route has 276), which costs
+        about 64 * actor_cap * actor_route_cap bytes per record (about 470 KB at 29
+        actor slots) in the records, the bank and every reset copy. Ego-only scenes
+        fit caps=dict(actor_cap=0, actor_route_cap=2) (3.3 KB per env, and the reset
+        folds into the step); SceneSpec.caps_needed() gives a scene's own needs.
+
         reset_pool: a scene_pool.BuildPool (created before this process touched the
         GPU) that builds the distinct scenes a reset(options) needs in worker
         processes; records are byte-identical to the in-process build. Built scenes
@@ -313,6 +321,25 @@ class CarlaBEVVectorEnv:
     def build_reset_record(self, buf: np.ndarray, seed, options: dict, env_index: int = 0):
         return self.builder.build(buf, seed, options)
 
+    def _check_records(self, recs, what: str):
+        """Refuse device or host records a StopReturn actor of which the narrow
+        k_actors could not retreat (layout.retreat_route_violations)."""
+        if self.caps.actor_cap == 0 or self.caps.actor_cap > 64:
+            return
+        o = self.layout.off
+        nhi, nai = 4 * len(LY.HI), 4 * len(LY.AI) * self.caps.actor_cap
+        if isinstance(recs, torch.Tensor):
+            hi = recs[:, o["hi"]:o["hi"] + nhi].cpu().numpy()
+            ai = recs[:, o["ai"]:o["ai"] + nai].cpu().numpy()
+        else:
+            hi, ai = recs[:, o["hi"]:o["hi"] + nhi], recs[:, o["ai"]:o["ai"] + nai]
+        hi = np.ascontiguousarray(hi).view(np.int32).reshape(len(hi), len(LY.HI))
+        ai = np.ascontiguousarray(ai).view(np.int32).reshape(len(ai), len(LY.AI), self.caps.actor_cap)
+        bad = np.flatnonzero(LY.retreat_route_violations(hi, ai, self.caps))
+        if bad.size:
+            raise ValueError(f"{what}: record {int(bad[0])} (of {bad.size}) has a yield_return actor whose retreat "
+                             f"route would exceed min(actor_route_cap, 64) points (scene_pack refuses such actors)")
+
     def _mask_array(self, mask) -> np.ndarray:
         if mask is None:
             return np.ones(self.num_envs, dtype=bool)
@@ -329,6 +356,7 @@ class CarlaBEVVectorEnv:
         without per-reset host work."""
         if bank_records.device != self.device or bank_records.dtype != torch.uint8 or bank_records.shape[1] != self.rb:
             raise ValueError("bank must be a (B, record_bytes) uint8 tensor on the env device")
+        self._check_records(bank_records, "attach_bank")
         self.flush()  # a deferred reset reads the old bank
         self.bank = bank_records.contiguous()
         self.bank_contexts = contexts
@@ -361,6 +389,7 @@ class CarlaBEVVectorEnv:
             return slot0
         if records.shape[1] != self.rb or k > B:
             raise ValueError(f"expected at most {B} records of {self.rb} bytes")
+        self._check_records(records, "refresh_bank")
         if contexts is not None:
             if len(contexts) != k:
                 raise ValueError(f"{len(contexts)} contexts for {k} records")
@@ -543,6 +572,7 @@ class CarlaBEVVectorEnv:
         if records.device != self.device or records.dtype != torch.uint8 or tuple(records.shape) != (N, self.rb):
             raise ValueError(f"expected a ({N}, {self.rb}) uint8 tensor on {self.device}")
         records = records.contiguous()
+        self._check_records(records, "load_scenes")
         dst = self.full if self.resize else self.ring
         check(lib().cbev_reset(self._ctx, _ptr(self.records), N, _ptr(records), N, None, None, 0, _ptr(dst),
                                1 if self.resize else self.F, self._stream()), "cbev_reset")

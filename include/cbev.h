@@ -171,9 +171,8 @@ int cbev_bank_stride(int n_bank);
  * captured into a graph while a reset is pending carries the folded reset, so
  * every replay resets the envs its term buffer selects at replay time (the mask
  * reads and the count advance run on the device); cbev_flush before capturing a
- * step that must not reset. The fold needs a scratch buffer, allocated by
- * cbev_reset_terminated outside any capture; a captured cbev_step never
- * allocates: if the buffer does not exist yet it launches the reset instead. */
+ * step that must not reset. Neither call allocates (safe under a global-mode
+ * stream capture). */
 int cbev_set_deferred_reset(cbev_ctx* ctx, int on);
 /* 1 when a deferred reset is recorded and not yet applied. */
 int cbev_reset_pending(const cbev_ctx* ctx);

@@ -208,3 +208,24 @@ def test_acb_circles_hold_their_blocks():
             q = pts[LY.ACB_PTS * b: LY.ACB_PTS * (b + 1)].astype(np.float64)
             d = np.hypot(q[:, 0] - c[0], q[:, 1] - c[1])
             assert d.max() <= w1 / 8.0 and w1 / 8.0 <= d.max() + 0.25 + 1e-9
+
+
+def test_retreat_route_check_flags_long_stop_return_routes():
+    """records whose yield_return actor has a route the narrow k_actors
+    cannot retreat along (more than 63 points) are found before they reach the
+    device (CarlaBEVVectorEnv.attach_bank / refresh_bank / load_scenes refuse
+    them); scene_pack's own records never are."""
+    caps = LY.Caps(64, 4, 288, 4)
+    cfg, P, padded, layout, builder = world(caps=caps)
+    recs, _ = build_records(builder, 6, ["mix3"], seed0=30_000)
+    o = layout.off
+    hi = recs[:, o["hi"]:o["hi"] + 4 * len(LY.HI)].copy().view(np.int32)
+    ai = recs[:, o["ai"]:o["ai"] + 4 * len(LY.AI) * 4].copy().view(np.int32).reshape(6, len(LY.AI), 4)
+    assert not LY.retreat_route_violations(hi, ai, caps).any()
+    ai[2, LY.AI["BEH"], 0] = LY.BEH["yield_return"]
+    ai[2, LY.AI["NRX"], 0] = 64
+    hi[2, LY.HI["NACT"]] = max(hi[2, LY.HI["NACT"]], 1)
+    got = LY.retreat_route_violations(hi, ai, caps)
+    assert got.tolist() == [False, False, True, False, False, False]
+    # the wide kernel (more than 64 actor slots) rebuilds any retreat serially: nothing to refuse
+    assert not LY.retreat_route_violations(hi, ai, LY.Caps(64, 72, 128, 0)).any()

@@ -1166,9 +1166,8 @@ def test_deferred_reset_matches_immediate():
 
 def _graph_pair(n, B, F, seed0, bank_seed0, capture_reset):
     """Deferred context B, one step + reset captured into a graph (capture_reset:
-    the reset_terminated inside the capture too, on a context that never
-    allocated the fold's scratch), against an eager context A with the deferral
-    off; both on the same scenes, bank and statistics."""
+    the reset_terminated inside the capture too), against an eager context A with
+    the deferral off; both on the same scenes, bank and statistics."""
     caps = bench_caps(2)
     P, layout, ctxs = _deferred_pair(n, B, F, caps, seed0, bank_seed0)
     L = lib()
@@ -1231,9 +1230,9 @@ def _graph_pair(n, B, F, seed0, bank_seed0, capture_reset):
 def test_folded_step_under_graph_capture():
     """a cbev_step captured while a reset is pending carries the
     folded reset (each replay resets the envs the term buffer selects, then
-    steps), and a capture that records the reset itself on a fresh context (no
-    fold scratch yet) allocates nothing under the capture: its step launches the
-    reset instead. Each replay equals the eager reset_terminated + step."""
+    steps), also when the capture records the reset itself on a fresh context
+    (nothing is allocated under the capture). Each replay equals the eager
+    reset_terminated + step."""
     _graph_pair(45, 13, 2, 7100, 17100, capture_reset=False)
     _graph_pair(45, 13, 2, 7200, 17200, capture_reset=True)
 
