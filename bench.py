@@ -432,8 +432,9 @@ def main():
                     help="timed passes of exactly --steps steps each (re-seeded between); value = their median")
     ap.add_argument("--no-defer-reset", action="store_true",
                     help="launch every canonical reset at once (k_reset_mask) instead of folding it into the next step")
-    ap.add_argument("--surface-steps", type=int, default=100,
-                    help="timed steps of the reference-surface loop legs (surface_loop, surface_loop_fresh; 0: off)")
+    ap.add_argument("--surface-steps", type=int, default=None,
+                    help="timed steps of the reference-surface loop legs (surface_loop, surface_loop_fresh; "
+                         "0: off; default 100 at config 2, off elsewhere)")
     ap.add_argument("--surface-warmup", type=int, default=300,
                     help="untimed steps before them (from the initial reset to a steady reset rate)")
     ap.add_argument("--surface-workers", type=int, default=16, help="BuildPool workers for the surface-loop resets")
@@ -453,6 +454,8 @@ def main():
         return dry_run(args, world, rank)
 
     cfgd = CONFIGS[args.config]
+    if args.surface_steps is None:
+        args.surface_steps = 100 if args.config == 2 else 0
     n = args.envs or cfgd["envs"]
     scenes = build_scene_sets(cfgd, n, rank, args.scene_cache)  # host workers, before the GPU is touched
     pool = None

@@ -11,7 +11,7 @@ tail -1 gpurun_out/bench_cfg$CFG.json
 OUT=gpurun_out/prof$CFG
 mkdir -p $OUT
 export TMPDIR=/tmp
-ARGS="--config $CFG --steps 30 --warmup 3 --no-cpu-baseline --no-wire --fresh-workers 0 --raster-reps 5 --scene-cache $CACHE"
+ARGS="--config $CFG --steps 30 --warmup 3 --no-cpu-baseline --no-wire --fresh-workers 0 --surface-steps 0 --raster-reps 5 --scene-cache $CACHE"
 run() {
   local name=$1; shift
   timeout -k 10 400 rocprofv3 "$@" -d $OUT/$name -o $name --output-format csv -- python bench.py $ARGS > $OUT/$name.log 2>&1

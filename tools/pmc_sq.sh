@@ -10,7 +10,7 @@ export TMPDIR=/tmp
 CACHE=/tmp/cbev_scene_cache
 run() {
   n=$1; shift
-  timeout -s KILL 200 rocprofv3 --kernel-trace --pmc "$@" -d gpurun_out/pm/$n -o $n --output-format csv -- python bench.py --config $CFG --steps 20 --warmup 3 --no-cpu-baseline --no-wire --fresh-workers 0 --raster-reps 5 --scene-cache $CACHE > gpurun_out/pm/$n.log 2>&1 || { tail -3 gpurun_out/pm/$n.log; exit 1; }
+  timeout -s KILL 200 rocprofv3 --kernel-trace --pmc "$@" -d gpurun_out/pm/$n -o $n --output-format csv -- python bench.py --config $CFG --steps 20 --warmup 3 --no-cpu-baseline --no-wire --fresh-workers 0 --surface-steps 0 --raster-reps 5 --scene-cache $CACHE > gpurun_out/pm/$n.log 2>&1 || { tail -3 gpurun_out/pm/$n.log; exit 1; }
   f=$(find gpurun_out/pm/$n -name "*counter_collection.csv" | head -1)
   python - "$f" <<'PY' >> gpurun_out/pm/sq_summary.jsonl
 import csv, sys, collections, json
