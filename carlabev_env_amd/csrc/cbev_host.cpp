@@ -17,6 +17,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <vector>
+
 #include "cbev_host.h"
 
 namespace {
@@ -67,6 +69,38 @@ struct Heap {
   ~Heap() { free(a); }
 };
 
+// The search's per-node state, kept per thread between calls: entries count as
+// set only when their stamp is this call's generation, so nothing is cleared
+// per call (the graphs have a few thousand nodes; a search settles a fraction)
+struct Workspace {
+  std::vector<uint32_t> settled[2], seen_at[2];
+  std::vector<double> seen[2];
+  std::vector<int32_t> parent[2], walk;
+  Heap fringe[2];
+  uint32_t gen = 0;
+  void prepare(int n) {
+    if ((int)walk.size() < n) {
+      for (int d = 0; d < 2; ++d) {
+        settled[d].assign(n, 0u);
+        seen_at[d].assign(n, 0u);
+        seen[d].resize(n);
+        parent[d].resize(n);
+      }
+      walk.resize(n);
+      gen = 0;
+    }
+    if (++gen == 0) {  // wrapped: clear the stamps once
+      for (int d = 0; d < 2; ++d) {
+        std::fill(settled[d].begin(), settled[d].end(), 0u);
+        std::fill(seen_at[d].begin(), seen_at[d].end(), 0u);
+      }
+      gen = 1;
+    }
+    fringe[0].n = fringe[1].n = 0;
+  }
+};
+thread_local Workspace g_ws;
+
 }  // namespace
 
 extern "C" {
@@ -81,42 +115,23 @@ int cbevh_shortest_path(int n, const int32_t* succ_off, const int32_t* succ_idx,
     path[0] = s;
     return 1;
   }
-  // per side: settled distance flag, seen distance (+ flag), parent
-  uint8_t* settled[2];
-  uint8_t* seenf[2];
-  double* seen[2];
-  int32_t* parent[2];
-  int32_t* walk = nullptr;
-  void* block = calloc((size_t)n, 2 * (2 * sizeof(uint8_t) + sizeof(double) + sizeof(int32_t)) + sizeof(int32_t));
-  if (!block) return CBEVH_ENOMEM;
-  {
-    uint8_t* p = (uint8_t*)block;
-    for (int d = 0; d < 2; ++d) {
-      seen[d] = (double*)p;
-      p += sizeof(double) * (size_t)n;
-    }
-    for (int d = 0; d < 2; ++d) {
-      parent[d] = (int32_t*)p;
-      p += sizeof(int32_t) * (size_t)n;
-    }
-    walk = (int32_t*)p;
-    p += sizeof(int32_t) * (size_t)n;
-    for (int d = 0; d < 2; ++d) {
-      settled[d] = p;
-      p += n;
-      seenf[d] = p;
-      p += n;
-    }
-  }
+  Workspace& W = g_ws;
+  W.prepare(n);
+  const uint32_t G = W.gen;
+  uint32_t* settled[2] = {W.settled[0].data(), W.settled[1].data()};
+  uint32_t* seen_at[2] = {W.seen_at[0].data(), W.seen_at[1].data()};
+  double* seen[2] = {W.seen[0].data(), W.seen[1].data()};
+  int32_t* parent[2] = {W.parent[0].data(), W.parent[1].data()};
+  int32_t* walk = W.walk.data();
   const int32_t* off[2] = {succ_off, pred_off};
   const int32_t* idx[2] = {succ_idx, pred_idx};
   const double* cost[2] = {succ_cost, pred_cost};
-  Heap fringe[2];
+  Heap* fringe = W.fringe;
   seen[0][s] = 0.0;
-  seenf[0][s] = 1;
+  seen_at[0][s] = G;
   parent[0][s] = -1;
   seen[1][t] = 0.0;
-  seenf[1][t] = 1;
+  seen_at[1][t] = G;
   parent[1][t] = -1;
   int rc = CBEVH_NOPATH;
   if (!fringe[0].push({0.0, 0, s}) || !fringe[1].push({0.0, 1, t})) rc = CBEVH_ENOMEM;
@@ -129,26 +144,26 @@ int cbevh_shortest_path(int n, const int32_t* succ_off, const int32_t* succ_idx,
     d = 1 - d;
     const Key k = fringe[d].pop();
     const int v = k.node;
-    if (settled[d][v]) continue;
-    settled[d][v] = 1;
-    if (settled[1 - d][v]) {  // the searches met: the best path recorded so far
+    if (settled[d][v] == G) continue;
+    settled[d][v] = G;
+    if (settled[1 - d][v] == G) {  // the searches met: the best path recorded so far
       rc = have_final ? final_len : CBEVH_NOPATH;
       break;
     }
     for (int e = off[d][v]; e < off[d][v + 1]; ++e) {
       const int w = idx[d][e];
       const double vw = k.dist + cost[d][e];
-      if (settled[d][w]) continue;  // non-negative costs: never shorter
-      if (!seenf[d][w] || vw < seen[d][w]) {
+      if (settled[d][w] == G) continue;  // non-negative costs: never shorter
+      if (seen_at[d][w] != G || vw < seen[d][w]) {
         seen[d][w] = vw;
-        seenf[d][w] = 1;
+        seen_at[d][w] = G;
         if (!fringe[d].push({vw, counter, w})) {
           rc = CBEVH_ENOMEM;
           break;
         }
         counter += 1;
         parent[d][w] = v;
-        if (seenf[0][w] && seenf[1][w]) {
+        if (seen_at[0][w] == G && seen_at[1][w] == G) {
           const double total = seen[0][w] + seen[1][w];
           if (!have_final || final_dist > total) {
             // walk(parent[0], w)[::-1] + walk(parent[1], w)[1:]
@@ -178,8 +193,33 @@ int cbevh_shortest_path(int n, const int32_t* succ_off, const int32_t* succ_idx,
       }
     }
   }
-  free(block);
   return rc;
+}
+
+int cbevh_find_path(int n, const int32_t* succ_off, const int32_t* succ_idx, const double* succ_cost,
+                    const int32_t* pred_off, const int32_t* pred_idx, const double* pred_cost, int s, int t,
+                    const double* pos_xy, double threshold, int32_t* path, int cap, int32_t* merged) {
+  const int len = cbevh_shortest_path(n, succ_off, succ_idx, succ_cost, pred_off, pred_idx, pred_cost, s, t, path, cap);
+  if (len < 0) return len;
+  // GraphPlanner.find_path's merge (graph_planner.py:92-116): a node closer than
+  // `threshold` raw units to the last kept one is dropped
+  const double t2 = threshold * threshold;
+  int m = 0;
+  double lx = 0.0, ly = 0.0;
+  for (int k = 0; k < len; ++k) {
+    const int i = path[k];
+    const double x = pos_xy[2 * (size_t)i], y = pos_xy[2 * (size_t)i + 1];
+    if (m > 0) {
+      const double dx = x - lx, dy = y - ly;
+      const double d2 = dx * dx + dy * dy;
+      if (fabs(d2 - t2) <= 1e-6 * t2) return CBEVH_NEAR;  // np.linalg.norm decides these (never seen): the caller's merge
+      if (!(d2 > t2)) continue;
+    }
+    merged[m++] = i;
+    lx = x;
+    ly = y;
+  }
+  return m;
 }
 
 double cbevh_route_length(const double* x, const double* y, int n) {

@@ -15,11 +15,49 @@ from __future__ import annotations
 from collections import OrderedDict
 
 import numpy as np
-from scipy.signal import savgol_filter
+from scipy.ndimage import convolve1d
+from scipy.signal import savgol_coeffs, savgol_filter  # noqa: F401 (savgol_filter: the tests' cross-check)
 
 L_WHEELBASE = 2.9
 K_GAIN = 2.0
 MAX_STEER = np.radians(30.0)
+
+
+_SG_CACHE: dict = {}
+
+
+def _sg_tables(window: int, poly: int):
+    """What scipy.signal.savgol_filter(x, window, poly) recomputes on every call
+    (scipy 1.15 signal/_savitzky_golay.py:230-360, numpy polyfit): the
+    convolution coefficients and polyfit's scaled Vandermonde matrix, its column
+    scale and rcond for the edge fits. Deterministic, so computed once."""
+    key = (window, poly)
+    if key not in _SG_CACHE:
+        coeffs = savgol_coeffs(window, poly, deriv=0, delta=1.0)
+        t = np.arange(0, window) + 0.0
+        lhs = np.vander(t, poly + 1)
+        scale = np.sqrt((lhs * lhs).sum(axis=0))
+        lhs /= scale
+        _SG_CACHE[key] = (coeffs, lhs, scale, len(t) * np.finfo(t.dtype).eps)
+    return _SG_CACHE[key]
+
+
+def savgol_interp(x: np.ndarray, window: int, poly: int) -> np.ndarray:
+    """scipy.signal.savgol_filter(x, window, poly) (mode "interp", deriv 0) of a
+    1-D float64 array, bit for bit: the same convolve1d of the same
+    coefficients, then each edge refit with the same lstsq call np.polyfit makes
+    (savgol_filter -> _fit_edges_polyfit -> _fit_edge) and np.polyval -- without
+    recomputing the coefficients and polyfit's matrix on every call."""
+    coeffs, lhs, scale, rcond = _sg_tables(window, poly)
+    y = convolve1d(x, coeffs, axis=-1, mode="constant")
+    n, half = x.shape[0], window // 2
+    for ws, is_, ie in ((0, 0, half), (n - window, n - half, n)):
+        rhs = x[ws:ws + window].reshape(window, 1) + 0.0  # polyfit's `y + 0.0`
+        c = np.linalg.lstsq(lhs, rhs, rcond)[0]
+        c = (c.T / scale).T
+        i = np.arange(is_ - ws, ie - ws)
+        y[is_:ie] = np.polyval(c, i.reshape(-1, 1)).reshape(ie - is_)  # / (delta ** 0) = / 1.0: exact
+    return y
 
 
 _SMOOTH_MEMO: "OrderedDict[tuple, tuple]" = OrderedDict()
@@ -61,8 +99,8 @@ def _smooth_and_compute(ax, ay, window: int, poly: int):
         window = 3
     poly = min(poly, window - 1)
     if len(ax) >= window:
-        cx = savgol_filter(ax, window_length=window, polyorder=poly)
-        cy = savgol_filter(ay, window_length=window, polyorder=poly)
+        cx = savgol_interp(ax, window, poly)
+        cy = savgol_interp(ay, window, poly)
     else:
         cx, cy = ax.copy(), ay.copy()
     seg = np.hypot(np.diff(cx), np.diff(cy))

@@ -259,14 +259,11 @@ class SceneGenerator:
             end = g.random_node(node_cls, rng)
             if start == end:
                 continue
-            path, _ = g.find_path(start, end)
-            if not path or len(path) < 2:
+            path = g.find_path_idx(start, end)
+            if len(path) < 2:
                 continue
-            rx, ry = [], []
-            for n in path[1:]:
-                x, y = g.node_xy_surface(n)
-                rx.append(x)
-                ry.append(y)
+            xy = g.surf_xy[path[1:]]  # node_pos_surface of path[1:]
+            rx, ry = xy[:, 0].tolist(), xy[:, 1].tolist()
             length = route_length_meters(rx, ry)
             if min_m <= length <= max_m:
                 metrics = route_profile_metrics(rx, ry)
@@ -282,12 +279,9 @@ class SceneGenerator:
         g = self.planners[f"vehicle-{lane}"]
         start = g.random_node(lane, rng)
         end = g.random_node(lane, rng)
-        path, _ = g.find_path(start, end)
-        rx, ry = [], []
-        for n in path[1:-1]:
-            x, y = g.node_xy_surface(n)
-            rx.append(x)
-            ry.append(y)
+        path = g.find_path_idx(start, end)
+        xy = g.surf_xy[path[1:-1]]
+        rx, ry = xy[:, 0].tolist(), xy[:, 1].tolist()
         return (rx, ry) if len(rx) > 5 else None
 
     def generate_random(self, num_cars, dist_range, bundle: RNGBundle, traffic_enabled=True, ego_target_speed=12.0,

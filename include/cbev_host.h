@@ -16,7 +16,7 @@ extern "C" {
 
 #define CBEVH_ABI_VERSION 1
 
-enum { CBEVH_NOPATH = -1, CBEVH_EINVAL = -2, CBEVH_ENOMEM = -3, CBEVH_ECAP = -4 };
+enum { CBEVH_NOPATH = -1, CBEVH_EINVAL = -2, CBEVH_ENOMEM = -3, CBEVH_ECAP = -4, CBEVH_NEAR = -5 };
 
 int cbevh_abi_version(void);
 
@@ -32,6 +32,16 @@ int cbevh_abi_version(void);
 int cbevh_shortest_path(int n, const int32_t* succ_off, const int32_t* succ_idx, const double* succ_cost,
                         const int32_t* pred_off, const int32_t* pred_idx, const double* pred_cost, int s, int t,
                         int32_t* path, int cap);
+
+/* GraphPlanner.find_path (graph_planner.py:92-116): the shortest path above,
+ * then the nodes closer than `threshold` raw units to the last kept one dropped.
+ * pos_xy = float64[n][2] node positions; path = scratch of cap entries; the kept
+ * node indices go to merged[0 .. m) (at most cap) and m is returned.
+ * CBEVH_NEAR when a distance is within 1e-6 relative of the threshold (the
+ * reference decides those with np.linalg.norm: the caller merges itself). */
+int cbevh_find_path(int n, const int32_t* succ_off, const int32_t* succ_idx, const double* succ_cost,
+                    const int32_t* pred_off, const int32_t* pred_idx, const double* pred_cost, int s, int t,
+                    const double* pos_xy, double threshold, int32_t* path, int cap, int32_t* merged);
 
 /* route_length_meters before the metres scale (envs/geometry.py:61-69): the
  * sum of the n - 1 segment lengths hypot(dx, dy), in order. */

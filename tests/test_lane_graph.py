@@ -198,3 +198,24 @@ def test_route_profile_mix_draws_from_the_route_stream(gen):
     assert r.choices(["mostly_straight", "single_right"], weights=[0.0, 1.0], k=1)[0] == "single_right"
     with pytest.raises(ValueError):
         gen.build_scene(dict(opts, route_profile_mix={"mostly_straight": -1.0}), build_rng_bundle(scene_seed=1))
+
+
+def test_savgol_restatement_is_bitwise_scipy():
+    """routes.savgol_interp (cached coefficients and polyfit matrix) equals
+    scipy.signal.savgol_filter bit for bit (mode "interp", the reference's call in
+    control/utils.py:200-269) on every window the routes use and on route-like,
+    quantised and noisy inputs; tests/golden/smooth_route.npz pins the whole
+    smoothing against the reference itself (test_oracle_golden)."""
+    from scipy.signal import savgol_filter
+    from carlabev_env_amd.routes import savgol_interp
+    rng = np.random.default_rng(11)
+    for t in range(1500):
+        n = int(rng.integers(3, 300))
+        w = (3, 5, 7, 9, 11)[t % 5]
+        if w > n:
+            continue
+        p = min(3, w - 1)
+        x = (rng.normal(size=n) * 1000, np.round(rng.uniform(0, 1200, n) * 8) / 8,
+             np.cumsum(rng.integers(-3, 4, n)).astype(float) * 0.125 + 500)[t % 3]
+        assert np.array_equal(savgol_filter(x, window_length=w, polyorder=p).view(np.int64),
+                              savgol_interp(x, w, p).view(np.int64)), (t, n, w)
