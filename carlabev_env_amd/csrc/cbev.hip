@@ -2890,6 +2890,53 @@ __global__ __launch_bounds__(256) void k_ego(uint8_t* __restrict__ recs, int n, 
   // rows once the mask is ranked.
   auto src_rec = [&](int k) -> uint8_t* { return recs + (int64_t)(e0 + k) * st_rb; };
   ego_stage_in(lds, src_rec, ne_eff > 0 ? ne_eff : 0, st_n0, st_n, st_raw_x);
+  // S2 + S1 under the staging (waves 0 and 1 issue none of it, so their loads
+  // are waited for precisely while the LDS-DMA of waves 2 and 3 stays in
+  // flight). S2's inputs come from HBM into registers, issued first: the pose,
+  // the route length and S2_PF route points per thread (128 / ne threads per
+  // env: the first 64 points at 16 envs per workgroup, 128 at 8; points beyond
+  // are loaded in the loop); each of an env's threads computes the yaw's cos /
+  // sin itself (the same d_sincos as S1), so S2 needs no barrier before it and
+  // runs under the staging instead of after it. With a folded reset pending they
+  // are loaded from the records speculatively, beside the mask read (most envs
+  // keep their record), and a reset env's threads load them again from its bank
+  // row once the mask is read.
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  constexpr int S2_PF = 8;
+  const int tpe2 = 128 / ne, s2k = tid / tpe2, s2sub = tid - s2k * tpe2;
+  const bool s2 = wave <= 1 && s2k < ne_eff;
+  double s2x[S2_PF], s2y[S2_PF], s2hx = 0.0, s2hy = 0.0, s2yaw = 0.0;
+  int s2nr = 0;
+  DRec s2g = bind_rec(src_rec(s2 ? s2k : 0), K.L, K.C);
+  auto s2_load = [&]() {
+    s2hx = s2g.hd[CBEV_HD_X];
+    s2hy = s2g.hd[CBEV_HD_Y];
+    s2yaw = s2g.hd[CBEV_HD_YAW];
+    s2nr = s2g.hi[CBEV_HI_NROUTE];
+#pragma unroll
+    for (int j = 0; j < S2_PF; ++j) {  // index clamped to the route capacity: no branch around a load
+      const int i = min(s2sub + j * tpe2, K.C.route_cap - 1);
+      s2x[j] = s2g.cx[i];
+      s2y[j] = s2g.cy[i];
+    }
+  };
+  if (s2) s2_load();
+  // S5's targets (env tid / tpe, points sub, sub + tpe, ...): the first S5_PF of
+  // a thread's route points, loaded now; the Stanley set point of S6's thread
+  // (tid < ne) is loaded in S4 once S3 has moved the target index
+  constexpr int S5_PF = 4;
+  const int tpe5 = 256 / ne, k5 = tid / tpe5, sub5 = tid - k5 * tpe5;
+  double t5x[S5_PF], t5y[S5_PF];
+  auto t5_load = [&](const DRec& g) {
+#pragma unroll
+    for (int j = 0; j < S5_PF; ++j) {
+      const int i = min(sub5 + j * tpe5, K.C.route_cap - 1);
+      t5x[j] = g.cx[i];
+      t5y[j] = g.cy[i];
+    }
+  };
+  if (k5 < ne_eff) t5_load(bind_rec(src_rec(k5), K.L, K.C));
   EgoReset R{0ull};
   if (K.rmask != nullptr) R = ego_reset_take(K, e0, ne_eff, (int*)scr, rrow);
   auto src = [&](int k) -> uint8_t* {
@@ -2897,7 +2944,14 @@ __global__ __launch_bounds__(256) void k_ego(uint8_t* __restrict__ recs, int n, 
       return (uint8_t*)K.rbank + (int64_t)rrow[k] * st_rb;
     return recs + (int64_t)(e0 + k) * st_rb;
   };
-  if (R.bits != 0ull) ego_restage(lds + ne * pk.bytes, src, R.bits, ne_eff, st_n0, st_n, st_raw_x);
+  if (R.bits != 0ull) {  // uniform
+    ego_restage(lds + ne * pk.bytes, src, R.bits, ne_eff, st_n0, st_n, st_raw_x);
+    if (s2 && ((R.bits >> s2k) & 1ull)) {  // a reset env's S2 / S5 inputs again, from its bank row
+      s2g = bind_rec(src(s2k), K.L, K.C);
+      s2_load();
+    }
+    if (k5 < ne_eff && ((R.bits >> k5) & 1ull)) t5_load(bind_rec(src(k5), K.L, K.C));
+  }
   // env k's staged ranges: its record slot, or its bank-row slot when the folded reset takes it
   auto slot = [&](int k) -> uint8_t* { return lds + ((R.bits >> k) & 1ull ? ne + k : k) * pk.bytes; };
   CBEV_STAMP(3, 0);
@@ -2922,51 +2976,8 @@ __global__ __launch_bounds__(256) void k_ego(uint8_t* __restrict__ recs, int n, 
     rest_v = *(const uint4*)(src(rest_k) + rest_o);
     asm volatile("" ::"v"(rest_v.x), "v"(rest_v.y), "v"(rest_v.z), "v"(rest_v.w));  // issued here, not sunk to S7
   }
-  const int tid = threadIdx.x;
-  const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   auto rec = [&](int k) { return bind_ego(slot(k), src(k), K, pk); };
   if (blockIdx.x == 0 && tid == 0 && K.ep_count_next != nullptr) *K.ep_count_next = 0;
-  // S2 + S1 under the staging (waves 0 and 1 issue none of it, so their loads
-  // are waited for precisely while the LDS-DMA of waves 2 and 3 stays in
-  // flight). S2's inputs come from HBM into registers, issued first: the pose,
-  // the route length and S2_PF route points per thread (128 / ne threads per
-  // env: the first 64 points at 16 envs per workgroup, 128 at 8; points beyond
-  // are loaded in the loop); each of an env's threads computes the yaw's cos /
-  // sin itself (the same d_sincos as S1), so S2 needs no barrier before it and
-  // runs under the staging instead of after it.
-  constexpr int S2_PF = 8;
-  const int tpe2 = 128 / ne, s2k = tid / tpe2, s2sub = tid - s2k * tpe2;
-  const bool s2 = wave <= 1 && s2k < ne_eff;
-  double s2x[S2_PF], s2y[S2_PF], s2hx = 0.0, s2hy = 0.0, s2yaw = 0.0;
-  int s2nr = 0;
-  const DRec s2g = bind_rec(src(s2 ? s2k : 0), K.L, K.C);
-  if (s2) {
-    s2hx = s2g.hd[CBEV_HD_X];
-    s2hy = s2g.hd[CBEV_HD_Y];
-    s2yaw = s2g.hd[CBEV_HD_YAW];
-    s2nr = s2g.hi[CBEV_HI_NROUTE];
-#pragma unroll
-    for (int j = 0; j < S2_PF; ++j) {  // index clamped to the route capacity: no branch around a load
-      const int i = min(s2sub + j * tpe2, K.C.route_cap - 1);
-      s2x[j] = s2g.cx[i];
-      s2y[j] = s2g.cy[i];
-    }
-  }
-  // S5's targets (env tid / tpe, points sub, sub + tpe, ...): the first S5_PF of
-  // a thread's route points, loaded now; the Stanley set point of S6's thread
-  // (tid < ne) is loaded in S4 once S3 has moved the target index
-  constexpr int S5_PF = 4;
-  const int tpe5 = 256 / ne, k5 = tid / tpe5, sub5 = tid - k5 * tpe5;
-  double t5x[S5_PF], t5y[S5_PF];
-  if (k5 < ne_eff) {
-    const DRec g = bind_rec(src(k5), K.L, K.C);
-#pragma unroll
-    for (int j = 0; j < S5_PF; ++j) {
-      const int i = min(sub5 + j * tpe5, K.C.route_cap - 1);
-      t5x[j] = g.cx[i];
-      t5y[j] = g.cy[i];
-    }
-  }
   // S1 on the staging waves once their LDS-DMA is issued (they would otherwise
   // idle until the barrier; S2 on waves 0 and 1 then starts as soon as its own
   // loads land): the actions, and from the record's yaw and speed cos / sin of
