@@ -16,6 +16,7 @@ import pytest
 torch = pytest.importorskip("torch")
 
 from carlabev_env_amd import layout as LY
+from carlabev_env_amd._lib import lib
 from stats_ref import Stats
 
 pytestmark = pytest.mark.gpu
@@ -173,11 +174,12 @@ def test_refresh_bank_releases_only_dead_contexts():
             if env_tag.get(i) is not None:
                 assert infos["episode_info"]["tag"][i] == env_tag[i], (t, i)
                 seen += 1
-        if done.any():
-            rows0 = env.bank_rows_used()
+        if done.any():  # env i's j-th masked reset takes bank row (i + j * stride) % B (cbev.h, ABI 7)
+            counts = env.reset_counts()
+            stride = lib().cbev_bank_stride(B)
             env.reset_terminated()
-            for k, i in enumerate(np.flatnonzero(done)):
-                env_tag[i] = bank_tag[(rows0 + k) % B]
+            for i in np.flatnonzero(done):
+                env_tag[i] = bank_tag[(int(i) + int(counts[i]) * stride) % B]
         # refresh the whole bank with fresh tagged scenes every step
         ctxs = []
         for k in range(B):
