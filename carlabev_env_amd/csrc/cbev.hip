@@ -2192,14 +2192,17 @@ __global__ __launch_bounds__(256) void k_reset_copy(KArgs K, uint8_t* __restrict
 }
 
 // Canonical-loop reset (reset(reset_mask=terminated), tools/debug_env.py:56-132)
-// from a bank with cached reset frames: every env with mask[e] != 0 takes its
-// next bank row, bank_row_of(e, j) = (e + j * stride) % n_bank for its j-th
-// reset (j = seq[e].x, the env's resets so far; stride coprime with n_bank, so
-// each env walks the whole bank before a scene repeats for it). The row of an
-// env depends on nothing outside that env (round 6: no global cursor, so the
-// reset folded into k_ego needs no other workgroup's mask bytes). The mask is
-// read when the reset runs (cbev_reset_terminated passes the last step's term
-// buffer, so in-place edits of it between the step and the reset count).
+// from a bank with cached reset frames: every env with mask[e] != 0 takes bank
+// row bank_row_of(e, j) = (e + j * stride) % n_bank, j = tcount[e], the env's
+// terminations so far (k_ego counts them; stride coprime with n_bank): each
+// reset after a new termination takes the env's next row, so each env walks
+// the whole bank before a scene repeats for it. The row of an env depends on
+// nothing outside that env, and no reset kernel writes the counts (round 6: no
+// global cursor, so the reset folded into k_ego needs no other workgroup's mask
+// bytes, and the workgroups copying one env's pieces need no ordering). The
+// mask is read when the reset runs (cbev_reset_terminated passes the last
+// step's term buffer, so in-place edits of it between the step and the reset
+// count).
 // Ranking (which envs are selected, to deal their copies over the grid), once
 // per workgroup and independent of how many envs are selected:
 // the mask is cut into 16-byte units, each thread takes `upt` consecutive
@@ -2209,13 +2212,8 @@ __global__ __launch_bounds__(256) void k_reset_copy(KArgs K, uint8_t* __restrict
 // 256 thread prefixes, the unit within the thread and the set bit within the
 // unit: O(n / 4096 + log) per workgroup, no pass over the selected envs per
 // piece. Pieces as in k_reset_copy (16 KB, RESET_PU loads per thread in
-// flight), dealt over the grid. An env's pieces are copied by different
-// workgroups, which all read seq[e].x before any of them moves it: each piece
-// ends with one acquire-release increment of seq[e].y (pieces done), and the
-// piece that completes the env advances seq[e].x and clears seq[e].y, after every
-// other piece's read. The sequence lives on the device only: graph replays hand
-// out fresh rows, and rows advance only when a reset runs. The leading scalar
-// arguments are preloaded into SGPRs.
+// flight), dealt over the grid. The leading scalar arguments are preloaded
+// into SGPRs.
 __device__ __forceinline__ uint32_t nonzero_bytes16(const uint4 v) {  // bit b: byte b of the 16 is nonzero
   uint32_t m = 0;
   const uint32_t w[4] = {v.x, v.y, v.z, v.w};
@@ -2232,7 +2230,7 @@ __device__ __forceinline__ int bank_row_of(int e, uint32_t j, uint32_t stride, i
 }
 __global__ __launch_bounds__(256) void k_reset_mask(int n, int n_bank, uint32_t stride, int rb, int SS, int n_frames,
                                                     int upt, const uint8_t* __restrict__ mask,
-                                                    uint32_t* __restrict__ seq,
+                                                    const uint32_t* __restrict__ tcount,
                                                     uint8_t* __restrict__ recs, const uint8_t* __restrict__ bank,
                                                     const uint8_t* __restrict__ bank_frames,
                                                     uint8_t* __restrict__ ring, KArgs K) {
@@ -2290,8 +2288,7 @@ __global__ __launch_bounds__(256) void k_reset_mask(int n, int n_bank, uint32_t 
       m = um[++u];
     }
     const int e = 16 * u + nth_set_bit(m, j);
-    const uint32_t js = seq[2 * (int64_t)e];  // the env's resets so far (moved only once all its pieces read it)
-    const int b = bank_row_of(e, js, stride, n_bank);
+    const int b = bank_row_of(e, tcount[e], stride, n_bank);
     const bool fr = c < pf;  // uniform
     const uint8_t* src = fr ? bank_frames + (int64_t)b * SS : bank + (int64_t)b * rb;
     uint8_t* dst = fr ? ring + (int64_t)e * SS : recs + (int64_t)e * rb;
@@ -2316,14 +2313,6 @@ __global__ __launch_bounds__(256) void k_reset_mask(int n, int n_bank, uint32_t 
       }
     }
     if (c == pf && threadIdx.x == 0 && K.stats != nullptr) K.stats[e].t0 = (double)wall_clock64();
-    __syncthreads();  // every wave's read of seq[e] has returned (its value addressed this piece's loads)
-    if (threadIdx.x == 0) {
-      const uint32_t d = __hip_atomic_fetch_add(seq + 2 * (int64_t)e + 1, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-      if (d == (uint32_t)ppe - 1) {  // the env's last piece: every other piece has read seq[e].x
-        seq[2 * (int64_t)e + 1] = 0u;
-        __hip_atomic_store(seq + 2 * (int64_t)e, js + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
   }
 }
 // k_reset_mask's dynamic LDS: prefixes + wave totals (1056 B) + the unit masks
@@ -2788,29 +2777,24 @@ __device__ __forceinline__ void butterfly(int tpe, F&& f) {
 // tools/debug_env.py:56-132) without a launch of its own: the next k_ego reads
 // its own envs' mask bytes (the previous step's term buffer, read when this
 // step runs, so in-place edits of it count), each selected env takes
-// bank_row_of(e, seq[e]) exactly as k_reset_mask gives it and advances its
-// sequence (the workgroup owns its envs' entries), and the workgroup stages its
-// reset envs from their bank rows instead of their records. Nothing is read
-// from another workgroup's envs: the mask bytes of a workgroup's envs were
-// published by the previous step's k_raster items of the same XCD.
+// bank_row_of(e, tcount[e]) exactly as k_reset_mask gives it, and the workgroup
+// stages its reset envs from their bank rows instead of their records. Nothing
+// is read from another workgroup's envs.
 __device__ __forceinline__ int P_size_sq(const KArgs& K) { return K.P.size * K.P.size; }
 struct EgoReset {
   uint64_t bits;  // the workgroup's envs to reset (bit k: env e0 + k); their bank rows in rrow[k]
 };
-__device__ __forceinline__ EgoReset ego_reset_take(const KArgs& K, int e0, int ne_eff, int* red, int* rrow) {
+__device__ __forceinline__ EgoReset ego_reset_take(const KArgs& K, int e0, int ne_eff, uint32_t tc, int* red,
+                                                   int* rrow) {
   // wave 0 (lane k: env e0 + k, ne <= 64); waves 2 and 3 keep their staging
   // LDS-DMA in flight (a raw barrier, no vmcnt drain)
   const int tid = threadIdx.x;
   if (tid < 64) {
     const int e = e0 + tid;
-    // the mask bytes were written by this workgroup's envs' previous k_ego (this
-    // XCD's L2); the reset counts are read for the selected envs only (a cold line)
     const bool sel = tid < ne_eff && K.rmask[e] != 0;
     const uint64_t bits = __ballot(sel);
     if (sel) {
-      const uint32_t j = K.rseq[2 * (int64_t)e];
-      rrow[tid] = bank_row_of(e, j, K.rstride, K.rn_bank);
-      K.rseq[2 * (int64_t)e] = j + 1u;
+      rrow[tid] = bank_row_of(e, tc, K.rstride, K.rn_bank);  // tc: the env's terminations so far, loaded at launch
       if (K.stats != nullptr) K.stats[e].t0 = (double)wall_clock64();  // the episode's start
     }
     if (tid == 0) {
@@ -2937,8 +2921,11 @@ __global__ __launch_bounds__(256) void k_ego(uint8_t* __restrict__ recs, int n, 
     }
   };
   if (k5 < ne_eff) t5_load(bind_rec(src_rec(k5), K.L, K.C));
+  // the env's terminations so far (lane k of wave 0 = env e0 + k, also S6's
+  // thread): the folded reset's bank row, and counted up at S6 on termination
+  const uint32_t tc0 = tid < ne_eff ? K.tcount[e0 + tid] : 0u;
   EgoReset R{0ull};
-  if (K.rmask != nullptr) R = ego_reset_take(K, e0, ne_eff, (int*)scr, rrow);
+  if (K.rmask != nullptr) R = ego_reset_take(K, e0, ne_eff, tc0, (int*)scr, rrow);
   auto src = [&](int k) -> uint8_t* {
     if (R.bits != 0ull && ((R.bits >> k) & 1ull))
       return (uint8_t*)K.rbank + (int64_t)rrow[k] * st_rb;
@@ -3269,6 +3256,7 @@ __global__ __launch_bounds__(256) void k_ego(uint8_t* __restrict__ recs, int n, 
     cp.spx = s6spx;  // tid < ne: wave 0, the lane that loaded them in S4
     cp.spy = s6spy;
     collide_env(K, r, e0 + tid, cp, reward_out, term_out, trunc_out, cause_out, info_out);
+    if (r.hi[CBEV_HI_TERM]) K.tcount[e0 + tid] = tc0 + 1u;  // the next reset's bank row moves on
   }
   __syncthreads();
   CBEV_STAMP(1, 2);
@@ -3627,10 +3615,10 @@ struct cbev_ctx {
   int ep_ring, ep_n;
   int64_t step_count;         // cbev_step calls since cbev_set_episode_stats
   double tick_s;
-  // per-env reset sequence of cbev_reset_masked (resets so far, pieces done):
-  // env e's j-th reset takes bank row (e + j * bank_stride(n_bank)) % n_bank
-  uint32_t* seq_dev;  // [CBEV_RESET_MASK_MAX_N][2]
-  int seq_n;          // the largest n a masked reset has run on
+  // per-env termination counts (k_ego): a masked reset of env e after its j-th
+  // termination takes bank row (e + j * bank_stride(n_bank)) % n_bank
+  uint32_t* seq_dev;  // [CBEV_RESET_MASK_MAX_N]
+  int seq_n;          // the largest n a step or a masked reset has run on
   // cbev_set_deferred_reset: a cbev_reset_terminated recorded here and folded
   // into the next cbev_step's k_ego (KArgs::rmask), or launched as k_reset_mask
   // by the next call that would observe it (flush_pending)
@@ -3761,7 +3749,7 @@ static KArgs kargs(const cbev_ctx* c) {
   K.tick_s = c->tick_s;
   K.rmask = K.rbank = K.rbank_frames = nullptr;
   K.rring = nullptr;
-  K.rseq = nullptr;
+  K.tcount = c->seq_dev;
   K.rring_stride = 0;
   K.rn_bank = K.rn_frames = K.rslot = 0;
   K.rstride = 0;
@@ -3904,7 +3892,7 @@ int cbev_create(const cbev_params* params, const cbev_caps* caps, int device, cb
   if (e == hipSuccess) e = hipMemset(c->err_dev, 0, sizeof(int32_t));
   if (e == hipSuccess) e = hipMalloc(&c->nterm_dev, sizeof(unsigned long long));
   if (e == hipSuccess) e = hipMemset(c->nterm_dev, 0, sizeof(unsigned long long));
-  const size_t seq_bytes = (size_t)CBEV_RESET_MASK_MAX_N * 2 * sizeof(uint32_t);
+  const size_t seq_bytes = (size_t)CBEV_RESET_MASK_MAX_N * sizeof(uint32_t);
   if (e == hipSuccess) e = hipMalloc(&c->seq_dev, seq_bytes);
   if (e == hipSuccess) e = hipMemset(c->seq_dev, 0, seq_bytes);
   if (e == hipSuccess) {
@@ -4141,9 +4129,7 @@ int cbev_step(cbev_ctx* c, void* records, int n, const void* actions, uint8_t* f
       K.rn_bank = c->pend.n_bank;
       K.rn_frames = c->pend.n_frames;
       K.rslot = (int)(off / stride);
-      K.rseq = c->seq_dev;
       K.rstride = bank_stride(c->pend.n_bank);
-      if (n > c->seq_n) c->seq_n = n;
       c->pend.on = 0;
     } else {
       CBEV_FLUSH(c);
@@ -4151,6 +4137,7 @@ int cbev_step(cbev_ctx* c, void* records, int n, const void* actions, uint8_t* f
   }
   c->last_term = term;
   c->last_n = n;
+  if (n > c->seq_n) c->seq_n = n;
   const int wg4 = (n + 3) / 4;
   hipEvent_t* ev = nullptr;
   if (c->prof_on && c->prof_n < CBEV_PROF_MAX) ev = c->prof_ev + 4 * c->prof_n++;
@@ -4310,10 +4297,10 @@ int cbev_bank_cursor(cbev_ctx* c, int64_t* cursor) {
   CBEV_FLUSH(c);  // a deferred reset is applied before anything observes the state
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(hipDeviceSynchronize());  // the resets are queued on the caller's (non-blocking) stream
-  std::vector<uint32_t> v((size_t)2 * c->seq_n);
+  std::vector<uint32_t> v((size_t)c->seq_n);
   if (c->seq_n > 0) HIP_TRY(hipMemcpy(v.data(), c->seq_dev, v.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
   int64_t t = 0;
-  for (int e = 0; e < c->seq_n; ++e) t += v[2 * (size_t)e];
+  for (int e = 0; e < c->seq_n; ++e) t += v[(size_t)e];
   *cursor = t;
   return CBEV_OK;
 }
@@ -4324,9 +4311,7 @@ int cbev_reset_counts(cbev_ctx* c, uint32_t* counts_host, int n) {
   CBEV_FLUSH(c);  // a deferred reset is applied before anything observes the state
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(hipDeviceSynchronize());
-  std::vector<uint32_t> v((size_t)2 * n);
-  if (n > 0) HIP_TRY(hipMemcpy(v.data(), c->seq_dev, v.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
-  for (int e = 0; e < n; ++e) counts_host[e] = v[2 * (size_t)e];
+  if (n > 0) HIP_TRY(hipMemcpy(counts_host, c->seq_dev, (size_t)n * sizeof(uint32_t), hipMemcpyDeviceToHost));
   return CBEV_OK;
 }
 

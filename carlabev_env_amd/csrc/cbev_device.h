@@ -39,18 +39,18 @@ struct KArgs {
   int32_t* ep_count_next;     // the next step's row count, zeroed by this step
   int ep_cap;                 // rows a slot holds (the n of cbev_set_episode_stats)
   double tick_s;              // seconds per wall_clock64() tick
+  uint32_t* tcount;  // [n] per env: terminations so far (k_ego counts them; a masked reset's bank row)
   // The canonical reset folded into this step (cbev_set_deferred_reset: a
   // cbev_reset_terminated recorded, applied by k_ego; rmask null: none). k_ego
   // reads its envs' mask bytes, takes each reset env's record from bank row
-  // (e + seq[e] * rstride) % rn_bank (and advances seq[e]) and k_raster copies the
-  // bank frame into the ring slots other than rslot. A workgroup reads only its
-  // own envs' mask bytes, before it writes their termination flags, so the mask
-  // may be the term buffer this step writes.
+  // (e + tcount[e] * rstride) % rn_bank and k_raster copies the bank frame into
+  // the ring slots other than rslot. A workgroup reads only its own envs' mask
+  // bytes, before it writes their termination flags, so the mask may be the
+  // term buffer this step writes.
   const uint8_t* rmask;
   const uint8_t* rbank;
   const uint8_t* rbank_frames;
   uint8_t* rring;
-  uint32_t* rseq;  // [n][2] per env: resets so far, pieces done (k_reset_mask's)
   int64_t rring_stride;  // bytes between ring slots (n * S * S)
   int rn_bank, rn_frames, rslot;
   uint32_t rstride;  // bank_stride(rn_bank)

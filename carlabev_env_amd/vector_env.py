@@ -282,6 +282,9 @@ class CarlaBEVVectorEnv:
         self._all_mask = None  # uint8 ones: reset_from_bank(mask=None) without bank_idx
         self._bank_ctx_ids = None  # scenario-context id per bank row set by refresh_bank
         self._retired_ctx: deque = deque()  # ids of overwritten bank rows, released oldest first
+        # (id, step) of scenario contexts reset() replaced: released once no unread
+        # StepInfos can refer to them (those of steps up to EP_RING back are read by then)
+        self._host_retired: deque = deque()
         self._stepped = False
         self._step_stream = 0
         self.auto_obs = True  # reset_from_bank also expands the wire observation
@@ -464,11 +467,11 @@ class CarlaBEVVectorEnv:
     def reset_terminated(self):
         """The canonical loop's reset(reset_mask=terminated) on the device: every env
         whose `term` flag is set when the launch runs (the last step's, including any
-        in-place edit of env.term since) <- its next bank row (env e's j-th reset
-        takes bank[(e + j * stride) % B], stride = cbev_bank_stride(B) coprime with B,
-        so each env walks the whole bank before a scene repeats for it), reset frame
-        into every frame-stack slot. One launch (or none: folded into the next
-        step), no host sync."""
+        in-place edit of env.term since) <- its next bank row (env e takes
+        bank[(e + j * stride) % B], j = its terminations so far, stride =
+        cbev_bank_stride(B) coprime with B, so each env walks the whole bank before a
+        scene repeats for it), reset frame into every frame-stack slot. One launch
+        (or none: folded into the next step), no host sync."""
         if self.bank is None:
             raise RuntimeError("no scene bank attached")
         if not self._stepped:
@@ -509,8 +512,8 @@ class CarlaBEVVectorEnv:
         return int(n.value)
 
     def reset_counts(self) -> np.ndarray:
-        """Per-env counts j of those resets (uint32[N], synchronises): env e's j-th
-        took bank row (e + j * cbev_bank_stride(B)) % B."""
+        """Per-env termination counts j (uint32[N], synchronises): a masked reset of
+        env e takes bank row (e + j * cbev_bank_stride(B)) % B."""
         out = np.zeros(self.num_envs, np.uint32)
         check(lib().cbev_reset_counts(self._ctx, out.ctypes.data_as(ctypes.c_void_p), self.num_envs),
               "cbev_reset_counts")
@@ -518,19 +521,20 @@ class CarlaBEVVectorEnv:
 
     @staticmethod
     def bank_rows_between(c0: np.ndarray, c1: np.ndarray, n_bank: int) -> np.ndarray:
-        """The bank rows the masked resets took between two reset_counts() readings."""
+        """The bank rows the canonical loop's resets took between two reset_counts()
+        readings (each termination reset: counts c0 + 1 .. c1)."""
         c0, c1 = c0.astype(np.int64), c1.astype(np.int64)
         d = c1 - c0
         e = np.repeat(np.arange(len(c0), dtype=np.int64), d)
-        j = np.repeat(c0, d) + (np.arange(int(d.sum()), dtype=np.int64) - np.repeat(np.cumsum(d) - d, d))
+        j = np.repeat(c0 + 1, d) + (np.arange(int(d.sum()), dtype=np.int64) - np.repeat(np.cumsum(d) - d, d))
         return (e + j * int(lib().cbev_bank_stride(n_bank))) % n_bank
 
     def reset_from_bank(self, mask: torch.Tensor | None = None, bank_idx: torch.Tensor | None = None):
         """Device-only partial reset from the scene bank, reset frame into every
         frame-stack slot. One launch, no host sync.
         Without bank_idx: the envs selected by mask (all when None; its contents as
-        the launch reads them) take their next bank rows (reset_terminated's per-env
-        rule; reset_terminated is this with mask = env.term).
+        the launch reads them) take the bank rows of their termination counts
+        (reset_terminated's per-env rule; reset_terminated is this with mask = env.term).
         With bank_idx: env i (mask[i]) <- bank[bank_idx[i]]; the cursor is untouched."""
         if self.bank is None:
             raise RuntimeError("no scene bank attached")
@@ -602,7 +606,11 @@ class CarlaBEVVectorEnv:
         idx = np.flatnonzero(mask)
         host = self._new_record_buffer(max(len(idx), 1))
         spawn_infos = []
-        self._flush_pending(all_=True)  # contexts released below may still be read
+        # contexts replaced by earlier resets that no StepInfos can still refer to:
+        # released (StepInfos of steps <= _ep_step - EP_RING have been read or dropped,
+        # _flush_pending); this reset's replaced ones wait their turn
+        while self._host_retired and self._host_retired[0][1] <= self._ep_step - EP_RING:
+            self._ctx_table.pop(self._host_retired.popleft()[0], None)
         if self.reset_pool is not None and len(idx) > 1:
             # the distinct scenes not memoised yet, built by the pool's workers and
             # memoised here; the loop below then copies them
@@ -622,7 +630,7 @@ class CarlaBEVVectorEnv:
             self.scene_context[i] = ctx
             old = int(self._env_ctx[i])
             if old:
-                self._ctx_table.pop(old, None)
+                self._host_retired.append((old, self._ep_step))
             cid = self._new_ctx_id(ctx)
             self._env_ctx[i] = cid
             LY.RecordView(host[k], self.layout).hi[LY.HI["CTX_ID"]] = cid

@@ -130,15 +130,17 @@ int cbev_reset_frames(cbev_ctx* ctx, void* records, int n, const void* bank, int
                       int n_frames, void* stream);
 
 /* `reset(options={"reset_mask": mask})` (SyncVectorEnv.reset -> CarlaBEV.reset,
- * carlabev.py:96-148) from a bank with cached reset frames, each reset a fresh
- * bank row: every env with mask[e] != 0 (uint8[n], read when the launch runs)
- * takes bank row (e + j * cbev_bank_stride(n_bank)) % n_bank for its j-th such
- * reset (j counted per env on the device from 0 at cbev_create; the stride is
- * coprime with n_bank, so each env walks the whole bank before a scene repeats
- * for it). The row of an env depends on that env alone (ABI 7; before, a global
- * cursor dealt rows in env-id order, which made every workgroup of the folded
- * reset read the whole mask). Records and ring contents as cbev_reset_frames
- * with those bank rows. One launch, no host sync; n <= 2^20. */
+ * carlabev.py:96-148) from a bank with cached reset frames, each reset after a
+ * termination a fresh bank row: every env with mask[e] != 0 (uint8[n], read
+ * when the launch runs) takes bank row (e + j * cbev_bank_stride(n_bank)) %
+ * n_bank, j = the env's terminations so far (counted by cbev_step on the device
+ * from 0 at cbev_create; the stride is coprime with n_bank, so each env walks
+ * the whole bank before a scene repeats for it; a reset with no termination
+ * since the last one takes the same row again). The row of an env depends on
+ * that env alone and no reset writes the counts (ABI 7; before, a global cursor
+ * dealt rows in env-id order, which made every workgroup of the folded reset
+ * read the whole mask). Records and ring contents as cbev_reset_frames with
+ * those bank rows. One launch, no host sync; n <= 2^20. */
 int cbev_reset_masked(cbev_ctx* ctx, void* records, int n, const uint8_t* mask, const void* bank, int n_bank,
                       const uint8_t* bank_frames, uint8_t* frames, int n_frames, void* stream);
 /* The canonical loop's reset, `reset(options={"reset_mask": terminated})`
@@ -146,19 +148,18 @@ int cbev_reset_masked(cbev_ctx* ctx, void* records, int n, const uint8_t* mask, 
  * of the last cbev_step on this context (n must be that step's n). */
 int cbev_reset_terminated(cbev_ctx* ctx, void* records, int n, const void* bank, int n_bank,
                           const uint8_t* bank_frames, uint8_t* frames, int n_frames, void* stream);
-/* Bank rows cbev_reset_masked / cbev_reset_terminated have handed out since
- * cbev_create: the sum of the per-env counts (synchronises the device). */
+/* The sum of the per-env termination counts (synchronises the device): the
+ * bank rows the canonical loop's resets have handed out since cbev_create. */
 int cbev_bank_cursor(cbev_ctx* ctx, int64_t* cursor);
-/* The per-env counts j of those resets for envs 0 .. n-1 (synchronises). */
+/* The per-env termination counts j of envs 0 .. n-1 (synchronises). */
 int cbev_reset_counts(cbev_ctx* ctx, uint32_t* counts_host, int n);
 /* The stride of the masked reset's bank rows for a bank of n_bank rows (-1 if n_bank < 1). */
 int cbev_bank_stride(int n_bank);
 /* Deferred canonical reset (off by default). With it on, cbev_reset_terminated
  * records the reset instead of launching it, and the next cbev_step of the same
  * records and frame ring folds it into its first kernel (k_ego; the envs take
- * the same bank rows and advance the same per-env counts, records and ring
- * slots end up as cbev_reset_masked leaves them, the mask is read when that
- * step runs): the canonical loop's
+ * the same bank rows, records and ring slots end up as cbev_reset_masked leaves
+ * them, the mask is read when that step runs): the canonical loop's
  * step -> reset(reset_mask=terminated) -> step costs no reset launch. Any other
  * call on the context that reads or writes its state (every cbev_reset* call,
  * cbev_expand_obs, cbev_vector_obs, cbev_resize_obs, cbev_pack_frames,
@@ -170,7 +171,7 @@ int cbev_bank_stride(int n_bank);
  * The deferral is host-side state, taken when cbev_step is called: a cbev_step
  * captured into a graph while a reset is pending carries the folded reset, so
  * every replay resets the envs its term buffer selects at replay time (the mask
- * reads and the count advance run on the device); cbev_flush before capturing a
+ * and the termination counts are read on the device); cbev_flush before capturing a
  * step that must not reset. Neither call allocates (safe under a global-mode
  * stream capture). */
 int cbev_set_deferred_reset(cbev_ctx* ctx, int on);
