@@ -2109,7 +2109,7 @@ __global__ __launch_bounds__(256) void k_bank_frames(KArgs K, const uint8_t* __r
 
 // Partial reset from a bank with cached reset frames: records[e] <- bank[b] and
 // bank_frames[b] into every frame-stack slot of env e, for the envs selected by
-// mask. Pure 16-byte copies, split into 16 KB pieces: one pass of the 256
+// mask. Pure 16-byte copies, split into 32 KB pieces: one pass of the 256
 // threads with RESET_PU 16-byte loads each in flight, then the stores. An env's
 // pieces are its frame's (each written to every ring slot), then its record's.
 // The pieces of the selected envs are dealt round-robin over the workgroups of
@@ -2118,7 +2118,7 @@ __global__ __launch_bounds__(256) void k_bank_frames(KArgs K, const uint8_t* __r
 // instead of one workgroup per env: every workgroup ballots the masks of its
 // XCD's env blocks and counts the selected envs' pieces in env order, taking
 // every WPX-th.
-#define RESET_PU 4                      // 16-byte loads per thread in flight (8: 12.1 vs 12.5 us at config 3, the step no faster)
+#define RESET_PU 8                      // 16-byte loads per thread in flight (round 6, with the streamed stores: k_reset_mask 12.8 -> 11.6 us at config 3, 15.8 -> 14.0 at config 4)
 #define RESET_MASK_WGS 512              // k_reset_mask's grid cap
 #define CBEV_RESET_MASK_MAX_N (1 << 20)  // k_reset_mask's unit masks: 2 B per 16 envs of LDS
 #define RESET_PIECE (4096 * RESET_PU)   // bytes per piece
@@ -2211,8 +2211,8 @@ __global__ __launch_bounds__(256) void k_reset_copy(KArgs K, uint8_t* __restrict
 // Piece p of slot s = p / ppe then finds its env by a binary search over the
 // 256 thread prefixes, the unit within the thread and the set bit within the
 // unit: O(n / 4096 + log) per workgroup, no pass over the selected envs per
-// piece. Pieces as in k_reset_copy (16 KB, RESET_PU loads per thread in
-// flight), dealt over the grid. The leading scalar arguments are preloaded
+// piece. Pieces as in k_reset_copy (32 KB, RESET_PU loads per thread in
+// flight, streamed stores), dealt over the grid. The leading scalar arguments are preloaded
 // into SGPRs.
 __device__ __forceinline__ uint32_t nonzero_bytes16(const uint4 v) {  // bit b: byte b of the 16 is nonzero
   uint32_t m = 0;
@@ -2225,6 +2225,17 @@ __device__ __forceinline__ uint32_t nonzero_bytes16(const uint4 v) {  // bit b: 
   return m;
 }
 
+// the reset's copies: streamed stores (the next step's kernels read the records
+// from memory anyway: each kernel's start invalidates the L2)
+constexpr bool kResetStoreNT = true;
+__device__ __forceinline__ void reset_store16(uint8_t* p, const uint4 v) {
+  if (kResetStoreNT) {
+    u32x4_nt w = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(w, (u32x4_nt*)p);
+  } else {
+    *(uint4*)p = v;
+  }
+}
 __device__ __forceinline__ int bank_row_of(int e, uint32_t j, uint32_t stride, int n_bank) {
   return (int)(((uint64_t)e + (uint64_t)j * stride) % (uint64_t)n_bank);
 }
@@ -2307,9 +2318,9 @@ __global__ __launch_bounds__(256) void k_reset_mask(int n, int n_bank, uint32_t 
       const int64_t o = o0 + 4096 * q;
       if (o >= lim) continue;
       if (fr) {
-        for (int f = 0; f < n_frames; ++f) *(uint4*)(dst + (int64_t)f * n * SS + o) = v[q];
+        for (int f = 0; f < n_frames; ++f) reset_store16(dst + (int64_t)f * n * SS + o, v[q]);
       } else {
-        *(uint4*)(dst + o) = v[q];
+        reset_store16(dst + o, v[q]);
       }
     }
     if (c == pf && threadIdx.x == 0 && K.stats != nullptr) K.stats[e].t0 = (double)wall_clock64();

@@ -8,7 +8,7 @@ CACHE=/tmp/cbev_scene_cache
 i=0
 for lib in ${LIBS}; do
   i=$((i+1))
-  CBEV_LIB=$PWD/$lib timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/kab/p$i -o run --output-format csv -- python bench.py --config ${CONFIG:-2} --steps 50 --warmup 10 --no-cpu-baseline --no-wire --fresh-workers 0 --scene-cache $CACHE > gpurun_out/kab/p$i.log 2>&1 || { echo "prof $lib failed"; tail -5 gpurun_out/kab/p$i.log; exit 1; }
+  CBEV_LIB=$PWD/$lib timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/kab/p$i -o run --output-format csv -- python bench.py --config ${CONFIG:-2} --steps 50 --warmup 10 --no-cpu-baseline --no-wire --surface-steps 0 --fresh-workers 0 --scene-cache $CACHE > gpurun_out/kab/p$i.log 2>&1 || { echo "prof $lib failed"; tail -5 gpurun_out/kab/p$i.log; exit 1; }
   f=$(find gpurun_out/kab/p$i -name "*kernel_stats.csv" | head -1)
   cp "$f" gpurun_out/kab/kstats_$i.csv
   python - "$f" "$lib" <<'PY'
