@@ -264,6 +264,9 @@ __device__ __forceinline__ void wave_mem_fence() { __builtin_amdgcn_fence(__ATOM
 // Takes the record base and the byte offsets of the groups it touches as plain
 // ints: a DRec (or KArgs) reference makes every k_actors wave spill that struct
 // to scratch at launch (12 KB per wave), retreat or not.
+// (one copy per k_actors occupancy class, MINAW: a callee shared with the
+// 3-wave kernels would take their register budget, not k_actors_g4's)
+template <int MINAW>
 __device__ __noinline__ bool wave_start_retreat(uint8_t* base, int o_ad, int o_ai, int o_aix, int o_aiy, int o_arx,
                                                 int o_ary, int o_acx, int o_acy, int o_acyaw, int o_acf, int o_acb, int A,
                                                 int RA, int a, int lane) {
@@ -1138,7 +1141,12 @@ __device__ __forceinline__ int actor_search(const DRec& r, int nact, uint64_t li
 // its circle comes within that reach of the front axle -- by the triangle
 // inequality no point of a skipped block is within 3 eps of the float32
 // minimum, so it is never a pass-1 candidate. Then passes 1-2 as actor_search.
-constexpr int ACTOR_CQ = 10;  // circles per lane held at once (routes of more blocks: every block scanned)
+// circles per lane held at once: enough for the 18 blocks of a 288-point route
+// (the reference's lane-graph routes have at most 276 points) at every group
+// width -- routes of more blocks scan every block -- and no more (each circle
+// is two VGPRs held across the window's loads)
+constexpr int ACTOR_NB = 18;
+__host__ __device__ constexpr int actor_cq(int aw) { return (ACTOR_NB + aw - 1) / aw; }
 template <int AW>
 __device__ __forceinline__ int actor_search_win(const DRec& r, int nact, uint64_t livem, double fx, double fy,
                                                 int nrt, int tid0, int lane, double p0x, double p0y, double p1x,
@@ -1147,6 +1155,7 @@ __device__ __forceinline__ int actor_search_win(const DRec& r, int nact, uint64_
   constexpr int BP = CBEV_ACB_PTS;
   constexpr int WPL = (2 * BP + AW - 1) / AW;  // window points per lane
   constexpr int BPL = (BP + AW - 1) / AW;      // points per lane of a further block
+  constexpr int ACTOR_CQ = actor_cq(AW);
   const int RA = r.RA, NBC = (RA + BP - 1) / BP;
   const int g = lane / AW, sub = lane - g * AW;
   int best = 0;
@@ -1307,14 +1316,16 @@ __device__ __forceinline__ int actor_search_win(const DRec& r, int nact, uint64_
 
 // WIDE: the context's capacity allows more than 64 actors, which take the
 // serial per-lane path (d_actor_step). Contexts within 64 actor slots launch
-// k_actors<false>, which compiles without it: 134 instead of 246 VGPRs, 3 waves
-// per SIMD instead of 2 (asking for 4 waves per SIMD, amdgpu_waves_per_eu(4),
-// still leaves 130 VGPRs and spills 12). Both rebuild a StopReturn retreat with
-// the whole wave (wave_start_retreat: at most 64 points, which scene_pack
-// guarantees); a serial rebuild compiled into the narrow kernel would take it
-// from 134 to 200 VGPRs.
-template <bool WIDE>
-__global__ __launch_bounds__(256) void k_actors(KArgs K, uint8_t* __restrict__ recs, int n) {
+// k_actors<false, 1>, which compiles without it: 165 instead of 244 VGPRs, 3
+// waves per SIMD instead of 2; contexts within 32 slots launch k_actors_g4
+// (round 6: MINAW = 4, groups of at least 4 lanes per actor, the searches of
+// narrower groups not compiled in): 128 VGPRs without spills, 4 waves per SIMD,
+// so config 3's 4096 waves are resident at once. All rebuild a StopReturn
+// retreat with the whole wave (wave_start_retreat: at most 64 points, which
+// scene_pack guarantees); a serial rebuild compiled into the narrow kernels
+// would take them to 200 VGPRs.
+template <bool WIDE, int MINAW>
+__device__ __forceinline__ void actors_body(KArgs K, uint8_t* __restrict__ recs, int n) {
   const int lane = threadIdx.x & 63;
   const int e = xcd_env4_of_wg(blockIdx.x, threadIdx.x >> 6, n);
   if (e >= n) return;
@@ -1360,7 +1371,7 @@ __global__ __launch_bounds__(256) void k_actors(KArgs K, uint8_t* __restrict__ r
       const int k = __builtin_ctzll(rm);
       rm &= rm - 1;
       uint8_t* base = recs + (int64_t)e * K.L.record_bytes;
-      if (!wave_start_retreat(base, (int)K.L.ad, (int)K.L.ai, (int)K.L.aix, (int)K.L.aiy, (int)K.L.arx, (int)K.L.ary,
+      if (!wave_start_retreat<MINAW>(base, (int)K.L.ad, (int)K.L.ai, (int)K.L.aix, (int)K.L.aiy, (int)K.L.arx, (int)K.L.ary,
                               (int)K.L.acx, (int)K.L.acy, (int)K.L.acyaw, (int)K.L.acf, (int)K.L.acb, r.A, RA, k,
                               lane)) {
         // a rebuilt route of more than 64 points: scene_pack refuses such actors
@@ -1401,7 +1412,10 @@ __global__ __launch_bounds__(256) void k_actors(KArgs K, uint8_t* __restrict__ r
   // ---- 2
   const uint64_t livem = __ballot(live);
   // lanes per actor: the widest group that still takes every actor in one round
-  const int aw = nact <= 1 ? 64 : nact <= 2 ? 32 : nact <= 4 ? 16 : nact <= 8 ? 8 : nact <= 16 ? 4 : nact <= 32 ? 2 : 1;
+  // (MINAW: the narrowest group the context's actor capacity can need; only
+  // the searches of groups at least that wide are compiled in)
+  const int aw = max(MINAW, nact <= 1 ? 64 : nact <= 2 ? 32 : nact <= 4 ? 16 : nact <= 8 ? 8 : nact <= 16 ? 4
+                                                                                    : nact <= 32 ? 2 : 1);
   int best;
   switch (aw) {
     case 64: best = actor_search_win<64>(r, nact, livem, fx, fy, nrt, tid0, lane, pcx[0], pcy[0], pcx[1], pcy[1]); break;
@@ -1409,8 +1423,16 @@ __global__ __launch_bounds__(256) void k_actors(KArgs K, uint8_t* __restrict__ r
     case 16: best = actor_search_win<16>(r, nact, livem, fx, fy, nrt, tid0, lane, pcx[0], pcy[0], pcx[1], pcy[1]); break;
     case 8: best = actor_search_win<8>(r, nact, livem, fx, fy, nrt, tid0, lane, pcx[0], pcy[0], pcx[1], pcy[1]); break;
     case 4: best = actor_search_win<4>(r, nact, livem, fx, fy, nrt, tid0, lane, pcx[0], pcy[0], pcx[1], pcy[1]); break;
-    case 2: best = actor_search_win<2>(r, nact, livem, fx, fy, nrt, tid0, lane, pcx[0], pcy[0], pcx[1], pcy[1]); break;
-    default: best = actor_search<1>(r, nact, livem, fx, fy, nrt, lane); break;  // one lane per actor: the 32-point window would not fit the registers
+    case 2:
+      if (MINAW <= 2) {
+        best = actor_search_win<2>(r, nact, livem, fx, fy, nrt, tid0, lane, pcx[0], pcy[0], pcx[1], pcy[1]);
+        break;
+      }
+      [[fallthrough]];
+    default:
+      // one lane per actor: the 32-point window would not fit the registers
+      best = MINAW <= 1 ? actor_search<1>(r, nact, livem, fx, fy, nrt, lane) : 0;
+      break;
   }
   CBEV_STAMPW(6, 2);
   // ---- 3: stanley_control (stanley_controller.py:64-89), pid_control, State.update
@@ -1441,6 +1463,17 @@ __global__ __launch_bounds__(256) void k_actors(KArgs K, uint8_t* __restrict__ r
     RAD(r, CBEV_AD_TIME, a) += CB_DT;
   }
   CBEV_STAMPW(6, 3);
+}
+template <bool WIDE, int MINAW>
+__global__ __launch_bounds__(256) void k_actors(KArgs K, uint8_t* __restrict__ recs, int n) {
+  actors_body<WIDE, MINAW>(K, recs, n);
+}
+// groups of at least 4 lanes per actor (contexts of up to 32 actor slots):
+// 128 VGPRs without spills, 4 waves per SIMD
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_actors_g4(KArgs K,
+                                                                                          uint8_t* __restrict__ recs,
+                                                                                          int n) {
+  actors_body<false, 4>(K, recs, n);
 }
 
 
@@ -3769,7 +3802,11 @@ static KArgs kargs(const cbev_ctx* c) {
 
 typedef void (*ActorsKernel)(KArgs, uint8_t*, int);
 static ActorsKernel actors_kernel(const cbev_caps& C) {
-  return C.actor_cap > 64 ? k_actors<true> : k_actors<false>;
+  // up to 32 actor slots: groups of at least 4 lanes per actor (two passes of the
+  // group loop for 17-32 actors), 128 VGPRs, 4 waves per SIMD -- config 3's 4096
+  // waves resident at once (k_actors 25.1 -> 24.2 us at config 3, 30.7 -> 28.1 at
+  // config 4; 2 lanes per actor at 4 waves per SIMD spills: 30.7 us)
+  return C.actor_cap > 64 ? k_actors<true, 1> : C.actor_cap > 32 ? k_actors<false, 1> : k_actors_g4;
 }
 static const void* raster_kernel(int size) {
   return size == 64 ? (const void*)k_raster<1> : size == 128 ? (const void*)k_raster<2> : (const void*)k_raster<4>;

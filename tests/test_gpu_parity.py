@@ -483,8 +483,9 @@ def test_parity_wide_actor_kernel():
 def _long_route_edit(recs, layout, P):
     """Actor slots 0-3 of every record on 600-point out-and-back routes (300
     points east along the start's row, then back beside it, half a point
-    shifted): 38 blocks of 16 points, more than the 10 circles a lane holds at 2
-    lanes per actor and than the 32 candidate bits. Slots 0-1 return 0.25 px
+    shifted): 38 blocks of 16 points, more than the circles a group holds (18
+    blocks at 2 lanes per actor, 20 at 4: cbev.hip actor_cq) and than the 32
+    candidate bits. Slots 0-1 return 0.25 px
     beside the outbound leg, so the first minimum is soon on the return leg's
     last blocks (the reference's whole-route scan); slots 2-3 return 3 px away
     and drive the outbound leg."""
@@ -502,11 +503,23 @@ def _long_route_edit(recs, layout, P):
 
 def test_parity_long_actor_routes():
     """k_actors' windowed search on routes with more blocks than its circles
-    (actor route capacity 640, 25 vehicles: 2 lanes per actor): every block
-    outside the window is scanned in the second round, blocks past the 32nd
-    included (stanley_controller.py:100-123 scans the whole route)."""
+    (actor route capacity 640, 25 vehicles: k_actors_g4, 4 lanes per actor in two
+    passes of the group loop): every block outside the window is scanned in the
+    second round, blocks past the 32nd included (stanley_controller.py:100-123
+    scans the whole route)."""
     caps = LY.Caps(128, 25, 640, 4)
     run_parity(["rt_hard_v1"], 8, 40, seed0=61_000, caps=caps, edit=_long_route_edit)
+
+
+def test_parity_actor_kernel_up_to_64_slots():
+    """k_actors<false, 1> (33-64 actor slots; up to 32 launch k_actors_g4): 2
+    lanes per actor for 17-32 vehicles, one lane per actor (the whole-route
+    search, actor_search<1>) beyond, and the long routes at 2 lanes per actor."""
+    caps = LY.Caps(128, 48, 288, 4)
+    many = dict(build_random_navigation_options(RandomNavigationReset(difficulty_id="rt_hard_v1")), num_vehicles=40)
+    run_parity(None, 6, 40, seed0=52_000, caps=caps, options=[many])
+    run_parity(["rt_hard_v1"], 12, 40, seed0=53_000, caps=caps)
+    run_parity(["rt_hard_v1"], 8, 30, seed0=61_000, caps=LY.Caps(128, 48, 640, 4), edit=_long_route_edit)
 
 
 def _sample_envs(n, k=160):
