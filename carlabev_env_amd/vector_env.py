@@ -262,6 +262,7 @@ class CarlaBEVVectorEnv:
         self.single_action_space.seed(seed)
         self.generator = scene_generator or SceneGenerator(self.cfg, self.cfg.map_name)
         self.builder = HostResetBuilder(self.cfg, self.classes, self.params, self.layout, self.generator)
+        self._ctx_id_off = self.layout.off["hi"] + 4 * LY.HI["CTX_ID"]  # byte offset of a record's CTX_ID
         self.reset_pool = reset_pool
         self.pool_builds = 0  # scenes reset() had the pool build
         self.scene_context = [dict() for _ in range(N)]
@@ -608,12 +609,24 @@ class CarlaBEVVectorEnv:
         # _flush_pending); this reset's replaced ones wait their turn
         while self._host_retired and self._host_retired[0][1] <= self._ep_step - EP_RING:
             self._ctx_table.pop(self._host_retired.popleft()[0], None)
+        key_of_seed = {}  # memo keys, once per distinct seed of this call
+
+        def key_of(i):
+            sd = seeds[i]
+            try:
+                k = key_of_seed.get(sd, key_of_seed)
+            except TypeError:  # an unhashable seed: its own key
+                return self.builder.memo_key(sd, options)
+            if k is key_of_seed:
+                k = key_of_seed[sd] = self.builder.memo_key(sd, options)
+            return k
+
         if self.reset_pool is not None and len(idx) > 1:
             # the distinct scenes not memoised yet, built by the pool's workers and
             # memoised here; the loop below then copies them
             todo = {}
             for i in idx.tolist():
-                key = self.builder.memo_key(seeds[i], options)
+                key = key_of(i)
                 if key is not None and key not in todo and self.builder.memo_get(key) is None:
                     todo[key] = i
             if len(todo) > 1:
@@ -621,8 +634,9 @@ class CarlaBEVVectorEnv:
                 for key, rec, (info, ctx) in zip(todo, recs, meta):
                     self.builder.memo_put(key, rec, info, None, ctx)
                 self.pool_builds += len(todo)
-        for k, i in enumerate(idx):
-            info, spec, ctx = self.builder.build(host[k], seeds[i], options)
+        ctx_ids = host[:, self._ctx_id_off:self._ctx_id_off + 4].view(np.int32)[:, 0] if len(idx) else None
+        for k, i in enumerate(idx.tolist()):
+            info, spec, ctx = self.builder.build(host[k], seeds[i], options, key_of(i))
             spawn_infos.append(info)
             self.scene_context[i] = ctx
             old = int(self._env_ctx[i])
@@ -630,7 +644,7 @@ class CarlaBEVVectorEnv:
                 self._host_retired.append((old, self._ep_step))
             cid = self._new_ctx_id(ctx)
             self._env_ctx[i] = cid
-            LY.RecordView(host[k], self.layout).hi[LY.HI["CTX_ID"]] = cid
+            ctx_ids[k] = cid  # the record's CTX_ID
         if len(idx):
             staging = torch.from_numpy(host[:len(idx)]).to(self.device)
             bank_idx = np.zeros(N, dtype=np.int32)
