@@ -996,8 +996,6 @@ __device__ __forceinline__ void hero_env_render_setup(const KArgs& K, DRec r) {
 // More than 64 actors: d_actor_step per lane.
 // calc_target_index of every live actor of one env (nact <= 64): AW lanes per
 // actor, 64 / AW actors per round; returns lane a's result for actor a
-// the float32 first pass (false: the float64 scan alone, tools/micro/actor_f64_only.patch)
-constexpr bool kActorF32 = true;
 // route points per lane loaded at once: 24 in the float32 pass (the lane-graph
 // routes of round 5 have 124 points at the median; 8: 47.7 us at config 3, 16:
 // 44.8, 24: 42.0, 32 spills the residency to 2 waves per SIMD), 8 in the rare
@@ -1034,7 +1032,7 @@ __device__ __forceinline__ int actor_search(const DRec& r, int nact, uint64_t li
     int i2 = 0x7fffffff;
     float f1 = INFINITY, f2 = INFINITY, f3 = INFINITY;
     int j1 = -1, j2 = -1;
-    if (glive && kActorF32) {
+    if (glive) {  // the float32 first pass (the float64 scan alone: tools/micro/actor_f64_only.patch)
       const float2* cf = (const float2*)r.acf + (int64_t)(aa & 63) * RA;
       const float ffx = (float)gfx, ffy = (float)gfy;
       for (int i0 = sub; i0 < gn; i0 += ACTOR_BATCH * AW) {
@@ -1073,7 +1071,7 @@ __device__ __forceinline__ int actor_search(const DRec& r, int nact, uint64_t li
       m2 = lt ? d2 : m2;
       i2 = lt ? i : i2;
     };
-    if (glive && (!kActorF32 || f3 <= thr)) {  // three or more candidates in this lane: the float64 scan
+    if (glive && f3 <= thr) {  // three or more candidates in this lane: the float64 scan
       for (int i0 = sub; i0 < gn; i0 += ACTOR_BATCH64 * AW) {
         double px[ACTOR_BATCH64], py[ACTOR_BATCH64];
 #pragma unroll
@@ -2259,15 +2257,11 @@ __device__ __forceinline__ uint32_t nonzero_bytes16(const uint4 v) {  // bit b: 
 }
 
 // the reset's copies: streamed stores (the next step's kernels read the records
-// from memory anyway: each kernel's start invalidates the L2)
-constexpr bool kResetStoreNT = true;
+// from memory anyway: each kernel's start invalidates the L2; round 6: 12.8 ->
+// 12.0 us at config 3 against plain stores)
 __device__ __forceinline__ void reset_store16(uint8_t* p, const uint4 v) {
-  if (kResetStoreNT) {
-    u32x4_nt w = {v.x, v.y, v.z, v.w};
-    __builtin_nontemporal_store(w, (u32x4_nt*)p);
-  } else {
-    *(uint4*)p = v;
-  }
+  u32x4_nt w = {v.x, v.y, v.z, v.w};
+  __builtin_nontemporal_store(w, (u32x4_nt*)p);
 }
 __device__ __forceinline__ int bank_row_of(int e, uint32_t j, uint32_t stride, int n_bank) {
   return (int)(((uint64_t)e + (uint64_t)j * stride) % (uint64_t)n_bank);
