@@ -110,3 +110,25 @@ def test_reset_build_memo_is_exact():
     assert c4["scene"] != "edited"
     b1.build(r2, 6, opts)  # another seed: built
     assert b1.builds == 2 and not np.array_equal(r1, r2)
+
+
+def test_memo_copies_are_deep_and_independent():
+    """The memo's plain-data copy (host_reset._copy_plain, in place of
+    copy.deepcopy) keeps values and types and shares nothing mutable; objects it
+    does not know go through copy.deepcopy."""
+    from carlabev_env_amd.host_reset import _copy_plain
+
+    class Box:
+        def __init__(self, v):
+            self.v = v
+
+    src = {"a": [1, 2.5, None, True, "s", np.int64(3)], "b": {"c": (np.arange(3), [4])}, "d": Box([7])}
+    out = _copy_plain(src)
+    assert out["a"] == src["a"] and type(out["a"][5]) is np.int64 and isinstance(out["b"]["c"], tuple)
+    assert np.array_equal(out["b"]["c"][0], src["b"]["c"][0])
+    out["a"].append(9)
+    out["b"]["c"][0][0] = 99
+    out["b"]["c"][1].append(5)
+    out["d"].v.append(8)
+    assert src["a"] == [1, 2.5, None, True, "s", 3] and src["b"]["c"][0][0] == 0
+    assert src["b"]["c"][1] == [4] and src["d"].v == [7]
