@@ -259,6 +259,28 @@ __device__ __forceinline__ double lane_value(double v, int k) {
 // lane ~50 k cycles, which the whole k_actors launch then waits for.
 // The record is only touched by this wave here, so workgroup-scope fences order
 // the lanes' global stores and loads (same CU); agent scope would also flush L2.
+// ---- butterfly reductions over the tpe lanes of an env (tpe a power of two,
+// groups aligned to tpe). Partner at level OFF: DPP inside a row of 16 lanes for
+// OFF = 1, 2 (quad_perm [1,0,3,2], [2,3,0,1]), 4 (row_half_mirror: lane l of a
+// group of 8 with 7 - l) and 8 (row_mirror: l with 15 - l) -- after levels 1 and
+// 2 every lane of a quad holds the quad's result and after 4 every lane of an 8,
+// so a mirror pairs complementary partials as an xor would -- then ds_bpermute
+// (__shfl_xor) across rows. The combines are commutative and associative
+// (minimum with a lowest-index tie-break), so the pairing order does not matter.
+// A DPP move is one VALU instruction; __shfl_xor is an LDS round trip each.
+template <int OFF>
+__device__ __forceinline__ int peer_i32(int v) {
+  if constexpr (OFF == 1) return __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xF, 0xF, false);
+  else if constexpr (OFF == 2) return __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xF, 0xF, false);
+  else if constexpr (OFF == 4) return __builtin_amdgcn_update_dpp(0, v, 0x141, 0xF, 0xF, false);
+  else if constexpr (OFF == 8) return __builtin_amdgcn_update_dpp(0, v, 0x140, 0xF, 0xF, false);
+  else return __shfl_xor(v, OFF, 64);
+}
+template <int OFF>
+__device__ __forceinline__ double peer_f64(double v) {
+  const int lo = peer_i32<OFF>(__double2loint(v)), hi = peer_i32<OFF>(__double2hiint(v));
+  return __hiloint2double(hi, lo);
+}
 __device__ __forceinline__ void wave_mem_fence() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup"); }
 
 // Takes the record base and the byte offsets of the groups it touches as plain
@@ -412,18 +434,25 @@ __device__ __noinline__ bool wave_start_retreat(uint8_t* base, int o_ad, int o_a
     const bool in = lane < nd;
     const double px = (double)(float)cxv, py = (double)(float)cyv;
     double x0 = in ? px : INFINITY, x1 = in ? px : -INFINITY, y0 = in ? py : INFINITY, y1 = in ? py : -INFINITY;
-#pragma unroll
-    for (int off = 1; off < 16; off <<= 1) {
-      x0 = fmin(x0, __shfl_xor(x0, off, 64));
-      x1 = fmax(x1, __shfl_xor(x1, off, 64));
-      y0 = fmin(y0, __shfl_xor(y0, off, 64));
-      y1 = fmax(y1, __shfl_xor(y1, off, 64));
-    }
+    // over each 16-lane block: DPP partners inside a row (peer_f64), not LDS round trips
+    auto mm = [&](auto off) {
+      constexpr int O = decltype(off)::value;
+      x0 = fmin(x0, peer_f64<O>(x0));
+      x1 = fmax(x1, peer_f64<O>(x1));
+      y0 = fmin(y0, peer_f64<O>(y0));
+      y1 = fmax(y1, peer_f64<O>(y1));
+    };
+    mm(std::integral_constant<int, 1>{});
+    mm(std::integral_constant<int, 2>{});
+    mm(std::integral_constant<int, 4>{});
+    mm(std::integral_constant<int, 8>{});
     const int qx = (int)fmin(fmax(rint((x0 + x1) * 0.5 * 8.0) + 32768.0, 0.0), 65535.0);
     const int qy = (int)fmin(fmax(rint((y0 + y1) * 0.5 * 8.0) + 32768.0, 0.0), 65535.0);
     double rr = in ? hypot(px - (qx - 32768) / 8.0, py - (qy - 32768) / 8.0) : 0.0;
-#pragma unroll
-    for (int off = 1; off < 16; off <<= 1) rr = fmax(rr, __shfl_xor(rr, off, 64));
+    rr = fmax(rr, peer_f64<1>(rr));
+    rr = fmax(rr, peer_f64<2>(rr));
+    rr = fmax(rr, peer_f64<4>(rr));
+    rr = fmax(rr, peer_f64<8>(rr));
     if ((lane & 15) == 0 && lane < nd) {
       uint2* cb = (uint2*)(base + o_acb) + (int64_t)a * ((RA + CBEV_ACB_PTS - 1) / CBEV_ACB_PTS) + (lane >> 4);
       *cb = make_uint2((uint32_t)qx | ((uint32_t)qy << 16), (uint32_t)ceil(rr * 8.0) + 1u);
@@ -2777,28 +2806,6 @@ __device__ __forceinline__ void collide_env(const KArgs& K, DRec r, int e, const
   CBEV_STAMP(4, 3);
 }
 
-// ---- butterfly reductions over the tpe lanes of an env (tpe a power of two,
-// groups aligned to tpe). Partner at level OFF: DPP inside a row of 16 lanes for
-// OFF = 1, 2 (quad_perm [1,0,3,2], [2,3,0,1]), 4 (row_half_mirror: lane l of a
-// group of 8 with 7 - l) and 8 (row_mirror: l with 15 - l) -- after levels 1 and
-// 2 every lane of a quad holds the quad's result and after 4 every lane of an 8,
-// so a mirror pairs complementary partials as an xor would -- then ds_bpermute
-// (__shfl_xor) across rows. The combines are commutative and associative
-// (minimum with a lowest-index tie-break), so the pairing order does not matter.
-// A DPP move is one VALU instruction; __shfl_xor is an LDS round trip each.
-template <int OFF>
-__device__ __forceinline__ int peer_i32(int v) {
-  if constexpr (OFF == 1) return __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xF, 0xF, false);
-  else if constexpr (OFF == 2) return __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xF, 0xF, false);
-  else if constexpr (OFF == 4) return __builtin_amdgcn_update_dpp(0, v, 0x141, 0xF, 0xF, false);
-  else if constexpr (OFF == 8) return __builtin_amdgcn_update_dpp(0, v, 0x140, 0xF, 0xF, false);
-  else return __shfl_xor(v, OFF, 64);
-}
-template <int OFF>
-__device__ __forceinline__ double peer_f64(double v) {
-  const int lo = peer_i32<OFF>(__double2loint(v)), hi = peer_i32<OFF>(__double2hiint(v));
-  return __hiloint2double(hi, lo);
-}
 // f(std::integral_constant<int, OFF>) for OFF = 1, 2, 4, ... < tpe (uniform tpe <= 64)
 template <class F>
 __device__ __forceinline__ void butterfly(int tpe, F&& f) {
