@@ -343,21 +343,18 @@ __device__ __noinline__ bool wave_start_retreat(uint8_t* base, int o_ad, int o_a
     const int i = lane;
     double accy = 0.0, accx = 0.0;
     // not unrolled: this callee's registers count against every k_actors wave
-    // (unrolled: 161 instead of 88 VGPRs, 3 instead of 5 waves per SIMD)
+    // (unrolled: k_actors_g4's callee spills 160 B per lane; config 5 k_actors
+    // 15.4 against 15.8 us, kept rolled) -- the lane's coefficient row and first
+    // sample up front, the next coefficient loaded one term ahead
+    const double* crow = i < h ? c_sg.left[ti][i] : (i >= nd - h ? c_sg.right[ti][i >= nd ? 0 : i - (nd - h)]
+                                                                  : c_sg.conv[ti]);
+    const int idx0 = i < h ? 0 : (i >= nd - h ? nd - w : i - h);
+    double cn = crow[0];
 #pragma unroll 1
     for (int j = 0; j < 11; ++j) {
-      int idx = 0;
-      double c = 0.0;
-      if (i < h) {
-        idx = j;
-        c = c_sg.left[ti][i][j];
-      } else if (i >= nd - h) {
-        idx = nd - w + j;
-        c = c_sg.right[ti][i >= nd ? 0 : i - (nd - h)][j];
-      } else {
-        idx = i - h + j;
-        c = c_sg.conv[ti][j];
-      }
+      const int idx = idx0 + j;
+      const double c = cn;
+      if (j + 1 < 11) cn = crow[j + 1];
       const double vy = __shfl(qy, idx & 63), vx = __shfl(qx, idx & 63);
       if (j < w) {  // the serial sum's terms, in its order
         accy += c * vy;
