@@ -1172,9 +1172,9 @@ __device__ __forceinline__ int actor_search(const DRec& r, int nact, uint64_t li
 constexpr int ACTOR_NB = 18;
 __host__ __device__ constexpr int actor_cq(int aw) { return (ACTOR_NB + aw - 1) / aw; }
 template <int AW>
-__device__ __forceinline__ int actor_search_win(const DRec& r, int nact, uint64_t livem, double fx, double fy,
+__device__ __forceinline__ int actor_search_win(const DRec& r, int a0, int nact, uint64_t livem, double fx, double fy,
                                                 int nrt, int tid0, int lane, double p0x, double p0y, double p1x,
-                                                double p1y) {
+                                                double p1y) {  // actors [a0, nact)
   constexpr int AG = 64 / AW;
   constexpr int BP = CBEV_ACB_PTS;
   constexpr int WPL = (2 * BP + AW - 1) / AW;  // window points per lane
@@ -1183,7 +1183,7 @@ __device__ __forceinline__ int actor_search_win(const DRec& r, int nact, uint64_
   const int RA = r.RA, NBC = (RA + BP - 1) / BP;
   const int g = lane / AW, sub = lane - g * AW;
   int best = 0;
-  for (int r0 = 0; r0 < nact; r0 += AG) {
+  for (int r0 = a0; r0 < nact; r0 += AG) {
     const int aa = r0 + g;  // this group's actor
     const double gfx = __shfl(fx, aa & 63), gfy = __shfl(fy, aa & 63);
     const int gn = __shfl(nrt, aa & 63), gt0 = __shfl(tid0, aa & 63);
@@ -1442,14 +1442,27 @@ __device__ __forceinline__ void actors_body(KArgs K, uint8_t* __restrict__ recs,
                                                                                     : nact <= 32 ? 2 : 1);
   int best;
   switch (aw) {
-    case 64: best = actor_search_win<64>(r, nact, livem, fx, fy, nrt, tid0, lane, pcx[0], pcy[0], pcx[1], pcy[1]); break;
-    case 32: best = actor_search_win<32>(r, nact, livem, fx, fy, nrt, tid0, lane, pcx[0], pcy[0], pcx[1], pcy[1]); break;
-    case 16: best = actor_search_win<16>(r, nact, livem, fx, fy, nrt, tid0, lane, pcx[0], pcy[0], pcx[1], pcy[1]); break;
-    case 8: best = actor_search_win<8>(r, nact, livem, fx, fy, nrt, tid0, lane, pcx[0], pcy[0], pcx[1], pcy[1]); break;
-    case 4: best = actor_search_win<4>(r, nact, livem, fx, fy, nrt, tid0, lane, pcx[0], pcy[0], pcx[1], pcy[1]); break;
+    case 64: best = actor_search_win<64>(r, 0, nact, livem, fx, fy, nrt, tid0, lane, pcx[0], pcy[0], pcx[1], pcy[1]); break;
+    case 32: best = actor_search_win<32>(r, 0, nact, livem, fx, fy, nrt, tid0, lane, pcx[0], pcy[0], pcx[1], pcy[1]); break;
+    case 16: best = actor_search_win<16>(r, 0, nact, livem, fx, fy, nrt, tid0, lane, pcx[0], pcy[0], pcx[1], pcy[1]); break;
+    case 8: best = actor_search_win<8>(r, 0, nact, livem, fx, fy, nrt, tid0, lane, pcx[0], pcy[0], pcx[1], pcy[1]); break;
+    case 4:
+      if (nact > 16) {
+        // 17-32 actors: the first 16 at 4 lanes each, the rest in one more pass
+        // as wide as they allow (up to 8 actors: 8 lanes each, half the window
+        // points per lane of a second 4-lane pass)
+        const int b1 = actor_search_win<4>(r, 0, 16, livem, fx, fy, nrt, tid0, lane, pcx[0], pcy[0], pcx[1], pcy[1]);
+        const int b2 = nact <= 24
+                           ? actor_search_win<8>(r, 16, nact, livem, fx, fy, nrt, tid0, lane, pcx[0], pcy[0], pcx[1], pcy[1])
+                           : actor_search_win<4>(r, 16, nact, livem, fx, fy, nrt, tid0, lane, pcx[0], pcy[0], pcx[1], pcy[1]);
+        best = lane < 16 ? b1 : b2;
+      } else {
+        best = actor_search_win<4>(r, 0, nact, livem, fx, fy, nrt, tid0, lane, pcx[0], pcy[0], pcx[1], pcy[1]);
+      }
+      break;
     case 2:
       if (MINAW <= 2) {
-        best = actor_search_win<2>(r, nact, livem, fx, fy, nrt, tid0, lane, pcx[0], pcy[0], pcx[1], pcy[1]);
+        best = actor_search_win<2>(r, 0, nact, livem, fx, fy, nrt, tid0, lane, pcx[0], pcy[0], pcx[1], pcy[1]);
         break;
       }
       [[fallthrough]];
